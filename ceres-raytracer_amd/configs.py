@@ -1,0 +1,86 @@
+"""Named scene/camera configurations (SURVEY.md §8(d) C1-C5 plus parity edge cases).
+
+Every entry is the explicit input set of one render: the mesh, the `--rotate` applied by
+`rotate_triangles` (render.hpp:24-44), the `Camera` (render.hpp:16-22), the sun position and
+the framebuffer size.  Defaults of the single-frame app are static.cpp:39-47,72-73.
+
+`mode` is "full" (primary + shadow + smooth shading, render.hpp:104-153) or "primary"
+(primary rays only; pixel = |normalize(tri.n)|, the normal visualisation left commented
+out at render.hpp:123-125 -- the C2 "primary rays only" configuration).
+"""
+import os
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DATA = os.path.join(REPO, "data")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+# static.cpp:39-47 camera + sun + rotation (dragon); README.md:11 eye/rotate for the bunny,
+# with dir/up chosen so the bunny is in view.
+_DRAGON = dict(obj="dragon.obj", eye=(0.0, -15.0, 2.0), dir=(0.0, 1.0, 0.0), up=(0.0, 0.0, 1.0),
+               fov=60.0, sun=(-50.0, -20.0, 0.0), rotate=("x", 90.0))
+_BUNNY = dict(obj="bunny.obj", eye=(0.0, 0.1, -0.3), dir=(0.0, 0.0, 1.0), up=(0.0, 1.0, 0.0),
+              fov=60.0, sun=(-50.0, -20.0, 0.0), rotate=("y", -145.0))
+# C5 procedural heightfield (no reference generator exists; SURVEY.md §8(d) C5 definition).
+_PROC = dict(obj=None, eye=(0.5, -0.4, 0.6), dir=(0.0, 0.9, -0.55), up=(0.0, 0.0, 1.0),
+             fov=60.0, sun=(-50.0, -20.0, 100.0), rotate=None)
+_TINY = dict(eye=(0.2, 0.2, -3.0), dir=(0.0, 0.0, 1.0), up=(0.0, 1.0, 0.0), fov=60.0,
+             sun=(-50.0, -20.0, 0.0), rotate=None)
+
+
+def _cfg(base, **kw):
+    d = dict(base)
+    d.update(kw)
+    d.setdefault("mode", "full")
+    d.setdefault("proc", 0)
+    return d
+
+
+CONFIGS = {
+    # C1: bunny 640x480 (CPU plumbing config of BASELINE.json configs[0])
+    "bunny_640": _cfg(_BUNNY, W=640, H=480),
+    # C2: bunny 1920x1080 primary rays only
+    "bunny_1080_primary": _cfg(_BUNNY, W=1920, H=1080, mode="primary"),
+    "bunny_1080": _cfg(_BUNNY, W=1920, H=1080),
+    # C3: dragon 1920x1080 primary+shadow -- the BASELINE.json headline metric config
+    "dragon_1080": _cfg(_DRAGON, W=1920, H=1080),
+    "dragon_640": _cfg(_DRAGON, W=640, H=480),
+    # C4: dragon 4096x4096
+    "dragon_4096": _cfg(_DRAGON, W=4096, H=4096),
+    # ragged sizes (not multiples of any tile), single pixel
+    "dragon_333x217": _cfg(_DRAGON, W=333, H=217),
+    "bunny_97x61_primary": _cfg(_BUNNY, W=97, H=61, mode="primary"),
+    "bunny_1x1": _cfg(_BUNNY, W=1, H=1),
+    # procedural heightfield, small (101x101 vertices = 20,000 tris) and C5 (2237^2 = 9,999,392 tris)
+    "proc_101": _cfg(_PROC, proc=101, W=320, H=240),
+    "proc_c5": _cfg(_PROC, proc=2237, W=3840, H=2160),
+    # tiny hand-written meshes: root-is-leaf, fan triangulation / negative indices / v/vt/vn, degenerate tris
+    "tri1": _cfg(_TINY, obj="@golden/tri1.obj", W=64, H=48),
+    "quad": _cfg(_TINY, obj="@golden/quad.obj", W=64, H=48),
+    "degenerate": _cfg(_TINY, obj="@golden/degenerate.obj", W=64, H=48),
+}
+
+
+def obj_path(cfg):
+    """Absolute path of a config's mesh (None for procedural meshes)."""
+    o = cfg["obj"]
+    if o is None:
+        return None
+    if o.startswith("@golden/"):
+        return os.path.join(GOLDEN, o[len("@golden/"):])
+    return os.path.join(DATA, o)
+
+
+def cli_args(cfg):
+    """The `./render` CLI flags (README.md:11 style) describing a config."""
+    a = []
+    if cfg["proc"]:
+        a += ["--proc", str(cfg["proc"])]
+    else:
+        a += [obj_path(cfg)]
+    a += ["--eye", *map(repr, cfg["eye"]), "--dir", *map(repr, cfg["dir"]), "--up", *map(repr, cfg["up"]),
+          "--fov", repr(cfg["fov"]), "--sun", *map(repr, cfg["sun"]), "--size", str(cfg["W"]), str(cfg["H"])]
+    if cfg["rotate"]:
+        a += ["--rotate", cfg["rotate"][0], repr(cfg["rotate"][1])]
+    if cfg["mode"] == "primary":
+        a += ["--primary-only"]
+    return a
