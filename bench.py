@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s of the CERES hot path on MI355X (BASELINE.json metric).
+
+Workload (default): C3 = dragon.obj 1920x1080, primary + shadow rays, static.cpp camera
+(static.cpp:38-47,72-73) -- the configuration BASELINE.json's metric is quoted on.  A step
+is one frame: ceres_primary + ceres_shadow over the rank's rows, RGB8 + float framebuffer
+written in HBM, and for N > 1 the RCCL gather of the RGB8 rows to rank 0 (one collective per
+frame).  Scene upload, OBJ load and BVH build are outside the timed region, as in the
+reference (static.cpp:129-133).  value = (primary + shadow rays of the whole frame) x steps
+/ wall time (max over ranks).  One process per GPU (torch.distributed, backend nccl = RCCL).
+
+Also reported (rank 0):
+  roofline      dominant kernel's algorithmic bytes per launch (pinned reference statistics,
+                SURVEY.md §8(d): 64 B per node-pair visit + 56 B per triangle test) / its mean
+                device duration from HIP events on the launch stream, vs 8 TB/s HBM peak;
+                traffic = rocprofv3 --pmc FETCH_SIZE (gfx950 x2 correction) per launch from
+                profiles/, when a profile of this workload is committed.
+  cpu_baseline  the REFERENCE hot path (oracle/_ref/ref_render, reference CMake flags) timed
+                on this host's cores on a bounded sample of the same workload (N = 1 only);
+                falls back to the oracle restatement if the reference binary is absent.
+  parity        sha256 of the rendered PPM vs the reference fixture.
+"""
+import argparse
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(REPO, "ceres-raytracer_amd")
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def import_package():
+    import importlib.util
+    if "ceres_raytracer_amd" in sys.modules:
+        return sys.modules["ceres_raytracer_amd"]
+    spec = importlib.util.spec_from_file_location("ceres_raytracer_amd", os.path.join(PKG_DIR, "__init__.py"),
+                                                  submodule_search_locations=[PKG_DIR])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["ceres_raytracer_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_golden(name):
+    p = os.path.join(REPO, "tests", "golden", name + ".json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def pinned_basis(meta, cfg, cam):
+    if meta is None:
+        return cam.basis(cfg["W"], cfg["H"])
+    bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
+    return np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
+
+
+def cpu_baseline(cfg_name, cfg, rays_per_frame, budget_s=3.0):
+    """Reference CPU path on this host, bounded sample of the same workload (rank 0, N = 1)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import configs
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_render")
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    if os.access(ref, os.X_OK):
+        try:
+            args = [ref] + configs.cli_args(cfg)
+            probe = json.loads(subprocess.run(args + ["--reps", "2"], capture_output=True, text=True, check=True,
+                                              env=env, timeout=300).stdout.strip().splitlines()[-1])
+            reps = int(max(3, min(200, budget_s * 1e3 / max(probe["render_ms_best"], 1e-3))))
+            out = json.loads(subprocess.run(args + ["--reps", str(reps)], capture_output=True, text=True, check=True,
+                                            env=env, timeout=600).stdout.strip().splitlines()[-1])
+            ms = out["render_ms_median"]
+            return {"value": round(out["rays"] / (ms * 1e3), 3), "unit": "Mrays/s", "cores": threads,
+                    "kind": "reference",
+                    "sample": f"{cfg_name}: {reps} full frames of reference render() (render.hpp:87, "
+                              f"-O3 -mavx2 -mfma -fopenmp), median {ms:.2f} ms/frame, {out['rays']} rays/frame",
+                    "cpu_model": _cpu_model()}
+        except Exception as e:  # noqa: BLE001 -- fall through to the port
+            sys.stderr.write(f"reference CPU baseline failed ({e}); timing the oracle port\n")
+    import oracle
+    sc = oracle.prepare(cfg)
+    oracle.render(sc, cfg, want_pixels=True, want_ppm=False, threads=threads)
+    times = []
+    t_end = time.time() + budget_s
+    while time.time() < t_end or len(times) < 3:
+        t0 = time.perf_counter()
+        oracle.render(sc, cfg, want_pixels=True, want_ppm=False, threads=threads)
+        times.append(time.perf_counter() - t0)
+    ms = float(np.median(times)) * 1e3
+    return {"value": round(rays_per_frame / (ms * 1e3), 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{cfg_name}: {len(times)} full frames of oracle/liboracle.so, median {ms:.2f} ms/frame",
+            "cpu_model": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_traffic(cfg_name, kernel):
+    """Per-launch HBM bytes of `kernel` from a committed rocprofv3 --pmc summary, or None."""
+    p = os.path.join(REPO, "profiles", "pmc_summary.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        e = d.get(cfg_name, {}).get(kernel)
+        return None if e is None else e.get("hbm_bytes_per_launch")
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="dragon_1080")
+    ap.add_argument("--row-block", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    pkg = import_package()
+    import ceres_raytracer_amd.distributed as D
+    cfg = pkg.configs.CONFIGS[args.config]
+    meta = load_golden(args.config)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.stderr.write("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)\n")
+            return 2
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    W, H = cfg["W"], cfg["H"]
+    mesh, bvh, cam = pkg.prepare(cfg)
+    scene = pkg.Scene(mesh, bvh, device=local_rank)
+    basis = pinned_basis(meta, cfg, cam)
+    mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
+    tiling = pkg.Tiling(args.row_block if world > 1 else H, rank, world)
+    gather = D.FrameGather(W, H, tiling.row_block, rank, world, device=dev)
+    rows = gather.local_rows
+    d_px = None if args.no_float else torch.empty(3 * W * max(rows, 1), dtype=torch.float32, device=dev)
+    counters = torch.zeros(8, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(with_counters=False):
+        scene.render_device(basis, cfg["sun"], W, H, mode=mode, tiling=tiling,
+                            d_pixels=0 if d_px is None else d_px.data_ptr(), d_rgb8=gather.local_ptr(),
+                            d_counters=counters.data_ptr() if with_counters else 0, stream=sh)
+        return gather.gather()
+
+    # validation frame: counts (exact) + PPM parity on rank 0
+    full = step(with_counters=True)
+    torch.cuda.synchronize(dev)
+    c = counters.clone()
+    if world > 1:
+        dist.all_reduce(c)
+    c = c.cpu().numpy()
+    rays_frame, hits_frame = int(c[0]), int(c[1])
+    parity = None
+    if rank == 0:
+        body = b"P6 %d %d 255\n" % (W, H) + full.cpu().numpy().tobytes()
+        sha = hashlib.sha256(body).hexdigest()
+        if meta is not None:
+            parity = {"ppm_sha256_matches_reference": sha == meta["ppm_sha256"]["exact"],
+                      "rays_match": rays_frame == meta["exact"]["rays"], "hits_match": hits_frame == meta["exact"]["hits"]}
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    T = float(elapsed.item())
+    value = rays_frame * args.steps / T / 1e6
+
+    roofline = None
+    cpu = None
+    if rank == 0 and not args.no_roofline and meta is not None:
+        # dominant kernel, timed live with HIP events on the launch stream (full frame, this GPU)
+        solo = pkg.Tiling(H, 0, 1)
+        solo_rgb = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
+        solo_px = torch.empty(3 * W * H, dtype=torch.float32, device=dev)
+        scene.set_timing(True)
+        n_t = max(10, min(args.steps, 200))
+        for _ in range(n_t):
+            scene.render_device(basis, cfg["sun"], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
+                                d_rgb8=solo_rgb.data_ptr(), stream=sh)
+        p_ms, s_ms, n = scene.read_timing()
+        scene.set_timing(False)
+        ex = meta["exact"]
+        kern = {"ceres_primary": (p_ms / n, 64 * ex["primary_pairs"] + 56 * ex["primary_tests"]),
+                "ceres_shadow": (s_ms / n, 64 * ex["shadow_pairs"] + 56 * ex["shadow_tests"])}
+        name = max(kern, key=lambda k: kern[k][0])
+        ms, nbytes = kern[name]
+        achieved = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": pmc_traffic(args.config, name),
+                    "algorithmic_bytes_per_launch": nbytes, "mean_launch_ms": round(ms, 5),
+                    "kernels_ms": {k: round(v[0], 5) for k, v in kern.items()},
+                    "frame_algorithmic_bytes": kern["ceres_primary"][1] + kern["ceres_shadow"][1],
+                    "frame_frac": round((kern["ceres_primary"][1] + kern["ceres_shadow"][1]) /
+                                        ((p_ms + s_ms) / n * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.config, cfg, rays_frame)
+
+    if rank == 0:
+        line = {
+            "metric": "Mrays/sec (primary+shadow) on dragon.obj 1920x1080; 1/2/4/8-GPU scaling"
+            if args.config == "dragon_1080" else f"Mrays/sec ({args.config})",
+            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(T / args.steps * 1e3, 5), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "real mesh from the reference repo (data/%s), static camera" % (cfg["obj"] or "procedural"),
+            "config": {"workload": f"{args.config}: {cfg['obj'] or 'proc'} {W}x{H} "
+                                   f"{'primary+shadow' if mode == pkg.MODE_FULL else 'primary only'}",
+                       "W": W, "H": H, "rays_per_frame": rays_frame, "hits_per_frame": hits_frame,
+                       "row_block": tiling.row_block, "parallelism": f"row-interleaved framebuffer x{world}"
+                       + (" + RCCL gather to rank 0" if world > 1 else ""),
+                       "float_framebuffer": d_px is not None},
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    scene.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

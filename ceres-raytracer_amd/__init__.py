@@ -1,0 +1,307 @@
+"""ceres_raytracer_amd -- MI355X-native CERES hot path, Python host mirror over the C ABI.
+
+This module mirrors the reference's render interface (include/render.hpp of
+iracigt/ceres-raytracer) for Python callers, tests and bench.py:
+
+    Camera(eye, dir, up, fov)                 render.hpp:16-22
+    load_obj(path) -> Mesh                    obj_norms.hpp:120-127 (triangles + tri_norms)
+    rotate_triangles(mesh, axis, degrees)     render.hpp:24-44
+    build_bvh(mesh) -> Bvh                    binned_sah_builder.hpp:39-234 (static.cpp:100-107)
+    Scene(mesh, bvh, device)                  the (bvh, triangles, tri_norms) arguments, on the GPU
+    render(camera, sun, scene, W, H) -> (pixels, rays, hits)   render.hpp:86-156
+
+Everything runs through libceres_hip.so (include/ceres_render.h): host scene preparation in
+C++, the hot path in hand-written gfx950 HIP kernels.  There is no CPU fallback: rendering
+without the library or without a gfx950 device raises CeresError.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libceres_hip.so")
+CLI_PATH = os.path.join(_PKG, "render")
+
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
+import configs  # noqa: E402,F401  (re-exported)
+
+MODE_FULL, MODE_PRIMARY = 0, 1
+SCENE_STATS = 1
+
+EXPORTED_SYMBOLS = (
+    "ceres_obj_load", "ceres_proc_mesh", "ceres_rotate_triangles", "ceres_bvh_build", "ceres_camera_basis",
+    "ceres_free", "ceres_scene_create", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
+    "ceres_render_device", "ceres_render_records", "ceres_tiling_local_rows", "ceres_scene_set_timing", "ceres_scene_read_timing",
+    "ceres_kernel_names", "ceres_last_error", "ceres_version",
+)
+
+
+class CeresError(RuntimeError):
+    pass
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("rays", ctypes.c_uint64), ("hits", ctypes.c_uint64), ("primary_rays", ctypes.c_uint64),
+                ("shadow_rays", ctypes.c_uint64), ("node_pairs", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64),
+                ("ms", ctypes.c_double)]
+
+
+class Tiling(ctypes.Structure):
+    _fields_ = [("row_block", ctypes.c_uint32), ("rank", ctypes.c_uint32), ("world", ctypes.c_uint32)]
+
+
+_lib = None
+_fp = ctypes.POINTER(ctypes.c_float)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_sz = ctypes.c_size_t
+_vp = ctypes.c_void_p
+
+
+def build(verbose=False):
+    """Compile libceres_hip.so and ./render for gfx950 (hipcc), in-tree."""
+    import subprocess
+    r = subprocess.run(["make", "-C", os.path.join(_PKG, "csrc"), "-j4", "all"], capture_output=True, text=True)
+    if verbose or r.returncode:
+        sys.stdout.write(r.stdout)
+        sys.stderr.write(r.stderr)
+    if r.returncode:
+        raise CeresError("build of libceres_hip.so failed")
+
+
+def lib():
+    """Load libceres_hip.so (import torch first when present so one HIP runtime is shared)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CeresError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+    if "torch" not in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+    L = ctypes.CDLL(LIB_PATH)
+    L.ceres_last_error.restype = ctypes.c_char_p
+    L.ceres_version.restype = ctypes.c_char_p
+    L.ceres_kernel_names.restype = ctypes.c_char_p
+    L.ceres_obj_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz)]
+    L.ceres_proc_mesh.argtypes = [ctypes.c_int, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz)]
+    L.ceres_rotate_triangles.argtypes = [_fp, _sz, ctypes.c_int, ctypes.c_float]
+    L.ceres_bvh_build.argtypes = [_fp, _sz, ctypes.POINTER(_u32p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p)]
+    L.ceres_camera_basis.argtypes = [_fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp]
+    L.ceres_free.argtypes = [_vp]
+    L.ceres_free.restype = None
+    L.ceres_scene_create.argtypes = [_fp, _sz, _fp, _vp, _sz, _u64p, ctypes.c_int, ctypes.c_uint32]
+    L.ceres_scene_create.restype = _vp
+    L.ceres_scene_destroy.argtypes = [_vp]
+    L.ceres_scene_destroy.restype = None
+    L.ceres_scene_info.argtypes = [_vp, _u32p, _u32p, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]
+    L.ceres_render_f32.argtypes = [_vp, _fp, _fp, ctypes.c_int, _fp, ctypes.POINTER(ctypes.c_uint8), _sz, _sz,
+                                   ctypes.POINTER(_Stats)]
+    L.ceres_render_device.argtypes = [_vp, _fp, _fp, ctypes.c_int, _sz, _sz, ctypes.POINTER(Tiling), _vp, _vp, _vp, _vp]
+    L.ceres_render_records.argtypes = [_vp, _fp, _fp, ctypes.c_int, _sz, _sz, ctypes.POINTER(ctypes.c_int32), _fp,
+                                       ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(_Stats)]
+    L.ceres_tiling_local_rows.argtypes = [_sz, ctypes.POINTER(Tiling)]
+    L.ceres_tiling_local_rows.restype = _sz
+    L.ceres_scene_set_timing.argtypes = [_vp, ctypes.c_int]
+    L.ceres_scene_read_timing.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                          _u64p]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise CeresError(f"ceres error {rc}: {lib().ceres_last_error().decode()}")
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def _take(ptr, count, dtype):
+    if count == 0:
+        lib().ceres_free(ctypes.cast(ptr, _vp))
+        return np.zeros(0, dtype)
+    a = np.ctypeslib.as_array(ptr, shape=(count,)).copy().view(dtype)
+    lib().ceres_free(ctypes.cast(ptr, _vp))
+    return a
+
+
+class Camera:
+    """render.hpp:16-22 -- eye, dir, up, fov (degrees)."""
+
+    def __init__(self, eye, dir, up, fov):
+        self.eye = np.asarray(eye, np.float32)
+        self.dir = np.asarray(dir, np.float32)
+        self.up = np.asarray(up, np.float32)
+        self.fov = float(fov)
+
+    def basis(self, W, H):
+        """render.hpp:91-97 on the host (libm stays on the host): {eye, dir, image_u, image_v}."""
+        out = np.zeros(9, np.float32)
+        _check(lib().ceres_camera_basis(_p(self.eye, ctypes.c_float), _p(self.dir, ctypes.c_float),
+                                        _p(self.up, ctypes.c_float), self.fov, W, H, _p(out, ctypes.c_float)))
+        return np.concatenate([self.eye, out]).astype(np.float32)
+
+
+class Mesh:
+    """Triangles (n x 12 f32 = bvh::Triangle<float>) and per-triangle vertex normals (n x 9)."""
+
+    def __init__(self, tri, norm):
+        self.tri = np.ascontiguousarray(tri, np.float32).reshape(-1, 12)
+        self.norm = np.ascontiguousarray(norm, np.float32).reshape(-1, 9)
+
+    def __len__(self):
+        return self.tri.shape[0]
+
+
+class Bvh:
+    """bvh::Bvh<float>: nodes (m x 8 u32 = Node) and primitive_indices (u64)."""
+
+    def __init__(self, nodes, prim):
+        self.nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
+        self.prim = np.ascontiguousarray(prim, np.uint64)
+
+
+def load_obj(path):
+    t, n, cnt = _fp(), _fp(), _sz()
+    _check(lib().ceres_obj_load(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt)))
+    c = cnt.value
+    return Mesh(_take(t, c * 12, np.float32).reshape(c, 12), _take(n, c * 9, np.float32).reshape(c, 9))
+
+
+def proc_mesh(n):
+    t, nn, cnt = _fp(), _fp(), _sz()
+    _check(lib().ceres_proc_mesh(int(n), ctypes.byref(t), ctypes.byref(nn), ctypes.byref(cnt)))
+    c = cnt.value
+    return Mesh(_take(t, c * 12, np.float32).reshape(c, 12), _take(nn, c * 9, np.float32).reshape(c, 9))
+
+
+def rotate_triangles(mesh, axis, degrees):
+    ax = {"x": 0, "y": 1, "z": 2}[axis] if isinstance(axis, str) else int(axis)
+    _check(lib().ceres_rotate_triangles(_p(mesh.tri, ctypes.c_float), len(mesh), ax, float(degrees)))
+    return mesh
+
+
+def build_bvh(mesh):
+    nodes, prim, m = _u32p(), _u64p(), _sz()
+    _check(lib().ceres_bvh_build(_p(mesh.tri, ctypes.c_float), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
+                                 ctypes.byref(prim)))
+    return Bvh(_take(nodes, m.value * 8, np.uint32).reshape(-1, 8), _take(prim, len(mesh), np.uint64))
+
+
+class Scene:
+    """A scene resident in HBM of one device (ceres_scene_create)."""
+
+    def __init__(self, mesh, bvh, device=0, stats=False):
+        L = lib()
+        self._h = L.ceres_scene_create(_p(mesh.tri, ctypes.c_float), len(mesh), _p(mesh.norm, ctypes.c_float),
+                                       bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0],
+                                       _p(bvh.prim, ctypes.c_uint64), int(device), SCENE_STATS if stats else 0)
+        if not self._h:
+            raise CeresError("ceres_scene_create: " + L.ceres_last_error().decode())
+        self.device = device
+        self.n_tri = len(mesh)
+
+    def info(self):
+        d, s, n, b = ctypes.c_uint32(), ctypes.c_uint32(), _sz(), _sz()
+        _check(lib().ceres_scene_info(self._h, ctypes.byref(d), ctypes.byref(s), ctypes.byref(n), ctypes.byref(b)))
+        return dict(depth=d.value, stack_entries=s.value, n_pairs=n.value, device_bytes=b.value)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ceres_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render(self, basis12, sun, W, H, mode=MODE_FULL, want_pixels=True, want_rgb8=True):
+        """ceres_render_f32: host buffers out; returns (pixels [H*W*3] f32 | None, rgb8 | None, stats dict)."""
+        b = np.ascontiguousarray(basis12, np.float32)
+        s = np.ascontiguousarray(sun, np.float32)
+        px = np.empty(3 * W * H, np.float32) if want_pixels else None
+        rgb = np.empty(3 * W * H, np.uint8) if want_rgb8 else None
+        st = _Stats()
+        _check(lib().ceres_render_f32(self._h, _p(b, ctypes.c_float), _p(s, ctypes.c_float), int(mode),
+                                      _p(px, ctypes.c_float), _p(rgb, ctypes.c_uint8), W, H, ctypes.byref(st)))
+        return px, rgb, dict(rays=st.rays, hits=st.hits, primary_rays=st.primary_rays, shadow_rays=st.shadow_rays,
+                             node_pairs=st.node_pairs, tri_tests=st.tri_tests, ms=st.ms)
+
+    def records(self, basis12, sun, W, H, mode=MODE_FULL):
+        """ceres_render_records: per-pixel (prim [W*H] i32, tuv [W*H,3] f32, shadow [W*H] i8, stats)."""
+        b = np.ascontiguousarray(basis12, np.float32)
+        s = np.ascontiguousarray(sun, np.float32)
+        prim = np.empty(W * H, np.int32)
+        tuv = np.empty(3 * W * H, np.float32)
+        sh = np.empty(W * H, np.int8)
+        st = _Stats()
+        _check(lib().ceres_render_records(self._h, _p(b, ctypes.c_float), _p(s, ctypes.c_float), int(mode), W, H,
+                                          _p(prim, ctypes.c_int32), _p(tuv, ctypes.c_float), _p(sh, ctypes.c_int8),
+                                          ctypes.byref(st)))
+        return prim, tuv.reshape(-1, 3), sh, dict(rays=st.rays, hits=st.hits, node_pairs=st.node_pairs,
+                                                  tri_tests=st.tri_tests)
+
+    def render_device(self, basis12, sun, W, H, mode=MODE_FULL, tiling=None, d_pixels=0, d_rgb8=0, d_counters=0,
+                      stream=0):
+        """ceres_render_device: device pointers (ints, e.g. torch data_ptr()), async on `stream`."""
+        b = np.ascontiguousarray(basis12, np.float32)
+        s = np.ascontiguousarray(sun, np.float32)
+        t = ctypes.byref(tiling) if tiling is not None else None
+        _check(lib().ceres_render_device(self._h, _p(b, ctypes.c_float), _p(s, ctypes.c_float), int(mode), W, H, t,
+                                         d_pixels or None, d_rgb8 or None, d_counters or None, stream or None))
+
+    def set_timing(self, on):
+        _check(lib().ceres_scene_set_timing(self._h, 1 if on else 0))
+
+    def read_timing(self):
+        p, q, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        _check(lib().ceres_scene_read_timing(self._h, ctypes.byref(p), ctypes.byref(q), ctypes.byref(n)))
+        return p.value, q.value, n.value
+
+
+def local_rows(H, tiling):
+    return lib().ceres_tiling_local_rows(H, ctypes.byref(tiling))
+
+
+def row_map(H, row_block, world):
+    """For each rank, the global rows j of its local rows k (ceres_tiling)."""
+    out = []
+    nb = (H + row_block - 1) // row_block
+    for r in range(world):
+        rows = []
+        for b in range(r, nb, world):
+            rows.extend(range(b * row_block, min(H, (b + 1) * row_block)))
+        out.append(np.asarray(rows, np.int64))
+    return out
+
+
+def prepare(cfg):
+    """Scene prep of the reference app for a config (configs.CONFIGS entry): mesh, bvh, camera."""
+    mesh = proc_mesh(cfg["proc"]) if cfg.get("proc") else load_obj(configs.obj_path(cfg))
+    if len(mesh) == 0:
+        raise CeresError("The given scene is empty or cannot be loaded")
+    if cfg.get("rotate"):
+        rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1])
+    bvh = build_bvh(mesh)
+    cam = Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    return mesh, bvh, cam
+
+
+def render(camera, sun, scene, W, H, mode=MODE_FULL):
+    """render<float>() (render.hpp:86-156): returns (pixels [3*W*H] f32, rays, hits)."""
+    px, _, st = scene.render(camera.basis(W, H), sun, W, H, mode=mode, want_rgb8=False)
+    return px, st["rays"], st["hits"]
+
+
+def ppm(W, H, rgb8):
+    """P6 file bytes exactly as static.cpp:135-147 writes them."""
+    return b"P6 %d %d 255\n" % (W, H) + np.asarray(rgb8, np.uint8).tobytes()

@@ -1,0 +1,85 @@
+// ceres_types.hpp -- data layouts shared by the host scene code and the gfx950 kernels.
+//
+// HBM layout of a device scene (DESIGN.md "Data layout in HBM"):
+//
+//   pairs[]  64-B SiblingPair records, one per inner node of the reference BVH, holding
+//            BOTH children's boxes and links.  The reference traverser always tests the two
+//            children of a node together (single_ray_traverser.hpp:85-87) and the reference
+//            keeps siblings adjacent (bvh.hpp:9-13, 32 B each), so one traversal step is
+//            exactly one 64-B record = four 16-B loads per lane, 64-B aligned (the reference
+//            pairs start at odd node indices, i.e. straddle 64-B boundaries).  Records are
+//            numbered in depth-first order of the reference topology.
+//   tris[]   48-B triangles {p0, e1, e2, n} (triangle.hpp:17-37) permuted into leaf order,
+//            so a leaf is a contiguous run: the reference's per-test u64 index gather
+//            (primitive_intersectors.hpp:17-20) disappears from the traversal loop.
+//   orig[]   u32 original triangle index per leaf slot (read once per primary hit).
+//   norms[]  36-B per-triangle vertex normals in ORIGINAL order (obj_norms.hpp:113-115),
+//            read only for lit pixels.
+#pragma once
+#include <cstdint>
+
+namespace ceres {
+
+struct Tri48 {                 // == bvh::Triangle<float>
+    float p0[3], e1[3], e2[3], n[3];
+};
+static_assert(sizeof(Tri48) == 48, "Tri48");
+
+struct RefNode {               // == bvh::Bvh<float>::Node (bvh.hpp:25-30)
+    float bounds[6];           // xmin, xmax, ymin, ymax, zmin, zmax
+    uint32_t primitive_count;  // 0 = inner node
+    uint32_t first_child_or_primitive;
+};
+static_assert(sizeof(RefNode) == 32, "RefNode");
+
+struct alignas(16) SiblingPair {
+    float lb[6];               // left child bounds  (reference order xmin,xmax,ymin,ymax,zmin,zmax)
+    float rb[6];               // right child bounds
+    uint32_t lcount, lfirst;   // count 0: inner, first = pair index of its children;
+    uint32_t rcount, rfirst;   // count > 0: leaf, first = first leaf slot in tris[]
+};
+static_assert(sizeof(SiblingPair) == 64, "SiblingPair");
+
+struct ShadowJob {             // one queued shadow ray (render.hpp:127-136), 32 B
+    uint32_t pixel;            // local pixel index = local_row * W + i
+    uint32_t slot;             // leaf slot of the primary hit
+    float u, v;                // barycentrics of the primary hit (reference convention)
+    float px, py, pz;          // offset hit point = shadow ray origin
+    uint32_t pad;
+};
+static_assert(sizeof(ShadowJob) == 32, "ShadowJob");
+
+constexpr int kShards = 32;    // shadow-queue / counter shards (one 128-B line each)
+struct alignas(128) Shard {
+    uint32_t queued;           // shadow jobs appended to this shard
+    uint32_t error;            // traversal stack overflow flag
+    unsigned long long hits;   // primary hits + occluded shadow rays
+    unsigned long long pairs;  // node-pair visits (stats variant)
+    unsigned long long tests;  // triangle tests (stats variant)
+    unsigned long long primary;
+    uint32_t pad[22];
+};
+static_assert(sizeof(Shard) == 128, "Shard");
+
+struct KParams {
+    float eye[3], dir[3], iu[3], iv[3], sun[3];
+    uint32_t W, H;
+    uint32_t row_block, rank, world, local_rows;
+    uint32_t stack_entries;
+    uint32_t root_leaf_count, root_leaf_first;   // root is a leaf (single_ray_traverser.hpp:72-73)
+    uint32_t shard_capacity;                     // jobs per shard
+    const SiblingPair* pairs;
+    const Tri48* tris;
+    const uint32_t* orig;
+    const float* norms;
+    float* pixels;
+    uint8_t* rgb8;
+    ShadowJob* jobs;
+    Shard* shards;
+    // optional per-pixel hit records (G-buffer / parity output), local pixel order
+    int32_t* rec_prim;         // original triangle index, -1 on a primary miss
+    float* rec_tuv;            // t, u, v of the primary hit
+    int8_t* rec_shadow;        // -1 no shadow ray, 0 lit, 1 occluded
+};
+
+}  // namespace ceres

@@ -1,0 +1,143 @@
+// render_cli.cpp -- the `./render <obj> --eye ... --rotate ...` CLI of README.md:11.
+//
+// The reference documents this CLI but never built it (include/CMakeLists.txt:1 comments the
+// target out; static.cpp:21-24 ignores argv).  This is its MI355X implementation: the
+// static.cpp sequence (load :76, rotate :83-88, BVH :100-107, render :130, PPM :135-147) with
+// the hot path on the GPU through libceres_hip.so.  Defaults follow static.cpp:39-47,72-73.
+//
+//   render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]
+//                [--rotate x|y|z deg] [--size W H] [-o|--out file.ppm] [--primary-only]
+//                [--proc N] [--device D] [--bench reps] [--json]
+//
+// Exit status: 0 on success, 1 on a load/render error (message on stderr), 2 on bad usage.
+// There is no CPU fallback: without a gfx950 device the render step fails.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <algorithm>
+#include <cctype>
+
+#include "ceres_render.h"
+
+namespace {
+
+struct Opts {
+    std::string obj, out = "render.ppm";
+    float eye[3] = {0.f, -15.f, 2.f}, dir[3] = {0.f, 1.f, 0.f}, up[3] = {0.f, 0.f, 1.f}, sun[3] = {-50.f, -20.f, 0.f};
+    float fov = 60.f;
+    int rot_axis = -1;
+    float rot_deg = 0.f;
+    size_t W = 1920, H = 1080;
+    int mode = CERES_MODE_FULL, proc = 0, device = 0, bench = 0;
+    bool json = false;
+};
+
+int usage() {
+    std::fprintf(stderr,
+                 "usage: render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]\n"
+                 "              [--rotate x|y|z deg] [--size W H] [-o out.ppm] [--primary-only] [--proc N]\n"
+                 "              [--device D] [--bench reps] [--json]\n");
+    return 2;
+}
+
+bool parse(int argc, char** argv, Opts& o) {
+    auto f = [](const char* s, float* dst) { char* e; *dst = std::strtof(s, &e); return *e == '\0'; };
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        auto have = [&](int n) { return i + n < argc; };
+        auto vec = [&](float* v) { if (!have(3)) return false; bool ok = f(argv[i + 1], v) && f(argv[i + 2], v + 1) && f(argv[i + 3], v + 2); i += 3; return ok; };
+        if (a == "--eye") { if (!vec(o.eye)) return false; }
+        else if (a == "--dir") { if (!vec(o.dir)) return false; }
+        else if (a == "--up") { if (!vec(o.up)) return false; }
+        else if (a == "--sun") { if (!vec(o.sun)) return false; }
+        else if (a == "--fov") { if (!have(1) || !f(argv[++i], &o.fov)) return false; }
+        else if (a == "--rotate") {
+            if (!have(2)) return false;
+            const char c = argv[i + 1][0];
+            o.rot_axis = c == 'x' ? 0 : c == 'y' ? 1 : c == 'z' ? 2 : -2;
+            if (o.rot_axis == -2 || argv[i + 1][1] != '\0' || !f(argv[i + 2], &o.rot_deg)) return false;
+            i += 2;
+        } else if (a == "--size") {
+            if (!have(2)) return false;
+            o.W = std::strtoul(argv[i + 1], nullptr, 10); o.H = std::strtoul(argv[i + 2], nullptr, 10); i += 2;
+            if (!o.W || !o.H) return false;
+        } else if (a == "-o" || a == "--out") { if (!have(1)) return false; o.out = argv[++i]; }
+        else if (a == "--primary-only") o.mode = CERES_MODE_PRIMARY;
+        else if (a == "--proc") { if (!have(1)) return false; o.proc = std::atoi(argv[++i]); }
+        else if (a == "--device") { if (!have(1)) return false; o.device = std::atoi(argv[++i]); }
+        else if (a == "--bench") { if (!have(1)) return false; o.bench = std::atoi(argv[++i]); }
+        else if (a == "--json") o.json = true;
+        else if (a == "-h" || a == "--help") return false;
+        else if (!a.empty() && a[0] == '-' && a.size() > 1 && !std::isdigit((unsigned char)a[1])) { std::fprintf(stderr, "unknown flag %s\n", a.c_str()); return false; }
+        else if (o.obj.empty()) o.obj = a;
+        else return false;
+    }
+    return !o.obj.empty() || o.proc > 0;
+}
+
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Opts o;
+    if (!parse(argc, argv, o)) return usage();
+    float* tri = nullptr; float* norm = nullptr; size_t n_tri = 0;
+    const int rc_load = o.proc ? ceres_proc_mesh(o.proc, &tri, &norm, &n_tri) : ceres_obj_load(o.obj.c_str(), &tri, &norm, &n_tri);
+    if (rc_load != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
+    if (n_tri == 0) { std::fprintf(stderr, "The given scene is empty or cannot be loaded\n"); return 1; }   // static.cpp:77-80
+    if (o.rot_axis >= 0) ceres_rotate_triangles(tri, n_tri, o.rot_axis, o.rot_deg);
+
+    std::printf("Building BVH ( using BinnedSahBuilder )...\n");
+    const double t0 = now_s();
+    uint32_t* nodes = nullptr; uint64_t* prim = nullptr; size_t n_nodes = 0;
+    if (ceres_bvh_build(tri, n_tri, &nodes, &n_nodes, &prim) != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
+    std::printf("%g\n", now_s() - t0);
+    std::printf("BVH of %zu node(s) and %zu reference(s)\n", n_nodes, n_tri);
+
+    ceres_scene* scene = ceres_scene_create(tri, n_tri, norm, nodes, n_nodes, prim, o.device, 0);
+    ceres_free(nodes); ceres_free(prim); ceres_free(tri); ceres_free(norm);
+    if (!scene) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
+
+    float basis[12];
+    std::memcpy(basis, o.eye, sizeof o.eye);
+    ceres_camera_basis(o.eye, o.dir, o.up, o.fov, o.W, o.H, basis + 3);
+    std::vector<uint8_t> rgb(3 * o.W * o.H);
+    std::printf("Rendering image (%zux%zu) on HIP device %d...\n", o.W, o.H, o.device);
+    ceres_stats st{};
+    const double t1 = now_s();
+    int rc = ceres_render_f32(scene, basis, o.sun, o.mode, nullptr, rgb.data(), o.W, o.H, &st);
+    const double t2 = now_s();
+    if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1; }
+    std::printf("%g\n", t2 - t1);
+    std::printf("Rays: %llu\tHits: %llu\n", (unsigned long long)st.rays, (unsigned long long)st.hits);   // anim.cpp:109
+    std::vector<double> ms;
+    for (int r = 0; r < o.bench; ++r) {
+        ceres_stats s2{};
+        rc = ceres_render_f32(scene, basis, o.sun, o.mode, nullptr, rgb.data(), o.W, o.H, &s2);
+        if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1; }
+        ms.push_back(s2.ms);
+    }
+    if (FILE* f = std::fopen(o.out.c_str(), "wb")) {                // static.cpp:135-147
+        std::fprintf(f, "P6 %zu %zu %d\n", o.W, o.H, 255);
+        std::fwrite(rgb.data(), 1, rgb.size(), f);
+        std::fclose(f);
+    } else {
+        std::fprintf(stderr, "error: cannot write %s\n", o.out.c_str());
+        ceres_scene_destroy(scene);
+        return 1;
+    }
+    if (o.json) {
+        double med = 0;
+        if (!ms.empty()) { std::sort(ms.begin(), ms.end()); med = ms[ms.size() / 2]; }
+        std::printf("{\"rays\": %llu, \"hits\": %llu, \"W\": %zu, \"H\": %zu, \"device_ms\": %.4f, \"bench_median_ms\": %.4f, "
+                    "\"mrays_per_s\": %.3f}\n",
+                    (unsigned long long)st.rays, (unsigned long long)st.hits, o.W, o.H, st.ms, med,
+                    med > 0 ? double(st.rays) / (med * 1e3) : 0.0);
+    }
+    ceres_scene_destroy(scene);
+    return 0;
+}

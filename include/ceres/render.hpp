@@ -1,0 +1,162 @@
+// ceres/render.hpp -- drop-in replacement for include/render.hpp of iracigt/ceres-raytracer.
+//
+// Same names, argument meaning and return value as the reference header (render.hpp:16-156):
+//
+//   template <typename Scalar> struct Camera { eye, dir, up; Scalar fov; };         render.hpp:16-22
+//   template <size_t Axis, ...> void rotate_triangles(Scalar deg, Tri*, size_t);     render.hpp:24-44
+//   template <...> std::pair<int,int> render(camera, sun_position, bvh, triangles,
+//                                            tri_norms, pixels, width, height);      render.hpp:86-156
+//
+// but the hot path runs on an MI355X through libceres_hip.so (include/ceres_render.h).  The
+// templates are duck-typed over the BVH / triangle / vector types, so the reference's own
+// callers (static.cpp, anim.cpp) compile against it unchanged with the reference's lib/bvh
+// types (bvh::Bvh<float>, bvh::Triangle<float>, bvh::Vector3<float>), and new code can use
+// the self-contained ceres::HostBvh / ceres::HostTriangle below.
+//
+// Semantics kept: the caller owns every buffer; pixels (3*W*H) are fully overwritten with
+// row j = 0 at the bottom; the return value is {rays traced, hits} (render.hpp:155).
+// Differences, all loud: HIP/launch errors throw std::runtime_error (the reference has no
+// error path); Scalar = double throws (GPU double path not built yet);
+// tri_norms == nullptr throws instead of dereferencing null (render.hpp:142).
+// The uploaded scene is cached per (bvh, triangles, tri_norms, node_count, fingerprint), so
+// multi-frame callers like anim.cpp:82-125 upload once.  Link with -lceres_hip.
+#ifndef CERES_RENDER_HPP_DROPIN
+#define CERES_RENDER_HPP_DROPIN
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "ceres_render.h"
+
+namespace ceres {
+
+// 3-vector that converts to/from any indexable 3-vector type (e.g. bvh::Vector3<Scalar>).
+template <typename Scalar>
+struct vec3 {
+    Scalar v[3] = {0, 0, 0};
+    vec3() = default;
+    vec3(Scalar x, Scalar y, Scalar z) : v{x, y, z} {}
+    template <typename V, typename = decltype(std::declval<const V&>()[0]),
+              typename = std::enable_if_t<!std::is_same<std::decay_t<V>, vec3>::value>>
+    vec3(const V& o) : v{Scalar(o[0]), Scalar(o[1]), Scalar(o[2])} {}
+    template <typename V, typename = std::enable_if_t<!std::is_same<V, vec3>::value &&
+                                                      std::is_constructible<V, Scalar, Scalar, Scalar>::value>>
+    operator V() const { return V(v[0], v[1], v[2]); }
+    Scalar& operator[](size_t i) { return v[i]; }
+    Scalar operator[](size_t i) const { return v[i]; }
+};
+
+// Self-contained equivalents of bvh::Triangle<float> / bvh::Bvh<float> (same layouts).
+struct HostTriangle { vec3<float> p0, e1, e2, n; };
+struct HostBvh {
+    struct Node { float bounds[6]; uint32_t primitive_count, first_child_or_primitive; };
+    std::unique_ptr<Node[]> nodes;
+    std::unique_ptr<size_t[]> primitive_indices;
+    size_t node_count = 0;
+};
+
+namespace detail {
+
+struct SceneCache {
+    const void *bvh = nullptr, *tris = nullptr, *norms = nullptr;
+    size_t node_count = 0, n_tri = 0;
+    uint64_t fingerprint = 0;
+    ceres_scene* scene = nullptr;
+    std::mutex mu;
+    ~SceneCache() { if (scene) ceres_scene_destroy(scene); }
+};
+inline SceneCache& cache() { static SceneCache c; return c; }
+
+inline uint64_t fnv(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ull; }
+    return h;
+}
+// Sampled fingerprint (every 4096th record + both ends) so an edited mesh re-uploads.
+inline uint64_t fingerprint(const void* nodes, size_t n_nodes, const void* tris, size_t n_tri) {
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n_nodes; i += 4096) h = fnv(h, static_cast<const char*>(nodes) + 32 * i, 32);
+    if (n_nodes) h = fnv(h, static_cast<const char*>(nodes) + 32 * (n_nodes - 1), 32);
+    for (size_t i = 0; i < n_tri; i += 4096) h = fnv(h, static_cast<const char*>(tris) + 48 * i, 48);
+    if (n_tri) h = fnv(h, static_cast<const char*>(tris) + 48 * (n_tri - 1), 48);
+    return h;
+}
+
+[[noreturn]] inline void fail(const char* what) {
+    throw std::runtime_error(std::string(what) + ": " + ceres_last_error());
+}
+
+}  // namespace detail
+}  // namespace ceres
+
+template <typename Scalar>
+struct Camera {                                                      // render.hpp:16-22
+    ceres::vec3<Scalar> eye;
+    ceres::vec3<Scalar> dir;
+    ceres::vec3<Scalar> up;
+    Scalar fov;
+};
+
+// render.hpp:24-44 -- rotation about one axis, in place, rebuilding each triangle from p0,
+// p1() = p0 - e1, p2() = p0 + e2 (bit-identical to the reference; runs on the host).
+template <size_t Axis, typename Scalar, typename Tri>
+static void rotate_triangles(Scalar degrees, Tri* triangles, size_t triangle_count) {
+    static_assert(std::is_same<Scalar, float>::value && sizeof(Tri) == 48, "ceres: float triangles (48 B) only");
+    if (ceres_rotate_triangles(reinterpret_cast<float*>(triangles), triangle_count, int(Axis), degrees) != CERES_OK)
+        ceres::detail::fail("rotate_triangles");
+}
+
+// render.hpp:86-156 -- renders W x H pixels on the GPU, returns {rays, hits}.
+template <typename Scalar, typename Vec, typename BvhT, typename TriT, typename NormT>
+std::pair<int, int> render(const Camera<Scalar>& camera, const Vec& sun_position, const BvhT& bvh,
+                           const TriT* triangles, NormT* tri_norms, Scalar* pixels, size_t width, size_t height) {
+    if (!std::is_same<Scalar, float>::value)
+        throw std::runtime_error("ceres render(): Scalar=double is not supported on the GPU path");
+    static_assert(sizeof(TriT) == 48 || !std::is_same<Scalar, float>::value, "triangle must be bvh::Triangle<float> layout");
+    if (!triangles || !tri_norms || !pixels) throw std::runtime_error("ceres render(): null triangles/tri_norms/pixels");
+    const auto* nodes = bvh.nodes.get();
+    const size_t n_nodes = bvh.node_count;
+    static_assert(sizeof(*nodes) == 32, "bvh node must be bvh::Bvh<float>::Node layout");
+    // triangle count = end of the furthest leaf (the reference never passes it explicitly)
+    size_t n_tri = 0;
+    for (size_t k = 0; k < n_nodes; ++k)
+        if (nodes[k].primitive_count)
+            n_tri = std::max<size_t>(n_tri, size_t(nodes[k].first_child_or_primitive) + nodes[k].primitive_count);
+    auto& c = ceres::detail::cache();
+    std::lock_guard<std::mutex> lock(c.mu);
+    const uint64_t fp = ceres::detail::fingerprint(nodes, n_nodes, triangles, n_tri);
+    if (!c.scene || c.bvh != &bvh || c.tris != triangles || c.norms != tri_norms || c.node_count != n_nodes ||
+        c.n_tri != n_tri || c.fingerprint != fp) {
+        if (c.scene) ceres_scene_destroy(c.scene);
+        c.scene = ceres_scene_create(reinterpret_cast<const float*>(triangles), n_tri,
+                                     reinterpret_cast<const float*>(tri_norms), nodes, n_nodes,
+                                     reinterpret_cast<const uint64_t*>(bvh.primitive_indices.get()), 0, 0);
+        if (!c.scene) ceres::detail::fail("ceres_scene_create");
+        c.bvh = &bvh; c.tris = triangles; c.norms = tri_norms; c.node_count = n_nodes; c.n_tri = n_tri; c.fingerprint = fp;
+    }
+    float eye[3] = {float(camera.eye[0]), float(camera.eye[1]), float(camera.eye[2])};
+    float dir[3] = {float(camera.dir[0]), float(camera.dir[1]), float(camera.dir[2])};
+    float up[3] = {float(camera.up[0]), float(camera.up[1]), float(camera.up[2])};
+    float basis[12];
+    std::memcpy(basis, eye, sizeof eye);
+    if (ceres_camera_basis(eye, dir, up, float(camera.fov), width, height, basis + 3) != CERES_OK)
+        ceres::detail::fail("camera basis");
+    const float sun[3] = {float(sun_position[0]), float(sun_position[1]), float(sun_position[2])};
+    ceres_stats st{};
+    if (ceres_render_f32(c.scene, basis, sun, CERES_MODE_FULL, reinterpret_cast<float*>(pixels), nullptr, width,
+                         height, &st) != CERES_OK)
+        ceres::detail::fail("ceres_render_f32");
+    return std::pair<int, int>(int(st.rays), int(st.hits));
+}
+
+#endif  // CERES_RENDER_HPP_DROPIN

@@ -1,0 +1,153 @@
+/* ceres_render.h -- C ABI of the MI355X-native CERES hot path (libceres_hip.so).
+ *
+ * The reference has no C ABI, plugin registry or FFI: its hot path is the header-only
+ * template `render()` (include/render.hpp:86-156 in iracigt/ceres-raytracer) plus the
+ * host-side scene preparation its callers run first (static.cpp:76-107, anim.cpp:38-65).
+ * Every entry point below replaces one of those reference interfaces; the reference
+ * file:line is cited per function.  Plain pointers and sizes only -- no C++ or torch
+ * types -- so it can be bound from C, C++, ctypes, cgo, JNI ...
+ *
+ * Data layouts (all little-endian, fp32 unless stated), identical to the reference's
+ * in-memory structures so a caller can hand its own arrays over unchanged:
+ *   tri48   n_tri  x {p0[3], e1[3], e2[3], n[3]}        = bvh::Triangle<float> (triangle.hpp:17-37)
+ *   norm36  n_tri  x {n0[3], n1[3], n2[3]}              = std::array<Vector3,3> (obj_norms.hpp:113-115)
+ *   nodes32 n_nodes x {bounds[6], u32 count, u32 first} = bvh::Bvh<float>::Node (bvh.hpp:25-30)
+ *   prim64  n_tri  x u64                                = Bvh::primitive_indices (bvh.hpp:94)
+ *   pixels  3*W*H  floats, row j = 0 at the BOTTOM       (render.hpp:107)
+ *   rgb8    3*W*H  bytes = the P6 body, rows top-down, truncating quantiser (static.cpp:135-147)
+ *
+ * Errors: functions return 0 on success and a negative ceres_status on failure;
+ * ceres_last_error() describes the last failure of the calling thread.  The product
+ * path has NO CPU fallback: without a usable gfx950 device every render call fails.
+ * Threading: a ceres_scene is not thread-safe; use one scene per thread (or lock).
+ */
+#ifndef CERES_RENDER_H
+#define CERES_RENDER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    CERES_OK = 0,
+    CERES_EINVAL = -1,      /* bad argument (null pointer, zero size, malformed BVH) */
+    CERES_EIO = -2,         /* file could not be read / malformed OBJ index (obj_norms.hpp:90) */
+    CERES_ENOMEM = -3,      /* host or device allocation failed */
+    CERES_EHIP = -4,        /* HIP runtime error (no device, launch failure, ...) */
+    CERES_ESTACK = -5,      /* traversal stack overflow (single_ray_traverser.hpp:29 assert) */
+    CERES_EUNSUPPORTED = -6
+} ceres_status;
+
+typedef enum {
+    CERES_MODE_FULL = 0,     /* primary + shadow + smooth shading (render.hpp:104-153) */
+    CERES_MODE_PRIMARY = 1   /* primary rays only; pixel = |normalize(tri.n)| (render.hpp:123-125) */
+} ceres_mode;
+
+typedef struct ceres_scene ceres_scene;
+
+/* Per-render counters.  rays/hits are exactly render()'s return pair (render.hpp:102,115,
+ * 119,138,148,155) widened to 64 bit.  The traversal counters are filled only when the
+ * scene was created with CERES_SCENE_STATS (they follow single_ray_traverser.hpp:132-135,
+ * except that shadow rays stop at the first occluder -- any-hit, result-identical). */
+typedef struct {
+    uint64_t rays;            /* primary + shadow traversals */
+    uint64_t hits;            /* primary hits + occluded shadow rays */
+    uint64_t primary_rays, shadow_rays;
+    uint64_t node_pairs;      /* traversal_steps, all rays */
+    uint64_t tri_tests;       /* intersections, all rays */
+    double   ms;              /* device time of the render (HIP events), host-buffer API only */
+} ceres_stats;
+
+/* Row partition across ranks: rows are dealt in blocks of `row_block` rows, block b to rank
+ * b % world; world = 1 renders the whole frame.  Local row k of a rank is
+ * global row j = ((k / row_block) * world + rank) * row_block + k % row_block. */
+typedef struct {
+    uint32_t row_block, rank, world;
+} ceres_tiling;
+
+/* ---- host-side scene preparation (what static.cpp / anim.cpp run before render()) ---- */
+
+/* obj::load_from_file<float> (obj_norms.hpp:120-127 / load_from_stream :57-118): v/f lines,
+ * fan triangulation, area-weighted left-handed vertex normals.  *tri48 / *norm36 are
+ * malloc'd (free with ceres_free).  An unreadable file yields n_tri = 0 like the reference. */
+int ceres_obj_load(const char* path, float** tri48, float** norm36, size_t* n_tri);
+/* Procedural heightfield mesh of the C5 configuration (n x n vertices, 2(n-1)^2 triangles,
+ * SURVEY.md §8(d)); same arrays as ceres_obj_load. */
+int ceres_proc_mesh(int n, float** tri48, float** norm36, size_t* n_tri);
+/* rotate_triangles<Axis> (render.hpp:24-44); axis 0/1/2 = x/y/z.  In place. */
+int ceres_rotate_triangles(float* tri48, size_t n_tri, int axis, float degrees);
+/* compute_bounding_boxes_and_centers + BinnedSahBuilder<Bvh,16>::build (utilities.hpp:142-171,
+ * binned_sah_builder.hpp:39-234).  *nodes32 (n_nodes x 32 B) / *prim64 malloc'd. */
+int ceres_bvh_build(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64);
+/* Camera basis of render.hpp:91-97: out = {dir[3], image_u*w[3], image_v*w*ratio[3]}. */
+int ceres_camera_basis(const float eye[3], const float dir[3], const float up[3], float fov_deg,
+                       size_t width, size_t height, float out9[9]);
+void ceres_free(void* p);
+
+/* ---- device scene ---- */
+
+#define CERES_SCENE_STATS 1u   /* flag: build the kernels' traversal-statistics variant */
+
+/* Upload a scene to HIP device `device` (re-laid for the GPU: sibling-pair 64-B node records,
+ * triangles permuted into leaf order).  The caller keeps ownership of its host arrays; they
+ * may be freed after the call.  Returns NULL on failure (see ceres_last_error).
+ * Replaces the (bvh, triangles, tri_norms) arguments of render() (render.hpp:87-88). */
+ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* norm36,
+                                const void* nodes32, size_t n_nodes, const uint64_t* prim64,
+                                int device, uint32_t flags);
+void ceres_scene_destroy(ceres_scene* scene);
+/* depth of the BVH (levels below the root) and the traversal-stack entries the kernels use */
+int ceres_scene_info(const ceres_scene* scene, uint32_t* depth, uint32_t* stack_entries,
+                     size_t* n_pairs, size_t* device_bytes);
+
+/* ---- the hot path ---- */
+
+/* render<float>() (render.hpp:86-156) on host buffers: uploads nothing but the camera,
+ * renders on the device, copies back.  pixels (3*W*H floats) and/or rgb8 (3*W*H bytes, PPM
+ * body) may be NULL.  basis12 = {eye[3], dir[3], image_u[3], image_v[3]} as produced by
+ * ceres_camera_basis (so libm stays on the host and is pinned by fixtures). */
+int ceres_render_f32(ceres_scene* scene, const float basis12[12], const float sun[3], int mode,
+                     float* pixels, uint8_t* rgb8, size_t width, size_t height, ceres_stats* stats);
+
+/* Device-resident variant for benchmarks and multi-GPU drivers: all output pointers are
+ * DEVICE pointers on the scene's device, work is enqueued on `stream` (a hipStream_t, NULL =
+ * default stream) and NOT synchronised.  Outputs cover only this rank's rows (ceres_tiling):
+ * d_pixels = 3*W*local_rows floats (local row-major, local row 0 first) or NULL;
+ * d_rgb8 = 3*W*local_rows bytes with local row k stored at position local_rows-1-k (so for
+ * world = 1 it is exactly the PPM body) or NULL.  d_counters (8 x u64, zeroed by this call)
+ * receives {rays, hits, primary_rays, shadow_rays, node_pairs, tri_tests, 0, 0}; may be NULL. */
+int ceres_render_device(ceres_scene* scene, const float basis12[12], const float sun[3], int mode,
+                        size_t width, size_t height, const ceres_tiling* tiling,
+                        float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, void* stream);
+/* Per-pixel hit records of one render (host buffers, W*H entries each, pixel = j*W + i):
+ * prim = ORIGINAL triangle index of the primary hit or -1 (render.hpp:120), tuv = {t, u, v}
+ * of that hit (triangle.hpp:95-115 convention), shadow = -1 (no shadow ray), 0 (lit) or
+ * 1 (occluded).  A G-buffer output for parity checks and downstream users. */
+int ceres_render_records(ceres_scene* scene, const float basis12[12], const float sun[3], int mode,
+                         size_t width, size_t height, int32_t* prim, float* tuv, int8_t* shadow,
+                         ceres_stats* stats);
+/* rows a rank owns under a tiling */
+size_t ceres_tiling_local_rows(size_t height, const ceres_tiling* tiling);
+
+/* Per-kernel device timing (bench.py roofline leg): while enabled, every render records HIP
+ * events around ceres_primary and ceres_shadow on the stream it was launched on.
+ * ceres_scene_read_timing synchronises, returns the summed durations (ms) and the number of
+ * renders since the last read, and resets. */
+int ceres_scene_set_timing(ceres_scene* scene, int enable);
+int ceres_scene_read_timing(ceres_scene* scene, double* primary_ms, double* shadow_ms, uint64_t* renders);
+
+/* Launch-geometry introspection for the roofline accounting in bench.py (kernel names as
+ * they appear in rocprofv3 traces). */
+const char* ceres_kernel_names(void);
+
+const char* ceres_last_error(void);
+const char* ceres_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CERES_RENDER_H */

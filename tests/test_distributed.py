@@ -1,0 +1,82 @@
+"""Multi-rank framebuffer partition + gather on CPU with the gloo backend.
+
+Each rank fills its local RGB8 buffer exactly as ceres_render_device lays it out (its rows of
+the reference PPM -- from the golden fixture -- local row k at position n-1-k), then
+FrameGather assembles the frame on rank 0 with one collective; the result must be the
+reference PPM byte for byte.  The GPU side of the same path is tests/test_gpu_parity.py.
+"""
+import gzip
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, REPO, import_package
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, name, W, H, row_block, q):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import import_package as ip
+    pkg = ip()
+    import ceres_raytracer_amd.distributed as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with open(os.path.join(GOLDEN, name + ".exact.ppm.gz"), "rb") as f:
+            ppm = gzip.decompress(f.read())
+        hdr = len(b"P6 %d %d 255\n" % (W, H))
+        body = np.frombuffer(ppm[hdr:], np.uint8).reshape(H, 3 * W)
+        g = D.FrameGather(W, H, row_block, rank, world, device="cpu")
+        rows = D.row_map(H, row_block, world)[rank]
+        assert g.local_rows == len(rows) == pkg.local_rows(H, pkg.Tiling(row_block, rank, world))
+        n = len(rows)
+        for k, j in enumerate(rows):
+            g.local[n - 1 - k] = torch.from_numpy(body[H - 1 - j].copy())
+        full = g.gather()
+        if rank == 0:
+            q.put(bool(np.array_equal(full.numpy(), body)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,row_block", [(2, 16), (3, 7), (2, 1000)])
+def test_gather_reassembles_reference_frame(world, row_block):
+    import_package()
+    name, W, H = "dragon_333x217", 333, 217
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, W, H, row_block, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
+
+
+def test_row_map_covers_every_row_once():
+    pkg = import_package()
+    import ceres_raytracer_amd.distributed as D
+    for H in (1, 15, 16, 17, 1080, 4096):
+        for world in (1, 2, 3, 8):
+            for rb in (1, 16, 64):
+                rows = D.row_map(H, rb, world)
+                allr = np.sort(np.concatenate(rows))
+                np.testing.assert_array_equal(allr, np.arange(H))
+                for r in range(world):
+                    assert len(rows[r]) == pkg.local_rows(H, pkg.Tiling(rb, r, world))
