@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "ceres_obj_load", "ceres_proc_mesh", "ceres_rotate_triangles", "ceres_bvh_build", "ceres_camera_basis",
     "ceres_free", "ceres_scene_create", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
     "ceres_render_device", "ceres_render_records", "ceres_tiling_local_rows", "ceres_scene_set_timing", "ceres_scene_read_timing",
+    "ceres_scene_wave_log",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
 )
 
@@ -110,6 +111,7 @@ def lib():
     L.ceres_scene_set_timing.argtypes = [_vp, ctypes.c_int]
     L.ceres_scene_read_timing.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           _u64p]
+    L.ceres_scene_wave_log.argtypes = [_vp, _u64p, _sz, ctypes.POINTER(_sz)]
     _lib = L
     return L
 
@@ -261,6 +263,13 @@ class Scene:
 
     def set_timing(self, on):
         _check(lib().ceres_scene_set_timing(self._h, 1 if on else 0))
+
+    def wave_log(self, max_waves=1 << 16):
+        """Diagnostic per-wavefront records of the last persistent-kernel frame (stats scenes)."""
+        out = np.zeros(8 * max_waves, np.uint64)
+        n = _sz()
+        _check(lib().ceres_scene_wave_log(self._h, _p(out, ctypes.c_uint64), max_waves, ctypes.byref(n)))
+        return out[: 8 * n.value].reshape(-1, 8)
 
     def read_timing(self):
         p, q, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()

@@ -51,13 +51,15 @@ static_assert(sizeof(ShadowJob) == 32, "ShadowJob");
 
 constexpr int kShards = 32;    // shadow-queue / counter shards (one 128-B line each)
 struct alignas(128) Shard {
-    uint32_t queued;           // shadow jobs appended to this shard
+    uint32_t queued;           // shadow rays traced (twopass: jobs appended to this shard)
     uint32_t error;            // traversal stack overflow flag
     unsigned long long hits;   // primary hits + occluded shadow rays
     unsigned long long pairs;  // node-pair visits (stats variant)
     unsigned long long tests;  // triangle tests (stats variant)
     unsigned long long primary;
-    uint32_t pad[22];
+    uint32_t tiles;            // persistent kernel: next chunk of this shard's tile band
+    uint32_t exhausted;        // persistent kernel (shard 0 only): bitmask of drained tile shards
+    uint32_t pad[20];
 };
 static_assert(sizeof(Shard) == 128, "Shard");
 
@@ -67,7 +69,9 @@ struct KParams {
     uint32_t row_block, rank, world, local_rows;
     uint32_t stack_entries;
     uint32_t root_leaf_count, root_leaf_first;   // root is a leaf (single_ray_traverser.hpp:72-73)
-    uint32_t shard_capacity;                     // jobs per shard
+    uint32_t shard_capacity;                     // jobs per shard (twopass kernels)
+    uint32_t tiles_x, tiles_y, n_chunks;         // persistent kernel: 8x8 tiles, chunks of kChunkTiles
+    uint32_t pad_;
     const SiblingPair* pairs;
     const Tri48* tris;
     const uint32_t* orig;
@@ -80,6 +84,8 @@ struct KParams {
     int32_t* rec_prim;         // original triangle index, -1 on a primary miss
     float* rec_tuv;            // t, u, v of the primary hit
     int8_t* rec_shadow;        // -1 no shadow ray, 0 lit, 1 occluded
+    // diagnostic (stats scenes only): 8 x u64 per wavefront of the persistent kernel
+    unsigned long long* wave_log;
 };
 
 }  // namespace ceres

@@ -27,6 +27,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -36,6 +37,7 @@
 #include "ceres_render.h"
 #include "ceres_types.hpp"
 #include "host_common.hpp"
+#include "pow24.hpp"
 
 #pragma clang fp contract(off)
 
@@ -71,88 +73,103 @@ __device__ __forceinline__ TriV load_tri(const Tri48* t) {
 // Per-ray traversal state; the hit is "last accepted wins" like intersect_leaf (:54-60).
 struct Hit { uint32_t slot; float t, u, v; };
 
-template <bool kAnyHit, bool kStats>
+// Triangle::intersect (triangle.hpp:95-115, left-handed normal): on an accepted hit updates
+// best / tmax (closest hit keeps the LAST accepted hit with t <= tmax, intersect_leaf :54-60).
+__device__ __forceinline__ bool tri_test(const Tri48* tp, F3 o, F3 d, float tmin, float tmax, float& t_out,
+                                         float& u_out, float& v_out) {
+    const TriV tr = load_tri(tp);
+    const F3 c = tr.p0 - o;
+    const F3 r = cross(d, c);
+    const float inv_det = 1.0f / dot(tr.n, d);
+    const float u = dot(r, tr.e2) * inv_det;
+    const float v = dot(r, tr.e1) * inv_det;
+    const float w = 1.0f - u - v;
+    if (u >= 0 && v >= 0 && w >= 0) {
+        const float t = dot(tr.n, c) * inv_det;
+        if (t >= tmin && t <= tmax) { t_out = t; u_out = u; v_out = v; return true; }
+    }
+    return false;
+}
+
+// Eager BVH2 traversal, single_ray_traverser.hpp:68-126 with FastNodeIntersector
+// (node_intersectors.hpp:35-47,83-103).  Exactly the reference's visiting order: both
+// children's slab tests use the tmax from before this step's leaves; left leaf triangles,
+// then right leaf triangles, are tested in leaf order; the far child is pushed, ties go left.
+//
+// Slab test restatement: the reference picks the entry/exit bound per axis by the ray octant
+// and evaluates fma(bound, inv, -o*inv).  fma is monotone in `bound`, so for inv >= 0 (octant
+// 0, including d = +0 -> inv = +1/eps) fma(min) <= fma(max) and for inv < 0 (d = -0 included)
+// the reverse: the octant-selected entry is min(fma(lo), fma(hi)) and the exit is the max,
+// bit for bit, without per-ray selects.  robust_max(x, y) = x > y ? x : y equals fmaxf(x, y)
+// whenever y is not NaN (y is tmin / tmax / a previous robust_max -- never NaN) up to the
+// sign of zero, which no comparison below can observe; likewise robust_min and fminf.  The
+// slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
+template <bool kAnyHit, bool kStats, int kStride = kBlock>
 __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* stk, Hit& best,
                                       uint32_t& n_pairs, uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f;
     float tmax = FLT_MAX;                                           // ray.hpp:17-21
     bool have = false;
-    auto leaf = [&](uint32_t first, uint32_t count) -> bool {        // intersect_leaf, :43-63
-        if (kStats) n_tests += count;
-        for (uint32_t k = first; k < first + count; ++k) {
-            const TriV tr = load_tri(P.tris + k);
-            const F3 c = tr.p0 - o;                                   // Triangle::intersect, triangle.hpp:95-115
-            const F3 r = cross(d, c);
-            const float inv_det = 1.0f / dot(tr.n, d);
-            const float u = dot(r, tr.e2) * inv_det;
-            const float v = dot(r, tr.e1) * inv_det;
-            const float w = 1.0f - u - v;
-            if (u >= 0 && v >= 0 && w >= 0) {
-                const float t = dot(tr.n, c) * inv_det;
-                if (t >= tmin && t <= tmax) {
-                    best = {k, t, u, v};
-                    have = true;
-                    if (kAnyHit) return true;
-                    tmax = t;
-                }
+    if (P.root_leaf_count) {                                          // root is a leaf, :72-73
+        if (kStats) n_tests += P.root_leaf_count;
+        for (uint32_t k = P.root_leaf_first; k < P.root_leaf_first + P.root_leaf_count; ++k) {
+            float t, u, v;
+            if (tri_test(P.tris + k, o, d, tmin, tmax, t, u, v)) {
+                best = {k, t, u, v}; have = true;
+                if (kAnyHit) return true;
+                tmax = t;
             }
         }
-        return false;
-    };
-    if (P.root_leaf_count) {                                          // :72-73
-        leaf(P.root_leaf_first, P.root_leaf_count);
         return have;
     }
-    // FastNodeIntersector (node_intersectors.hpp:83-103): octant, safe_inverse, -o * inv
-    const bool ox = signbit(d.x), oy = signbit(d.y), oz = signbit(d.z);
-    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
+    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };   // vector.hpp:69-74
     const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
     const float sx = (-o.x) * ix, sy = (-o.y) * iy, sz = (-o.z) * iz;
-    uint32_t cur = 0, sp = 0;                                         // pair of the root's children
-    while (true) {                                                    // single_ray_traverser.hpp:82-123
+    uint32_t cur = 0, sp = 0;                                         // pair of the root's children (:81)
+    while (true) {                                                    // :82-123
         if (kStats) ++n_pairs;
         const float4* q = reinterpret_cast<const float4*>(P.pairs + cur);
         const float4 A = q[0], B = q[1], C = q[2];
         const uint4 L = reinterpret_cast<const uint4*>(q)[3];
-        // left child bounds A.x A.y A.z A.w B.x B.y ; right child B.z B.w C.x C.y C.z C.w
-        const float le = rmax(__builtin_fmaf(ox ? A.y : A.x, ix, sx),
-                         rmax(__builtin_fmaf(oy ? A.w : A.z, iy, sy),
-                         rmax(__builtin_fmaf(oz ? B.y : B.x, iz, sz), tmin)));
-        const float lx = rmin(__builtin_fmaf(ox ? A.x : A.y, ix, sx),
-                         rmin(__builtin_fmaf(oy ? A.z : A.w, iy, sy),
-                         rmin(__builtin_fmaf(oz ? B.x : B.y, iz, sz), tmax)));
-        const float re = rmax(__builtin_fmaf(ox ? B.w : B.z, ix, sx),
-                         rmax(__builtin_fmaf(oy ? C.y : C.x, iy, sy),
-                         rmax(__builtin_fmaf(oz ? C.w : C.z, iz, sz), tmin)));
-        const float rx = rmin(__builtin_fmaf(ox ? B.z : B.w, ix, sx),
-                         rmin(__builtin_fmaf(oy ? C.x : C.y, iy, sy),
-                         rmin(__builtin_fmaf(oz ? C.z : C.w, iz, sz), tmax)));
-        bool go_l = false, go_r = false;
-        if (le <= lx) {
-            if (L.x) { if (leaf(L.y, L.x) && kAnyHit) return true; }
-            else go_l = true;
-        }
-        if (re <= rx) {
-            if (L.z) { if (leaf(L.w, L.z) && kAnyHit) return true; }
-            else go_r = true;
-        }
-        if (go_l) {
-            if (go_r) {
-                uint32_t near_c = L.y, far_c = L.w;
-                if (le > re) { near_c = L.w; far_c = L.y; }
-                if (sp >= P.stack_entries) { overflow = true; return have; }
-                stk[sp * kBlock] = far_c;
-                ++sp;
-                cur = near_c;
-            } else {
-                cur = L.y;
+        // left bounds A.x A.y | A.z A.w | B.x B.y ; right bounds B.z B.w | C.x C.y | C.z C.w
+        const float l0 = __builtin_fmaf(A.x, ix, sx), l1 = __builtin_fmaf(A.y, ix, sx);
+        const float l2 = __builtin_fmaf(A.z, iy, sy), l3 = __builtin_fmaf(A.w, iy, sy);
+        const float l4 = __builtin_fmaf(B.x, iz, sz), l5 = __builtin_fmaf(B.y, iz, sz);
+        const float r0 = __builtin_fmaf(B.z, ix, sx), r1 = __builtin_fmaf(B.w, ix, sx);
+        const float r2 = __builtin_fmaf(C.x, iy, sy), r3 = __builtin_fmaf(C.y, iy, sy);
+        const float r4 = __builtin_fmaf(C.z, iz, sz), r5 = __builtin_fmaf(C.w, iz, sz);
+        const float le = fmaxf(fminf(l0, l1), fmaxf(fminf(l2, l3), fmaxf(fminf(l4, l5), tmin)));
+        const float lx = fminf(fmaxf(l0, l1), fminf(fmaxf(l2, l3), fminf(fmaxf(l4, l5), tmax)));
+        const float re = fmaxf(fminf(r0, r1), fmaxf(fminf(r2, r3), fmaxf(fminf(r4, r5), tmin)));
+        const float rx = fminf(fmaxf(r0, r1), fminf(fmaxf(r2, r3), fminf(fmaxf(r4, r5), tmax)));
+        const bool hit_l = le <= lx, hit_r = re <= rx;
+        // leaves of this step, left then right (intersect_leaf on each, :89-107)
+        uint32_t k = 0, k_end = 0, k2 = 0, k2_end = 0;
+        if (hit_l && L.x) { k = L.y; k_end = L.y + L.x; }
+        if (hit_r && L.z) { k2 = L.w; k2_end = L.w + L.z; }
+        if (kStats) n_tests += (k_end - k) + (k2_end - k2);
+        while (k < k_end || k2 < k2_end) {
+            const uint32_t idx = k < k_end ? k++ : k2++;
+            float t, u, v;
+            if (tri_test(P.tris + idx, o, d, tmin, tmax, t, u, v)) {
+                best = {idx, t, u, v}; have = true;
+                if (kAnyHit) return true;
+                tmax = t;
             }
-        } else if (go_r) {
-            cur = L.w;
+        }
+        const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
+        if (go_l && go_r) {                                           // near first, ties left (:109-115)
+            const bool swap = le > re;
+            if (sp >= P.stack_entries) { overflow = true; return have; }
+            stk[sp * kStride] = swap ? L.y : L.w;
+            ++sp;
+            cur = swap ? L.w : L.y;
+        } else if (go_l || go_r) {
+            cur = go_l ? L.y : L.w;                                   // :115-117
         } else {
-            if (sp == 0) break;
+            if (sp == 0) break;                                       // :118-121
             --sp;
-            cur = stk[sp * kBlock];
+            cur = stk[sp * kStride];
         }
     }
     return have;
@@ -198,7 +215,7 @@ __device__ __forceinline__ void shade(F3 sun_line, const float* nrm, F3 view, fl
     for (int k = 0; k < 3; ++k) {
         const F3 N{nrm[3 * k], nrm[3 * k + 1], nrm[3 * k + 2]};
         const float diffuse = 0.5f * fabsf(sun_line.x * N.x + sun_line.y * N.y + sun_line.z * N.z);
-        const float spec = 0.8f * float(pow(double(dot(N, normalize(sun_line + vneg))), 24.0));
+        const float spec = 0.8f * pow24f(dot(N, normalize(sun_line + vneg)));   // == (float)std::pow(double, 24)
         const float base = amb + diffuse;
         auto clamp01 = [](float x) { return (x < 0.f) ? 0.f : (1.f < x) ? 1.f : x; };   // std::clamp
         c[0] += w[k] * clamp01(base * 0.5f + spec);
@@ -214,15 +231,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 }
 
 // ---------------------------------------------------------------- primary kernel
-template <int kMode, bool kStats>
-__global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t* stk = lds + tid;                                       // [entries][kBlock]
-    uint32_t* red = lds + P.stack_entries * kBlock;                  // block-reduction scratch (16 words)
-    // 16x16 pixel block = 2x2 wavefront tiles of 8x8 (coherent primary rays per wave)
-    const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const uint32_t lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+// kBS threads per workgroup (64: one 8x8 tile per workgroup; 256: 16x16 pixels as 2x2 wave
+// tiles).  Every wavefront is independent: no workgroup barrier, one queue atomic per wave.
+template <int kMode, bool kStats, int kBS>
+__device__ __forceinline__ void primary_tile(const KParams& P, uint32_t* stk, uint32_t lane, uint32_t wave_id,
+                                             uint32_t i, uint32_t lr) {
     const bool active = i < P.W && lr < P.local_rows;
     bool hit = false, job = false;
     Hit h{0, 0.f, 0.f, 0.f};
@@ -233,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
         const uint32_t j = global_row(P, lr);
         const F3 eye{P.eye[0], P.eye[1], P.eye[2]};
         const F3 view = primary_dir(P, i, j);
-        hit = trace<false, kStats>(P, eye, view, stk, h, n_pairs, n_tests, overflow);
+        hit = trace<false, kStats, kBS>(P, eye, view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
             const size_t px = size_t(lr) * P.W + i;
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
@@ -257,60 +270,70 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
             }
         }
     }
-    // wave-level compaction of shadow rays + hit count; one queue atomic per workgroup
+    // wave-level compaction of the shadow rays: ballot + popcount prefix, one atomic per wave
+    const uint32_t shard = wave_id % kShards;
     const unsigned long long jm = __ballot(job);
-    const unsigned long long hm = __ballot(hit);
-    if (lane == 0) { red[wave] = __popcll(jm); red[kWaves + wave] = __popcll(hm); }
-    __syncthreads();
-    const uint32_t shard = (blockIdx.y * gridDim.x + blockIdx.x) % kShards;
-    if (tid == 0) {
-        uint32_t nj = 0, nh = 0;
-        for (int w = 0; w < kWaves; ++w) { nj += red[w]; nh += red[kWaves + w]; }
-        red[2 * kWaves] = nj ? atomicAdd(&P.shards[shard].queued, nj) : 0u;
+    const uint32_t nh = __popcll(__ballot(hit));
+    uint32_t base = 0;
+    if (lane == 0) {
+        if (jm) base = atomicAdd(&P.shards[shard].queued, uint32_t(__popcll(jm)));
         if (nh) atomicAdd(&P.shards[shard].hits, (unsigned long long)nh);
     }
-    __syncthreads();
-    if (job) {
-        uint32_t off = red[2 * kWaves];
-        for (uint32_t w = 0; w < wave; ++w) off += red[w];
-        off += __popcll(jm & ((1ull << lane) - 1ull));
-        ShadowJob* dst = P.jobs + size_t(shard) * P.shard_capacity + off;
-        float4* q = reinterpret_cast<float4*>(dst);
-        q[0] = make_float4(__uint_as_float(lr * P.W + i), __uint_as_float(h.slot), h.u, h.v);
-        q[1] = make_float4(shadow_o.x, shadow_o.y, shadow_o.z, 0.f);
+    if (jm) {
+        base = __shfl(base, 0, 64);
+        if (job) {
+            const uint32_t off = base + __popcll(jm & ((1ull << lane) - 1ull));
+            float4* q = reinterpret_cast<float4*>(P.jobs + size_t(shard) * P.shard_capacity + off);
+            q[0] = make_float4(__uint_as_float(lr * P.W + i), __uint_as_float(h.slot), h.u, h.v);
+            q[1] = make_float4(shadow_o.x, shadow_o.y, shadow_o.z, 0.f);
+        }
     }
     if (kStats) {
         const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
-        __syncthreads();
-        if (lane == 0) { red[wave] = wp; red[kWaves + wave] = wt; }
-        __syncthreads();
-        if (tid == 0) {
-            unsigned long long sp = 0, st = 0;
-            for (int w = 0; w < kWaves; ++w) { sp += red[w]; st += red[kWaves + w]; }
-            atomicAdd(&P.shards[shard].pairs, sp);
-            atomicAdd(&P.shards[shard].tests, st);
+        if (lane == 0) {
+            atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
+            atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
         }
     }
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
 }
 
+
+template <int kMode, bool kStats, int kBS>
+__global__ __launch_bounds__(kBS) void ceres_primary(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t* stk = lds + tid;                                       // [entries][kBS]
+    if (kBS == 64) {
+        // one wavefront per workgroup; tiles_per_wave 8x8 tiles, interleaved over the grid
+        const uint32_t n_tiles = P.tiles_x * P.tiles_y;
+        for (uint32_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+            const uint32_t ty = t / P.tiles_x, tx = t - ty * P.tiles_x;
+            primary_tile<kMode, kStats, kBS>(P, stk, lane, t, tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
+        }
+    } else {
+        const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+        const uint32_t lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+        primary_tile<kMode, kStats, kBS>(P, stk, lane, (blockIdx.y * gridDim.x + blockIdx.x) * (kBS / 64) + wave, i, lr);
+    }
+}
+
 // ---------------------------------------------------------------- shadow kernel
-template <bool kStats>
-__global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
+template <bool kStats, int kBS>
+__global__ __launch_bounds__(kBS) void ceres_shadow(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* stk = lds + tid;
-    uint32_t* pre = lds + P.stack_entries * kBlock;                  // 33 prefix words + 8 reduction words
-    uint32_t* red = pre + 36;
-    if (tid < kShards) pre[tid + 1] = P.shards[tid].queued;
-    __syncthreads();
-    if (tid == 0) { pre[0] = 0; for (int s = 1; s <= kShards; ++s) pre[s] += pre[s - 1]; }
-    __syncthreads();
+    // per-shard job prefix, read by every wave from the shard counters (scalar loads)
+    uint32_t pre[kShards + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int s = 0; s < kShards; ++s) pre[s + 1] = pre[s] + __builtin_amdgcn_readfirstlane(P.shards[s].queued);
     const uint32_t total = pre[kShards];
     const F3 sun{P.sun[0], P.sun[1], P.sun[2]};
     uint32_t occluded = 0, n_pairs = 0, n_tests = 0;
     bool overflow = false;
-    for (uint32_t g = blockIdx.x * kBlock + tid; g < total; g += gridDim.x * kBlock) {
+    for (uint32_t g = blockIdx.x * kBS + tid; g < total; g += gridDim.x * kBS) {
         uint32_t s = 0;                                              // shard holding global job g
 #pragma unroll
         for (uint32_t step = 16; step > 0; step >>= 1)
@@ -322,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
         const F3 o{J1.x, J1.y, J1.z};
         const F3 sun_line = normalize(sun - o);                      // render.hpp:135
         Hit h2{0, 0.f, 0.f, 0.f};
-        const bool blocked = trace<true, kStats>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow);
+        const bool blocked = trace<true, kStats, kBS>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow);
         const uint32_t lr = pix / P.W, i = pix - lr * P.W;
         if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
         if (blocked) {                                               // render.hpp:147-150
@@ -336,15 +359,182 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
         }
     }
     const uint32_t wo = wave_sum(occluded);
-    const uint32_t wp = kStats ? wave_sum(n_pairs) : 0u, wt = kStats ? wave_sum(n_tests) : 0u;
-    if (lane == 0) { red[wave] = wo; red[kWaves + wave] = wp; red[2 * kWaves + wave] = wt; }
-    __syncthreads();
-    const uint32_t shard = blockIdx.x % kShards;
-    if (tid == 0) {
-        unsigned long long so = 0, sp = 0, st = 0;
-        for (int w = 0; w < kWaves; ++w) { so += red[w]; sp += red[kWaves + w]; st += red[2 * kWaves + w]; }
-        if (so) atomicAdd(&P.shards[shard].hits, so);
-        if (kStats) { atomicAdd(&P.shards[shard].pairs, sp); atomicAdd(&P.shards[shard].tests, st); }
+    const uint32_t shard = (blockIdx.x * (kBS / 64) + wave) % kShards;
+    if (lane == 0 && wo) atomicAdd(&P.shards[shard].hits, (unsigned long long)wo);
+    if (kStats) {
+        const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
+        if (lane == 0) {
+            atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
+            atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
+        }
+    }
+    if (overflow) atomicOr(&P.shards[shard].error, 1u);
+}
+
+// ---------------------------------------------------------------- persistent frame kernel
+// One launch per frame.  Each wavefront is an independent worker with a private LDS region:
+//   [stack: entries x 64 lanes][shadow-ray queue: 7 x 128 words (pixel, slot, u, v, px, py, pz)]
+// Loop: fetch a chunk of 8x8 tiles (dynamic, sharded counters); trace the tile's primary rays
+// (one pixel per lane, closest hit); write misses; COMPACT the hits' shadow rays into the
+// wave's LDS queue with __ballot + popcount prefix; whenever >= 64 are queued, trace a FULL
+// wavefront of shadow rays (any-hit) and shade them.  The queue is flushed when the work runs
+// out.  No global queue, no block barriers, no second launch; shadow rays stay coherent
+// (they come from the same tiles) and waves stay dense.
+constexpr int kFrameBlock = 128;          // 2 independent wavefronts per workgroup
+constexpr int kQueue = 128;               // shadow-ray queue capacity per wavefront
+constexpr int kQueueWords = 7 * kQueue;
+constexpr int kChunkTiles = 2;            // tiles per dynamic fetch
+constexpr int kTileShards = 16;           // tile counters (bands of the tile grid)
+
+__device__ __forceinline__ uint32_t band_begin(uint32_t s, uint32_t n_chunks) {
+    return uint32_t((uint64_t(n_chunks) * s) / kTileShards);
+}
+
+// Lane 0 claims the next chunk: its own band first, then the others (skipping drained ones).
+__device__ __forceinline__ uint32_t fetch_chunk(const KParams& P, uint32_t home, uint32_t lane) {
+    uint32_t got = 0xffffffffu;
+    if (lane == 0) {
+        uint32_t dead = __hip_atomic_load(&P.shards[0].exhausted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t k = 0; k < kTileShards; ++k) {
+            const uint32_t s = (home + k) % kTileShards;
+            if (dead & (1u << s)) continue;
+            const uint32_t b0 = band_begin(s, P.n_chunks), b1 = band_begin(s + 1, P.n_chunks);
+            const uint32_t v = atomicAdd(&P.shards[s].tiles, 1u);
+            if (v < b1 - b0) { got = b0 + v; break; }
+            atomicOr(&P.shards[0].exhausted, 1u << s);
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(__shfl(got, 0, 64));
+}
+
+template <bool kStats>
+__device__ __forceinline__ void shade_queued(const KParams& P, uint32_t* q, uint32_t base, uint32_t count,
+                                             uint32_t lane, uint32_t* stk, uint32_t& occluded, uint32_t& traced,
+                                             uint32_t& n_pairs, uint32_t& n_tests, bool& overflow) {
+    if (lane >= count) return;
+    const uint32_t e = base + lane;
+    const uint32_t pix = q[e], slot = q[kQueue + e];
+    const float hu = __uint_as_float(q[2 * kQueue + e]), hv = __uint_as_float(q[3 * kQueue + e]);
+    const F3 o{__uint_as_float(q[4 * kQueue + e]), __uint_as_float(q[5 * kQueue + e]), __uint_as_float(q[6 * kQueue + e])};
+    const F3 sun{P.sun[0], P.sun[1], P.sun[2]};
+    const F3 sun_line = normalize(sun - o);                          // render.hpp:135
+    Hit h2{0, 0.f, 0.f, 0.f};
+    const bool blocked = trace<true, kStats, 64>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow);
+    ++traced;
+    const uint32_t lr = pix / P.W, i = pix - lr * P.W;
+    if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
+    if (blocked) {                                                   // render.hpp:147-150
+        ++occluded;
+        store_pixel(P, lr, i, 0.f, 0.f, 0.f);
+    } else {                                                         // render.hpp:139-146
+        const F3 view = primary_dir(P, i, global_row(P, lr));
+        float c[3];
+        shade(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
+        store_pixel(P, lr, i, c[0], c[1], c[2]);
+    }
+}
+
+template <int kMode, bool kStats>
+__global__ __launch_bounds__(kFrameBlock) void ceres_frame(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t lane = threadIdx.x & 63, wslot = threadIdx.x >> 6;
+    const uint32_t per_wave = P.stack_entries * 64 + kQueueWords;
+    uint32_t* base = lds + wslot * per_wave;
+    uint32_t* stk = base + lane;                                     // entry k of this lane at stk[k * 64]
+    uint32_t* q = base + P.stack_entries * 64;
+    const uint32_t wave_id = blockIdx.x * (kFrameBlock / 64) + wslot;
+    const uint32_t home = wave_id % kTileShards;
+    const F3 eye{P.eye[0], P.eye[1], P.eye[2]};
+    uint32_t qn = 0;                                                 // queued shadow rays (wave-uniform)
+    uint32_t hits = 0, occluded = 0, traced = 0, n_pairs = 0, n_tests = 0;
+    bool overflow = false;
+    // diagnostic stamps (stats build only): wall clock (100 MHz) + shader-clock fetch time
+    unsigned long long t_begin = 0, fetch_clk = 0, n_chunk = 0, n_batch = 0;
+    if (kStats) t_begin = __builtin_amdgcn_s_memrealtime();
+    auto fetch = [&]() {
+        unsigned long long c0 = 0;
+        if (kStats) c0 = __builtin_amdgcn_s_memtime();
+        const uint32_t r = fetch_chunk(P, home, lane);
+        if (kStats) { fetch_clk += __builtin_amdgcn_s_memtime() - c0; ++n_chunk; }
+        return r;
+    };
+    for (uint32_t chunk = fetch(); chunk < P.n_chunks; chunk = fetch()) {
+#pragma unroll 1
+        for (uint32_t t = chunk * kChunkTiles; t < (chunk + 1) * kChunkTiles && t < P.tiles_x * P.tiles_y; ++t) {
+            const uint32_t ty = t / P.tiles_x, tx = t - ty * P.tiles_x;
+            const uint32_t i = tx * 8 + (lane & 7), lr = ty * 8 + (lane >> 3);
+            bool job = false;
+            Hit h{0, 0.f, 0.f, 0.f};
+            F3 so{0.f, 0.f, 0.f};
+            if (i < P.W && lr < P.local_rows) {
+                const F3 view = primary_dir(P, i, global_row(P, lr));
+                const bool hit = trace<false, kStats, 64>(P, eye, view, stk, h, n_pairs, n_tests, overflow);
+                if (P.rec_prim) {
+                    const size_t px = size_t(lr) * P.W + i;
+                    P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
+                    P.rec_tuv[3 * px] = hit ? h.t : 0.f; P.rec_tuv[3 * px + 1] = hit ? h.u : 0.f; P.rec_tuv[3 * px + 2] = hit ? h.v : 0.f;
+                    P.rec_shadow[px] = -1;
+                }
+                if (!hit) {
+                    store_pixel(P, lr, i, 0.f, 0.f, 0.f);            // render.hpp:116-117
+                } else {
+                    ++hits;
+                    const TriV tr = load_tri(P.tris + h.slot);
+                    const F3 normal = normalize(tr.n);
+                    if (kMode == CERES_MODE_PRIMARY) {               // render.hpp:123-125
+                        store_pixel(P, lr, i, fabsf(normal.x), fabsf(normal.y), fabsf(normal.z));
+                    } else {                                         // render.hpp:127-133
+                        const F3 p1 = tr.p0 - tr.e1, p2 = tr.p0 + tr.e2;
+                        F3 p = tr.p0 * h.u + p1 * h.v + p2 * (1 - h.u - h.v);
+                        const float scale = -0.00001;
+                        so = p + normal * scale;
+                        job = true;
+                    }
+                }
+            }
+            if (kMode == CERES_MODE_FULL) {
+                const unsigned long long m = __ballot(job);
+                if (job) {                                           // append to the wave's LDS queue
+                    const uint32_t e = qn + __popcll(m & ((1ull << lane) - 1ull));
+                    q[e] = lr * P.W + i; q[kQueue + e] = h.slot;
+                    q[2 * kQueue + e] = __float_as_uint(h.u); q[3 * kQueue + e] = __float_as_uint(h.v);
+                    q[4 * kQueue + e] = __float_as_uint(so.x); q[5 * kQueue + e] = __float_as_uint(so.y);
+                    q[6 * kQueue + e] = __float_as_uint(so.z);
+                }
+                qn += __popcll(m);
+                __builtin_amdgcn_wave_barrier();
+                if (qn >= 64) {                                      // a full wavefront of shadow rays
+                    qn -= 64;
+                    if (kStats) ++n_batch;
+                    shade_queued<kStats>(P, q, qn, 64, lane, stk, occluded, traced, n_pairs, n_tests, overflow);
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+        }
+    }
+    if (kMode == CERES_MODE_FULL && qn > 0)
+        shade_queued<kStats>(P, q, 0, qn, lane, stk, occluded, traced, n_pairs, n_tests, overflow);
+    // one set of counter atomics per wavefront
+    const uint32_t wh = wave_sum(hits + occluded), wq = wave_sum(traced);
+    const uint32_t shard = wave_id % kShards;
+    if (lane == 0) {
+        if (wh) atomicAdd(&P.shards[shard].hits, (unsigned long long)wh);
+        if (wq) atomicAdd(&P.shards[shard].queued, wq);
+    }
+    if (kStats) {
+        const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
+        if (lane == 0) {
+            atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
+            atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
+            if (P.wave_log) {
+                unsigned long long* w = P.wave_log + 8 * size_t(wave_id);
+                uint32_t xcc = 0, hw = 0;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                w[0] = t_begin; w[1] = __builtin_amdgcn_s_memrealtime(); w[2] = n_chunk; w[3] = n_batch;
+                w[4] = fetch_clk; w[5] = wp; w[6] = (unsigned long long)xcc << 32 | hw; w[7] = wave_sum(traced);
+            }
+        }
     }
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
 }
@@ -385,6 +575,11 @@ struct ceres_scene {
     size_t px_cap = 0;
     hipStream_t stream = nullptr;
     int num_cus = 256;
+    unsigned long long* d_wave_log = nullptr;   // stats scenes: per-wave diagnostic records
+    size_t wave_log_waves = 0, last_grid_waves = 0;
+    int variant = 0;                   // kVariantWave (default), kVariantTwoPass / kVariantFrame via CERES_KERNEL
+    int frame_blocks_per_cu[4] = {0, 0, 0, 0};
+    uint32_t tiles_per_wave = 1;       // primary kernel (wave variant): 8x8 tiles per wavefront
     // optional per-kernel device timing (bench.py roofline leg)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -392,6 +587,8 @@ struct ceres_scene {
 };
 
 namespace {
+
+constexpr int kVariantWave = 0, kVariantTwoPass = 1, kVariantFrame = 2;
 
 #define HIP_TRY(expr)                                                                         \
     do {                                                                                      \
@@ -406,9 +603,9 @@ void scene_release(ceres_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     dfree(s->d_pairs); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
-    dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
+    dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
-    for (auto e : s->ev_used) (void)hipEventDestroy(e);
+    for (auto e : s->ev_used) if (e) (void)hipEventDestroy(e);
     s->ev_pool.clear(); s->ev_used.clear();
     if (s->stream) (void)hipStreamDestroy(s->stream);
     s->stream = nullptr;
@@ -514,10 +711,12 @@ int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode
     const size_t rows = local_rows_of(H, t.row_block, t.rank, t.world);
     if (W * rows > 0xffffffffull) return set_error(CERES_EINVAL, "render: more than 2^32 pixels per rank");
     HIP_TRY(hipSetDevice(s->device));
+    const bool twopass = s->variant != kVariantFrame;
     const uint32_t bx = uint32_t((W + 15) / 16), by = uint32_t((rows + 15) / 16);
     const size_t nblocks = size_t(bx) * by;
     const uint32_t cap = uint32_t(((nblocks + kShards - 1) / kShards) * dev::kBlock);
-    if (int rc = ensure_workspace(s, size_t(cap) * kShards, 0, false, false)) return rc;
+    if (twopass)
+        if (int rc = ensure_workspace(s, size_t(cap) * kShards, 0, false, false)) return rc;
 
     KParams P{};
     std::memcpy(P.eye, basis12, 12); std::memcpy(P.dir, basis12 + 3, 12);
@@ -528,6 +727,8 @@ int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode
     P.stack_entries = s->stack_entries;
     P.root_leaf_count = s->root_leaf_count; P.root_leaf_first = s->root_leaf_first;
     P.shard_capacity = cap;
+    P.tiles_x = uint32_t((W + 7) / 8); P.tiles_y = uint32_t((rows + 7) / 8);
+    P.n_chunks = uint32_t((size_t(P.tiles_x) * P.tiles_y + dev::kChunkTiles - 1) / dev::kChunkTiles);
     P.pairs = s->d_pairs; P.tris = s->d_tris; P.orig = s->d_orig; P.norms = s->d_norms;
     P.pixels = d_pixels; P.rgb8 = d_rgb8; P.jobs = s->d_jobs; P.shards = s->d_shards;
     P.rec_prim = d_rec_prim; P.rec_tuv = d_rec_tuv; P.rec_shadow = d_rec_shadow;
@@ -535,8 +736,6 @@ int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode
         return set_error(CERES_EINVAL, "render: hit records need all three arrays");
 
     const bool stats = (s->flags & CERES_SCENE_STATS) != 0;
-    const size_t lds_primary = (size_t(s->stack_entries) * dev::kBlock + 16) * 4;
-    const size_t lds_shadow = (size_t(s->stack_entries) * dev::kBlock + 48) * 4;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (s->timing) {
         while (s->ev_pool.size() < 3) { hipEvent_t e; HIP_TRY(hipEventCreate(&e)); s->ev_pool.push_back(e); }
@@ -547,25 +746,71 @@ int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode
     }
     HIP_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, stream));
     if (e0) HIP_TRY(hipEventRecord(e0, stream));
-    const dim3 grid(bx, by), block(dev::kBlock);
-    if (mode == CERES_MODE_PRIMARY) {
-        if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, true>), grid, block, lds_primary, stream, P);
-        else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, false>), grid, block, lds_primary, stream, P);
-    } else {
-        if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, true>), grid, block, lds_primary, stream, P);
-        else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, false>), grid, block, lds_primary, stream, P);
-    }
-    HIP_TRY(hipGetLastError());
-    if (e1) HIP_TRY(hipEventRecord(e1, stream));
-    if (mode == CERES_MODE_FULL) {
-        const size_t max_jobs = W * rows;
-        const size_t want = (max_jobs + dev::kBlock - 1) / dev::kBlock;
-        const uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, size_t(s->num_cus) * 8)));
-        if (stats) hipLaunchKernelGGL((dev::ceres_shadow<true>), dim3(sgrid), block, lds_shadow, stream, P);
-        else hipLaunchKernelGGL((dev::ceres_shadow<false>), dim3(sgrid), block, lds_shadow, stream, P);
+    if (!twopass) {
+        // persistent frame kernel: one resident grid of independent wavefronts
+        const size_t lds = size_t(dev::kFrameBlock / 64) * (size_t(s->stack_entries) * 64 + dev::kQueueWords) * 4;
+        const int mi = (mode == CERES_MODE_PRIMARY ? 1 : 0) * 2 + (stats ? 1 : 0);
+        const void* fn[4] = {reinterpret_cast<const void*>(dev::ceres_frame<CERES_MODE_FULL, false>),
+                             reinterpret_cast<const void*>(dev::ceres_frame<CERES_MODE_FULL, true>),
+                             reinterpret_cast<const void*>(dev::ceres_frame<CERES_MODE_PRIMARY, false>),
+                             reinterpret_cast<const void*>(dev::ceres_frame<CERES_MODE_PRIMARY, true>)};
+        if (s->frame_blocks_per_cu[mi] <= 0) {
+            int nb = 0;
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn[mi], dev::kFrameBlock, lds));
+            s->frame_blocks_per_cu[mi] = std::max(1, nb);
+        }
+        const size_t want_waves = size_t(P.n_chunks);                 // never more waves than chunks
+        size_t grid = size_t(s->num_cus) * size_t(s->frame_blocks_per_cu[mi]);
+        grid = std::max<size_t>(1, std::min(grid, (want_waves + 1) / 2));
+        if (stats && s->wave_log_waves < grid * 2) {
+            dfree(s->d_wave_log);
+            HIP_TRY(hipMalloc(&s->d_wave_log, grid * 2 * 64));
+            s->wave_log_waves = grid * 2;
+        }
+        P.wave_log = stats ? s->d_wave_log : nullptr;
+        s->last_grid_waves = grid * 2;
+        switch (mi) {
+            case 0: hipLaunchKernelGGL((dev::ceres_frame<CERES_MODE_FULL, false>), dim3(uint32_t(grid)), dim3(dev::kFrameBlock), lds, stream, P); break;
+            case 1: hipLaunchKernelGGL((dev::ceres_frame<CERES_MODE_FULL, true>), dim3(uint32_t(grid)), dim3(dev::kFrameBlock), lds, stream, P); break;
+            case 2: hipLaunchKernelGGL((dev::ceres_frame<CERES_MODE_PRIMARY, false>), dim3(uint32_t(grid)), dim3(dev::kFrameBlock), lds, stream, P); break;
+            default: hipLaunchKernelGGL((dev::ceres_frame<CERES_MODE_PRIMARY, true>), dim3(uint32_t(grid)), dim3(dev::kFrameBlock), lds, stream, P); break;
+        }
         HIP_TRY(hipGetLastError());
+        if (e1) HIP_TRY(hipEventRecord(e1, stream));
+        if (e2) { s->ev_used.back() = nullptr; s->ev_pool.push_back(e2); }   // single kernel: no shadow interval
+    } else {
+        const bool w64 = s->variant == kVariantWave;
+        const int bs = w64 ? 64 : dev::kBlock;
+        const size_t lds = size_t(s->stack_entries) * bs * 4;
+        dim3 grid(uint32_t((W + 15) / 16), uint32_t((rows + 15) / 16)), block(bs);
+        if (w64) grid = dim3(uint32_t((size_t(P.tiles_x) * P.tiles_y + s->tiles_per_wave - 1) / s->tiles_per_wave));
+#define CERES_PRIMARY(MODE, ST, BS) hipLaunchKernelGGL((dev::ceres_primary<MODE, ST, BS>), grid, block, lds, stream, P)
+        if (w64) {
+            if (mode == CERES_MODE_PRIMARY) { if (stats) CERES_PRIMARY(CERES_MODE_PRIMARY, true, 64); else CERES_PRIMARY(CERES_MODE_PRIMARY, false, 64); }
+            else { if (stats) CERES_PRIMARY(CERES_MODE_FULL, true, 64); else CERES_PRIMARY(CERES_MODE_FULL, false, 64); }
+        } else {
+            if (mode == CERES_MODE_PRIMARY) { if (stats) CERES_PRIMARY(CERES_MODE_PRIMARY, true, 256); else CERES_PRIMARY(CERES_MODE_PRIMARY, false, 256); }
+            else { if (stats) CERES_PRIMARY(CERES_MODE_FULL, true, 256); else CERES_PRIMARY(CERES_MODE_FULL, false, 256); }
+        }
+#undef CERES_PRIMARY
+        HIP_TRY(hipGetLastError());
+        if (e1) HIP_TRY(hipEventRecord(e1, stream));
+        if (mode == CERES_MODE_FULL) {
+            const size_t max_jobs = W * rows;
+            const size_t want = (max_jobs + bs - 1) / bs;
+            const size_t cap_blocks = size_t(s->num_cus) * (w64 ? 32 : 8);
+            const uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, cap_blocks)));
+            if (w64) {
+                if (stats) hipLaunchKernelGGL((dev::ceres_shadow<true, 64>), dim3(sgrid), block, lds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_shadow<false, 64>), dim3(sgrid), block, lds, stream, P);
+            } else {
+                if (stats) hipLaunchKernelGGL((dev::ceres_shadow<true, 256>), dim3(sgrid), block, lds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_shadow<false, 256>), dim3(sgrid), block, lds, stream, P);
+            }
+            HIP_TRY(hipGetLastError());
+        }
+        if (e2) HIP_TRY(hipEventRecord(e2, stream));
     }
-    if (e2) HIP_TRY(hipEventRecord(e2, stream));
     if (d_counters) {
         hipLaunchKernelGGL(dev::ceres_finalize, dim3(1), dim3(64), 0, stream, s->d_shards, uint64_t(W * rows), d_counters);
         HIP_TRY(hipGetLastError());
@@ -579,7 +824,7 @@ extern "C" {
 
 const char* ceres_last_error(void) { return error_buffer(); }
 const char* ceres_version(void) { return "ceres-mi355x 0.1 (gfx950)"; }
-const char* ceres_kernel_names(void) { return "ceres_primary,ceres_shadow,ceres_finalize"; }
+const char* ceres_kernel_names(void) { return "ceres_frame,ceres_primary,ceres_shadow,ceres_finalize"; }
 
 size_t ceres_tiling_local_rows(size_t height, const ceres_tiling* t) {
     if (!t) return height;
@@ -606,6 +851,9 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     s->device = device; s->flags = flags; s->n_tri = n_tri; s->n_pairs = pairs.size();
     s->depth = depth; s->root_leaf_count = rlc; s->root_leaf_first = rlf;
     s->stack_entries = std::max<uint32_t>(1, depth);                 // stack <= depth - 1 entries
+    if (const char* v = std::getenv("CERES_KERNEL"))
+        s->variant = std::strcmp(v, "twopass") == 0 ? kVariantTwoPass : std::strcmp(v, "frame") == 0 ? kVariantFrame : kVariantWave;
+    if (const char* v = std::getenv("CERES_TPW")) s->tiles_per_wave = std::max(1, std::atoi(v));
     auto fail = [&](int rc) -> ceres_scene* { (void)rc; scene_release(s); delete s; return nullptr; };
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { set_error(CERES_EHIP, "no HIP device available"); return fail(0); }
@@ -715,6 +963,17 @@ int ceres_render_records(ceres_scene* s, const float basis12[12], const float su
     return CERES_OK;
 }
 
+int ceres_scene_wave_log(ceres_scene* s, uint64_t* out, size_t max_waves, size_t* n_waves) {
+    if (!s || !out || !n_waves) return set_error(CERES_EINVAL, "ceres_scene_wave_log: null argument");
+    if (!s->d_wave_log) return set_error(CERES_EINVAL, "wave log needs a CERES_SCENE_STATS scene and a persistent-kernel render");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(nullptr));
+    const size_t n = std::min(max_waves, s->last_grid_waves);
+    HIP_TRY(hipMemcpy(out, s->d_wave_log, n * 64, hipMemcpyDeviceToHost));
+    *n_waves = n;
+    return CERES_OK;
+}
+
 // Per-kernel device timing for the roofline leg of bench.py: while enabled, every render
 // records HIP events around ceres_primary and ceres_shadow on the caller's stream.
 int ceres_scene_set_timing(ceres_scene* s, int enable) {
@@ -731,13 +990,13 @@ int ceres_scene_read_timing(ceres_scene* s, double* primary_ms, double* shadow_m
     const size_t n = s->ev_used.size() / 3;
     for (size_t k = 0; k < n; ++k) {
         hipEvent_t e0 = s->ev_used[3 * k], e1 = s->ev_used[3 * k + 1], e2 = s->ev_used[3 * k + 2];
-        HIP_TRY(hipEventSynchronize(e2));
+        HIP_TRY(hipEventSynchronize(e2 ? e2 : e1));
         float a = 0.f, b = 0.f;
         HIP_TRY(hipEventElapsedTime(&a, e0, e1));
-        HIP_TRY(hipEventElapsedTime(&b, e1, e2));
+        if (e2) HIP_TRY(hipEventElapsedTime(&b, e1, e2));
         p += a; q += b;
     }
-    for (auto e : s->ev_used) s->ev_pool.push_back(e);
+    for (auto e : s->ev_used) if (e) s->ev_pool.push_back(e);
     s->ev_used.clear();
     if (primary_ms) *primary_ms = p;
     if (shadow_ms) *shadow_ms = q;

@@ -139,6 +139,12 @@ size_t ceres_tiling_local_rows(size_t height, const ceres_tiling* tiling);
 int ceres_scene_set_timing(ceres_scene* scene, int enable);
 int ceres_scene_read_timing(ceres_scene* scene, double* primary_ms, double* shadow_ms, uint64_t* renders);
 
+/* Diagnostic: per-wavefront records of the last persistent-kernel render of a
+ * CERES_SCENE_STATS scene, 8 x u64 each: {start, end (s_memrealtime, 100 MHz), chunks fetched,
+ * full shadow batches, shader clocks spent fetching, node pairs, xcc_id << 32 | hw_id,
+ * shadow rays traced}.  Synchronises the device. */
+int ceres_scene_wave_log(ceres_scene* scene, uint64_t* out, size_t max_waves, size_t* n_waves);
+
 /* Launch-geometry introspection for the roofline accounting in bench.py (kernel names as
  * they appear in rocprofv3 traces). */
 const char* ceres_kernel_names(void);

@@ -466,7 +466,7 @@ void oracle_camera_basis(const float eye[3], const float dir[3], const float up[
 int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const uint32_t* nodes32, size_t n_nodes,
                   const uint64_t* prim64, const float eye[3], const float basis[9], const float sun[3], int mode,
                   size_t W, size_t H, float* pixels, uint8_t* ppm, int32_t* rec_prim, float* rec_tuv,
-                  int8_t* rec_shadow, uint64_t counts[6], int threads) {
+                  int8_t* rec_shadow, uint64_t counts[6], int threads, uint32_t* rec_pairs) {
     if (n_tri == 0 || n_nodes == 0) { g_err = "empty scene"; return -1; }
     Ctx cx{reinterpret_cast<const Tri*>(tri48), reinterpret_cast<const Node*>(nodes32), prim64};
     const auto* norms = reinterpret_cast<const std::array<V3, 3>*>(norm36);
@@ -487,6 +487,7 @@ int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const u
             float v = 2 * (j + float(0.5)) / float(H) - float(1);
             V3 view = normalize(add(add(mul(IU, u), mul(IV, v)), D));
             Hit h{}; bool ovf = false;
+            const uint64_t pp0 = pp, sp0 = sp_;
             bool hit = traverse(cx, E, view, &h, &pp, &pt, &ovf);
             rays++;
             float c[3] = {0.f, 0.f, 0.f};
@@ -519,6 +520,7 @@ int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const u
             }
             size_t pix = W * j + i;
             if (rec_prim) rec_prim[pix] = rp;
+            if (rec_pairs) { rec_pairs[2 * pix] = uint32_t(pp - pp0); rec_pairs[2 * pix + 1] = uint32_t(sp_ - sp0); }
             if (rec_shadow) rec_shadow[pix] = rs;
             if (rec_tuv) { rec_tuv[3 * pix] = hit ? h.t : 0.f; rec_tuv[3 * pix + 1] = hit ? h.u : 0.f; rec_tuv[3 * pix + 2] = hit ? h.v : 0.f; }
         }

@@ -44,7 +44,7 @@ def lib():
         L.oracle_camera_basis.restype = None
         L.oracle_render.argtypes = [_fp, _fp, _sz, _u32p, _sz, _u64p, _fp, _fp, _fp, ctypes.c_int, _sz, _sz,
                                     _fp, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int32), _fp,
-                                    ctypes.POINTER(ctypes.c_int8), _u64p, ctypes.c_int]
+                                    ctypes.POINTER(ctypes.c_int8), _u64p, ctypes.c_int, _u32p]
         L.oracle_free.argtypes = [ctypes.c_void_p]
         L.oracle_free.restype = None
         _lib = L
@@ -122,7 +122,7 @@ def prepare(cfg):
     return dict(tri=tri, norm=nor, nodes=nodes, prim=prim, basis=basis)
 
 
-def render(scene, cfg, basis=None, want_pixels=True, want_ppm=True, want_records=False, threads=0):
+def render(scene, cfg, basis=None, want_pixels=True, want_ppm=True, want_records=False, threads=0, want_pairs=False):
     L = lib()
     W, H = cfg["W"], cfg["H"]
     basis = scene["basis"] if basis is None else np.asarray(basis, np.float32)
@@ -134,17 +134,21 @@ def render(scene, cfg, basis=None, want_pixels=True, want_ppm=True, want_records
     tuv = np.zeros(3 * W * H, np.float32) if want_records else None
     rs = np.zeros(W * H, np.int8) if want_records else None
     counts = np.zeros(6, np.uint64)
+    pairs = np.zeros(2 * W * H, np.uint32) if want_pairs else None
     tri, nor, nodes, prim = scene["tri"], scene["norm"], scene["nodes"], scene["prim"]
     _check(L.oracle_render(_ptr(tri, ctypes.c_float), _ptr(nor, ctypes.c_float), tri.shape[0],
                            _ptr(nodes, ctypes.c_uint32), nodes.shape[0], _ptr(prim, ctypes.c_uint64),
                            _ptr(eye, ctypes.c_float), _ptr(basis, ctypes.c_float), _ptr(sun, ctypes.c_float),
                            1 if cfg["mode"] == "primary" else 0, W, H, _ptr(px, ctypes.c_float),
                            _ptr(ppm, ctypes.c_uint8), _ptr(rp, ctypes.c_int32), _ptr(tuv, ctypes.c_float),
-                           _ptr(rs, ctypes.c_int8), _ptr(counts, ctypes.c_uint64), int(threads)))
+                           _ptr(rs, ctypes.c_int8), _ptr(counts, ctypes.c_uint64), int(threads),
+                           _ptr(pairs, ctypes.c_uint32)))
     out = dict(rays=int(counts[0]), hits=int(counts[1]), primary_pairs=int(counts[2]), primary_tests=int(counts[3]),
                shadow_pairs=int(counts[4]), shadow_tests=int(counts[5]), pixels=px, ppm=ppm)
     if want_records:
         out.update(prim=rp, tuv=tuv.reshape(-1, 3), shadow=rs)
+    if want_pairs:
+        out["pairs_per_pixel"] = pairs.reshape(-1, 2)      # (primary, shadow) node-pair visits
     return out
 
 
