@@ -257,7 +257,7 @@ def main():
                        + (" + RCCL gather to rank 0" if world > 1 else ""),
                        "float_framebuffer": d_px is not None},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
-            "kernel_variant": os.environ.get("CERES_KERNEL", "frame"),
+            "kernel_variant": os.environ.get("CERES_KERNEL", "twopass"),
         }
         print(json.dumps(line), flush=True)
     scene.close()

@@ -41,6 +41,7 @@
 
 #pragma clang fp contract(off)
 
+
 namespace ceres {
 
 char* error_buffer() {
@@ -75,9 +76,8 @@ struct Hit { uint32_t slot; float t, u, v; };
 
 // Triangle::intersect (triangle.hpp:95-115, left-handed normal): on an accepted hit updates
 // best / tmax (closest hit keeps the LAST accepted hit with t <= tmax, intersect_leaf :54-60).
-__device__ __forceinline__ bool tri_test(const Tri48* tp, F3 o, F3 d, float tmin, float tmax, float& t_out,
+__device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin, float tmax, float& t_out,
                                          float& u_out, float& v_out) {
-    const TriV tr = load_tri(tp);
     const F3 c = tr.p0 - o;
     const F3 r = cross(d, c);
     const float inv_det = 1.0f / dot(tr.n, d);
@@ -104,9 +104,19 @@ __device__ __forceinline__ bool tri_test(const Tri48* tp, F3 o, F3 d, float tmin
 // whenever y is not NaN (y is tmin / tmax / a previous robust_max -- never NaN) up to the
 // sign of zero, which no comparison below can observe; likewise robust_min and fminf.  The
 // slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
-template <bool kAnyHit, bool kStats, int kStride = kBlock>
+// Diagnostic section clocks (stats builds only): wave-uniform s_memtime sums per trace().
+struct Stamps { unsigned long long box = 0, leaf = 0, next = 0, iters = 0; };
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
+template <bool kAnyHit, bool kStats, int kStride = kBlock, bool kPF = false>
 __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* stk, Hit& best,
-                                      uint32_t& n_pairs, uint32_t& n_tests, bool& overflow) {
+                                      uint32_t& n_pairs, uint32_t& n_tests, bool& overflow, Stamps* ss = nullptr) {
     const float tmin = 0.0f;
     float tmax = FLT_MAX;                                           // ray.hpp:17-21
     bool have = false;
@@ -114,7 +124,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         if (kStats) n_tests += P.root_leaf_count;
         for (uint32_t k = P.root_leaf_first; k < P.root_leaf_first + P.root_leaf_count; ++k) {
             float t, u, v;
-            if (tri_test(P.tris + k, o, d, tmin, tmax, t, u, v)) {
+            if (tri_test(load_tri(P.tris + k), o, d, tmin, tmax, t, u, v)) {
                 best = {k, t, u, v}; have = true;
                 if (kAnyHit) return true;
                 tmax = t;
@@ -125,9 +135,12 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
     auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };   // vector.hpp:69-74
     const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
     const float sx = (-o.x) * ix, sy = (-o.y) * iy, sz = (-o.z) * iz;
-    uint32_t cur = 0, sp = 0;                                         // pair of the root's children (:81)
+    uint32_t sp = 0;
+    uint32_t cur = 0;                                                 // pair of the root's children (:81)
+    unsigned long long c0 = 0, c1 = 0, c2 = 0;
     while (true) {                                                    // :82-123
         if (kStats) ++n_pairs;
+        if (kStats && ss) c0 = stamp();
         const float4* q = reinterpret_cast<const float4*>(P.pairs + cur);
         const float4 A = q[0], B = q[1], C = q[2];
         const uint4 L = reinterpret_cast<const uint4*>(q)[3];
@@ -143,7 +156,9 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         const float re = fmaxf(fminf(r0, r1), fmaxf(fminf(r2, r3), fmaxf(fminf(r4, r5), tmin)));
         const float rx = fminf(fmaxf(r0, r1), fminf(fmaxf(r2, r3), fminf(fmaxf(r4, r5), tmax)));
         const bool hit_l = le <= lx, hit_r = re <= rx;
-        // leaves of this step, left then right (intersect_leaf on each, :89-107)
+        if (kStats && ss) { volatile bool keep = hit_l | hit_r; (void)keep; c1 = stamp(); }
+        // leaves of this step, left then right (intersect_leaf on each, :89-107), one loop so a
+        // wavefront runs max(left + right) trips rather than max(left) + max(right)
         uint32_t k = 0, k_end = 0, k2 = 0, k2_end = 0;
         if (hit_l && L.x) { k = L.y; k_end = L.y + L.x; }
         if (hit_r && L.z) { k2 = L.w; k2_end = L.w + L.z; }
@@ -151,12 +166,13 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         while (k < k_end || k2 < k2_end) {
             const uint32_t idx = k < k_end ? k++ : k2++;
             float t, u, v;
-            if (tri_test(P.tris + idx, o, d, tmin, tmax, t, u, v)) {
+            if (tri_test(load_tri(P.tris + idx), o, d, tmin, tmax, t, u, v)) {
                 best = {idx, t, u, v}; have = true;
-                if (kAnyHit) return true;
+                if (kAnyHit) { if (kStats && ss) { ss->box += c1 - c0; ss->iters++; } return true; }
                 tmax = t;
             }
         }
+        if (kStats && ss) { c2 = stamp(); ss->box += c1 - c0; ss->leaf += c2 - c1; ss->iters++; }
         const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
         if (go_l && go_r) {                                           // near first, ties left (:109-115)
             const bool swap = le > re;
@@ -167,10 +183,11 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         } else if (go_l || go_r) {
             cur = go_l ? L.y : L.w;                                   // :115-117
         } else {
-            if (sp == 0) break;                                       // :118-121
+            if (sp == 0) { if (kStats && ss) ss->next += stamp() - c2; break; }   // :118-121
             --sp;
             cur = stk[sp * kStride];
         }
+        if (kStats && ss) ss->next += stamp() - c2;
     }
     return have;
 }
@@ -233,7 +250,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // ---------------------------------------------------------------- primary kernel
 // kBS threads per workgroup (64: one 8x8 tile per workgroup; 256: 16x16 pixels as 2x2 wave
 // tiles).  Every wavefront is independent: no workgroup barrier, one queue atomic per wave.
-template <int kMode, bool kStats, int kBS>
+template <int kMode, bool kStats, int kBS, bool kPF>
 __device__ __forceinline__ void primary_tile(const KParams& P, uint32_t* stk, uint32_t lane, uint32_t wave_id,
                                              uint32_t i, uint32_t lr) {
     const bool active = i < P.W && lr < P.local_rows;
@@ -246,7 +263,7 @@ __device__ __forceinline__ void primary_tile(const KParams& P, uint32_t* stk, ui
         const uint32_t j = global_row(P, lr);
         const F3 eye{P.eye[0], P.eye[1], P.eye[2]};
         const F3 view = primary_dir(P, i, j);
-        hit = trace<false, kStats, kBS>(P, eye, view, stk, h, n_pairs, n_tests, overflow);
+        hit = trace<false, kStats, kBS, kPF>(P, eye, view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
             const size_t px = size_t(lr) * P.W + i;
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
@@ -299,7 +316,7 @@ __device__ __forceinline__ void primary_tile(const KParams& P, uint32_t* stk, ui
 }
 
 
-template <int kMode, bool kStats, int kBS>
+template <int kMode, bool kStats, int kBS, bool kPF>
 __global__ __launch_bounds__(kBS) void ceres_primary(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -309,17 +326,17 @@ __global__ __launch_bounds__(kBS) void ceres_primary(const KParams P) {
         const uint32_t n_tiles = P.tiles_x * P.tiles_y;
         for (uint32_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
             const uint32_t ty = t / P.tiles_x, tx = t - ty * P.tiles_x;
-            primary_tile<kMode, kStats, kBS>(P, stk, lane, t, tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
+            primary_tile<kMode, kStats, kBS, kPF>(P, stk, lane, t, tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
         }
     } else {
         const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
         const uint32_t lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-        primary_tile<kMode, kStats, kBS>(P, stk, lane, (blockIdx.y * gridDim.x + blockIdx.x) * (kBS / 64) + wave, i, lr);
+        primary_tile<kMode, kStats, kBS, kPF>(P, stk, lane, (blockIdx.y * gridDim.x + blockIdx.x) * (kBS / 64) + wave, i, lr);
     }
 }
 
 // ---------------------------------------------------------------- shadow kernel
-template <bool kStats, int kBS>
+template <bool kStats, int kBS, bool kPF>
 __global__ __launch_bounds__(kBS) void ceres_shadow(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -333,6 +350,9 @@ __global__ __launch_bounds__(kBS) void ceres_shadow(const KParams P) {
     const F3 sun{P.sun[0], P.sun[1], P.sun[2]};
     uint32_t occluded = 0, n_pairs = 0, n_tests = 0;
     bool overflow = false;
+    unsigned long long t_begin = 0;
+    Stamps stamps;
+    if (kStats) t_begin = __builtin_amdgcn_s_memrealtime();
     for (uint32_t g = blockIdx.x * kBS + tid; g < total; g += gridDim.x * kBS) {
         uint32_t s = 0;                                              // shard holding global job g
 #pragma unroll
@@ -345,7 +365,8 @@ __global__ __launch_bounds__(kBS) void ceres_shadow(const KParams P) {
         const F3 o{J1.x, J1.y, J1.z};
         const F3 sun_line = normalize(sun - o);                      // render.hpp:135
         Hit h2{0, 0.f, 0.f, 0.f};
-        const bool blocked = trace<true, kStats, kBS>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow);
+        const bool blocked = trace<true, kStats, kBS, kPF>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow,
+                                                           kStats ? &stamps : nullptr);
         const uint32_t lr = pix / P.W, i = pix - lr * P.W;
         if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
         if (blocked) {                                               // render.hpp:147-150
@@ -363,9 +384,20 @@ __global__ __launch_bounds__(kBS) void ceres_shadow(const KParams P) {
     if (lane == 0 && wo) atomicAdd(&P.shards[shard].hits, (unsigned long long)wo);
     if (kStats) {
         const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
+        uint32_t mp = n_pairs;                                       // max chain in the wave
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mp = max(mp, __shfl_xor(mp, off, 64));
         if (lane == 0) {
             atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
             atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
+            if (P.wave_log) {                                        // diagnostic wave timeline
+                unsigned long long* w = P.wave_log + 8 * size_t(blockIdx.x * (kBS / 64) + wave);
+                uint32_t xcc = 0, hw = 0;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                w[0] = t_begin; w[1] = __builtin_amdgcn_s_memrealtime(); w[2] = mp; w[3] = stamps.iters;
+                w[4] = stamps.box; w[5] = stamps.leaf; w[6] = stamps.next; w[7] = wp;
+            }
         }
     }
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
@@ -577,9 +609,10 @@ struct ceres_scene {
     int num_cus = 256;
     unsigned long long* d_wave_log = nullptr;   // stats scenes: per-wave diagnostic records
     size_t wave_log_waves = 0, last_grid_waves = 0;
-    int variant = 0;                   // kVariantWave (default), kVariantTwoPass / kVariantFrame via CERES_KERNEL
+    int variant = 0;                   // kVariantTwoPass (default); kVariantWave / kVariantFrame via CERES_KERNEL
     int frame_blocks_per_cu[4] = {0, 0, 0, 0};
     uint32_t tiles_per_wave = 1;       // primary kernel (wave variant): 8x8 tiles per wavefront
+    bool pf_primary = false, pf_shadow = false; // (reserved variant bit, currently identical code)
     // optional per-kernel device timing (bench.py roofline leg)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -588,7 +621,7 @@ struct ceres_scene {
 
 namespace {
 
-constexpr int kVariantWave = 0, kVariantTwoPass = 1, kVariantFrame = 2;
+constexpr int kVariantTwoPass = 0, kVariantWave = 1, kVariantFrame = 2;
 
 #define HIP_TRY(expr)                                                                         \
     do {                                                                                      \
@@ -784,14 +817,16 @@ int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode
         const size_t lds = size_t(s->stack_entries) * bs * 4;
         dim3 grid(uint32_t((W + 15) / 16), uint32_t((rows + 15) / 16)), block(bs);
         if (w64) grid = dim3(uint32_t((size_t(P.tiles_x) * P.tiles_y + s->tiles_per_wave - 1) / s->tiles_per_wave));
-#define CERES_PRIMARY(MODE, ST, BS) hipLaunchKernelGGL((dev::ceres_primary<MODE, ST, BS>), grid, block, lds, stream, P)
+#define CERES_PRIMARY(MODE, ST, BS, PF) hipLaunchKernelGGL((dev::ceres_primary<MODE, ST, BS, PF>), grid, block, lds, stream, P)
+#define CERES_PRIMARY_PF(MODE, ST, BS) do { if (s->pf_primary) CERES_PRIMARY(MODE, ST, BS, true); else CERES_PRIMARY(MODE, ST, BS, false); } while (0)
         if (w64) {
-            if (mode == CERES_MODE_PRIMARY) { if (stats) CERES_PRIMARY(CERES_MODE_PRIMARY, true, 64); else CERES_PRIMARY(CERES_MODE_PRIMARY, false, 64); }
-            else { if (stats) CERES_PRIMARY(CERES_MODE_FULL, true, 64); else CERES_PRIMARY(CERES_MODE_FULL, false, 64); }
+            if (mode == CERES_MODE_PRIMARY) { if (stats) CERES_PRIMARY_PF(CERES_MODE_PRIMARY, true, 64); else CERES_PRIMARY_PF(CERES_MODE_PRIMARY, false, 64); }
+            else { if (stats) CERES_PRIMARY_PF(CERES_MODE_FULL, true, 64); else CERES_PRIMARY_PF(CERES_MODE_FULL, false, 64); }
         } else {
-            if (mode == CERES_MODE_PRIMARY) { if (stats) CERES_PRIMARY(CERES_MODE_PRIMARY, true, 256); else CERES_PRIMARY(CERES_MODE_PRIMARY, false, 256); }
-            else { if (stats) CERES_PRIMARY(CERES_MODE_FULL, true, 256); else CERES_PRIMARY(CERES_MODE_FULL, false, 256); }
+            if (mode == CERES_MODE_PRIMARY) { if (stats) CERES_PRIMARY_PF(CERES_MODE_PRIMARY, true, 256); else CERES_PRIMARY_PF(CERES_MODE_PRIMARY, false, 256); }
+            else { if (stats) CERES_PRIMARY_PF(CERES_MODE_FULL, true, 256); else CERES_PRIMARY_PF(CERES_MODE_FULL, false, 256); }
         }
+#undef CERES_PRIMARY_PF
 #undef CERES_PRIMARY
         HIP_TRY(hipGetLastError());
         if (e1) HIP_TRY(hipEventRecord(e1, stream));
@@ -800,13 +835,23 @@ int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode
             const size_t want = (max_jobs + bs - 1) / bs;
             const size_t cap_blocks = size_t(s->num_cus) * (w64 ? 32 : 8);
             const uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, cap_blocks)));
-            if (w64) {
-                if (stats) hipLaunchKernelGGL((dev::ceres_shadow<true, 64>), dim3(sgrid), block, lds, stream, P);
-                else hipLaunchKernelGGL((dev::ceres_shadow<false, 64>), dim3(sgrid), block, lds, stream, P);
-            } else {
-                if (stats) hipLaunchKernelGGL((dev::ceres_shadow<true, 256>), dim3(sgrid), block, lds, stream, P);
-                else hipLaunchKernelGGL((dev::ceres_shadow<false, 256>), dim3(sgrid), block, lds, stream, P);
+            if (stats) {
+                const size_t waves = size_t(sgrid) * (bs / 64);
+                if (s->wave_log_waves < waves) {
+                    dfree(s->d_wave_log);
+                    HIP_TRY(hipMalloc(&s->d_wave_log, waves * 64));
+                    s->wave_log_waves = waves;
+                }
+                HIP_TRY(hipMemsetAsync(s->d_wave_log, 0, waves * 64, stream));
+                P.wave_log = s->d_wave_log;
+                s->last_grid_waves = waves;
             }
+#define CERES_SHADOW(ST, BS, PF) hipLaunchKernelGGL((dev::ceres_shadow<ST, BS, PF>), dim3(sgrid), block, lds, stream, P)
+#define CERES_SHADOW_PF(ST, BS) do { if (s->pf_shadow) CERES_SHADOW(ST, BS, true); else CERES_SHADOW(ST, BS, false); } while (0)
+            if (w64) { if (stats) CERES_SHADOW_PF(true, 64); else CERES_SHADOW_PF(false, 64); }
+            else { if (stats) CERES_SHADOW_PF(true, 256); else CERES_SHADOW_PF(false, 256); }
+#undef CERES_SHADOW_PF
+#undef CERES_SHADOW
             HIP_TRY(hipGetLastError());
         }
         if (e2) HIP_TRY(hipEventRecord(e2, stream));
@@ -852,8 +897,12 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     s->depth = depth; s->root_leaf_count = rlc; s->root_leaf_first = rlf;
     s->stack_entries = std::max<uint32_t>(1, depth);                 // stack <= depth - 1 entries
     if (const char* v = std::getenv("CERES_KERNEL"))
-        s->variant = std::strcmp(v, "twopass") == 0 ? kVariantTwoPass : std::strcmp(v, "frame") == 0 ? kVariantFrame : kVariantWave;
+        s->variant = std::strcmp(v, "wave") == 0 ? kVariantWave : std::strcmp(v, "frame") == 0 ? kVariantFrame : kVariantTwoPass;
     if (const char* v = std::getenv("CERES_TPW")) s->tiles_per_wave = std::max(1, std::atoi(v));
+    if (const char* v = std::getenv("CERES_PF")) {                   // "pf_primary pf_shadow" bits, e.g. "01"
+        s->pf_primary = v[0] == '1';
+        s->pf_shadow = v[0] && v[1] ? v[1] == '1' : s->pf_primary;
+    }
     auto fail = [&](int rc) -> ceres_scene* { (void)rc; scene_release(s); delete s; return nullptr; };
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { set_error(CERES_EHIP, "no HIP device available"); return fail(0); }

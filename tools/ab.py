@@ -30,18 +30,24 @@ def main():
     mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
     scenes = {}
     for v in variants:
-        kern, _, tpw = v.partition(":")          # e.g. "wave:4" = wave variant, 4 tiles per wave
-        os.environ["CERES_KERNEL"] = kern
-        os.environ["CERES_TPW"] = tpw or "1"
+        # "kernel[:tiles_per_wave[:pf_bits]]", e.g. "wave:1:01" = wave variant, prefetch in shadow only
+        parts = v.split(":")
+        os.environ["CERES_KERNEL"] = parts[0]
+        os.environ["CERES_TPW"] = parts[1] if len(parts) > 1 and parts[1] else "1"
+        if len(parts) > 2:
+            os.environ["CERES_PF"] = parts[2]
+        else:
+            os.environ.pop("CERES_PF", None)
         scenes[v] = pkg.Scene(mesh, bvh)
     res = {v: [] for v in variants}
     ok = {}
     for v, sc in scenes.items():
         _, rgb, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=False)
         ok[v] = hashlib.sha256(pkg.ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
+    want_px = os.environ.get("AB_FLOAT", "1") == "1"
     for _ in range(rounds):
         for v, sc in scenes.items():
-            _, _, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=True, want_rgb8=True)
+            _, _, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=want_px, want_rgb8=True)
             res[v].append(st["ms"])
     out = {v: {"median_ms": round(float(np.median(r)), 4), "min_ms": round(float(np.min(r)), 4),
                "mrays_s_median": round(meta["exact"]["rays"] / (np.median(r) * 1e3), 1), "parity": ok[v]}

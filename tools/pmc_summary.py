@@ -27,7 +27,7 @@ def short(name):
 
 def load(prof_dir):
     acc = defaultdict(lambda: defaultdict(list))
-    for f in glob.glob(os.path.join(prof_dir, "pmc_*", "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(prof_dir, "*", "*counter_collection.csv")):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = short(row["Kernel_Name"])
