@@ -2,23 +2,31 @@
 """bench.py -- Mrays/s of the CERES hot path on MI355X (BASELINE.json metric).
 
 Workload (default): C3 = dragon.obj 1920x1080, primary + shadow rays, static.cpp camera
-(static.cpp:38-47,72-73) -- the configuration BASELINE.json's metric is quoted on.  A step
-is one frame: ceres_primary + ceres_shadow over the rank's rows, RGB8 + float framebuffer
-written in HBM, and for N > 1 the RCCL gather of the RGB8 rows to rank 0 (one collective per
-frame).  Scene upload, OBJ load and BVH build are outside the timed region, as in the
-reference (static.cpp:129-133).  value = (primary + shadow rays of the whole frame) x steps
-/ wall time (max over ranks).  One process per GPU (torch.distributed, backend nccl = RCCL).
+(static.cpp:38-47,72-73) -- the configuration BASELINE.json's metric is quoted on.
+
+A step renders F frames (F = --frames, default = number of GPUs): the anim.cpp:76-88 orbit of
+the C3 camera + sun about z in 45-degree steps, frame 0 = C3 exactly.  So at N = 1 a step is
+exactly one C3 frame, and at N GPUs a step is N frames -- WEAK scaling, fixed work per GPU.
+Every frame's rows are interleaved over the ranks in blocks of --row-block rows (balanced
+load); each rank renders its rows of all F frames with one ceres_render_batch_device launch
+pair (ceres_primary + ceres_shadow), RGB8 + float framebuffers in HBM, then ONE RCCL gather
+per step brings the F frames' rows to rank 0, where ceres_assemble_rgb8 un-interleaves them
+into F PPM bodies.  The gather/assembly of step k overlaps the render of step k+1 (double
+buffered); the timed region ends when the last step's frames are assembled on rank 0.
+Scene upload, OBJ load and BVH build are outside the timed region, as in the reference
+(static.cpp:129-133).  value = (primary + shadow rays of all F frames) x steps / wall time
+(max over ranks).  One process per GPU (torch.distributed, backend nccl = RCCL).
 
 Also reported (rank 0):
   roofline      dominant kernel's algorithmic bytes per launch (pinned reference statistics,
                 SURVEY.md §8(d): 64 B per node-pair visit + 56 B per triangle test) / its mean
-                device duration from HIP events on the launch stream, vs 8 TB/s HBM peak;
-                traffic = rocprofv3 --pmc FETCH_SIZE (gfx950 x2 correction) per launch from
-                profiles/, when a profile of this workload is committed.
+                device duration from HIP events on the launch stream, vs 8 TB/s HBM peak, for
+                one full C3 frame on one GPU; traffic = rocprofv3 --pmc FETCH_SIZE (gfx950 x2
+                correction) per launch from profiles/pmc_summary.json.
   cpu_baseline  the REFERENCE hot path (oracle/_ref/ref_render, reference CMake flags) timed
                 on this host's cores on a bounded sample of the same workload (N = 1 only);
                 falls back to the oracle restatement if the reference binary is absent.
-  parity        sha256 of the rendered PPM vs the reference fixture.
+  parity        sha256 of frame 0's PPM vs the reference fixture, rays/hits vs the fixture.
 """
 import argparse
 import hashlib
@@ -56,6 +64,7 @@ def load_golden(name):
 
 
 def pinned_basis(meta, cfg, cam):
+    """C3 camera basis from the fixture's hex bits (never trust a host libm for parity)."""
     if meta is None:
         return cam.basis(cfg["W"], cfg["H"])
     bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
@@ -129,7 +138,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="dragon_1080")
-    ap.add_argument("--row-block", type=int, default=16)
+    ap.add_argument("--frames", type=int, default=0, help="orbit frames per step (default: number of GPUs)")
+    ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
@@ -155,49 +165,77 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     W, H = cfg["W"], cfg["H"]
+    F = args.frames or world
     mesh, bvh, cam = pkg.prepare(cfg)
     scene = pkg.Scene(mesh, bvh, device=local_rank)
-    basis = pinned_basis(meta, cfg, cam)
+    axis, step_deg = pkg.configs.BENCH_ORBIT
+    b12, s3 = pkg.orbit_cameras(cam, cfg["sun"], W, H, F, axis=axis, step_deg=step_deg, rotate_first=False)
+    b12[0] = pinned_basis(meta, cfg, cam)          # frame 0 = C3 (fixture bits)
+    s3[0] = np.asarray(cfg["sun"], np.float32)
     mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
-    tiling = pkg.Tiling(args.row_block if world > 1 else H, rank, world)
-    gather = D.FrameGather(W, H, tiling.row_block, rank, world, device=dev)
+    row_block = args.row_block if world > 1 else H
+    tiling = pkg.Tiling(row_block, rank, world)
+    gather = D.BatchGather(W, H, row_block, rank, world, frames=F, device=dev, slots=2)
     rows = gather.local_rows
-    d_px = None if args.no_float else torch.empty(3 * W * max(rows, 1), dtype=torch.float32, device=dev)
+    d_px = None if args.no_float else torch.empty(F * 3 * W * max(rows, 1), dtype=torch.float32, device=dev)
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
+    pending = [False, False]
 
-    def step(with_counters=False):
-        scene.render_device(basis, cfg["sun"], W, H, mode=mode, tiling=tiling,
-                            d_pixels=0 if d_px is None else d_px.data_ptr(), d_rgb8=gather.local_ptr(),
-                            d_counters=counters.data_ptr() if with_counters else 0, stream=sh)
-        return gather.gather()
+    def render(slot, with_counters=False):
+        scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=tiling,
+                                  d_pixels=0 if d_px is None else d_px.data_ptr(), d_rgb8=gather.local_ptr(slot),
+                                  d_counters=counters.data_ptr() if with_counters else 0, stream=sh)
 
-    # validation frame: counts (exact) + PPM parity on rank 0
-    full = step(with_counters=True)
+    def step(k):
+        slot = k % 2
+        render(slot)
+        gather.start(slot)
+        prev = 1 - slot
+        if pending[prev]:
+            gather.finish(prev)
+            pending[prev] = False
+        pending[slot] = True
+
+    def drain():
+        for s_ in (0, 1):
+            if pending[s_]:
+                gather.finish(s_)
+                pending[s_] = False
+        gather.wait_assembled()
+
+    # validation step (not timed): exact counts of the F-frame batch + frame-0 PPM parity on rank 0
+    render(0, with_counters=True)
+    gather.start(0)
+    full = gather.finish(0)
+    gather.wait_assembled()
     torch.cuda.synchronize(dev)
     c = counters.clone()
     if world > 1:
         dist.all_reduce(c)
     c = c.cpu().numpy()
-    rays_frame, hits_frame = int(c[0]), int(c[1])
+    rays_step, hits_step = int(c[0]), int(c[1])
     parity = None
     if rank == 0:
-        body = b"P6 %d %d 255\n" % (W, H) + full.cpu().numpy().tobytes()
+        body = b"P6 %d %d 255\n" % (W, H) + full[0].cpu().numpy().tobytes()
         sha = hashlib.sha256(body).hexdigest()
         if meta is not None:
-            parity = {"ppm_sha256_matches_reference": sha == meta["ppm_sha256"]["exact"],
-                      "rays_match": rays_frame == meta["exact"]["rays"], "hits_match": hits_frame == meta["exact"]["hits"]}
+            parity = {"frame0_ppm_sha256_matches_reference": sha == meta["ppm_sha256"]["exact"]}
+            if F == 1:
+                parity.update(rays_match=rays_step == meta["exact"]["rays"], hits_match=hits_step == meta["exact"]["hits"])
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        step(k)
+    drain()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
@@ -206,41 +244,42 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     T = float(elapsed.item())
-    value = rays_frame * args.steps / T / 1e6
+    value = rays_step * args.steps / T / 1e6
 
     roofline = None
     cpu = None
     if rank == 0 and not args.no_roofline and meta is not None:
-        # dominant kernel, timed live with HIP events on the launch stream (full frame, this GPU)
+        # dominant kernel, timed live with HIP events on the launch stream (one full C3 frame, this GPU)
         solo = pkg.Tiling(H, 0, 1)
         solo_rgb = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
         solo_px = torch.empty(3 * W * H, dtype=torch.float32, device=dev)
         scene.set_timing(True)
         n_t = max(10, min(args.steps, 200))
         for _ in range(n_t):
-            scene.render_device(basis, cfg["sun"], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
+            scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
                                 d_rgb8=solo_rgb.data_ptr(), stream=sh)
         p_ms, s_ms, n = scene.read_timing()
         scene.set_timing(False)
         ex = meta["exact"]
         b_p = 64 * ex["primary_pairs"] + 56 * ex["primary_tests"]
         b_s = 64 * ex["shadow_pairs"] + 56 * ex["shadow_tests"]
-        if s_ms == 0.0:     # persistent single-launch frame kernel: the whole frame is one kernel
-            kern = {"ceres_frame": (p_ms / n, b_p + b_s)}
-        else:               # CERES_KERNEL=twopass: primary and shadow kernels
-            kern = {"ceres_primary": (p_ms / n, b_p), "ceres_shadow": (s_ms / n, b_s)}
+        kern = {"ceres_primary": (p_ms / n, b_p)}
+        if mode == pkg.MODE_FULL:
+            kern["ceres_shadow"] = (s_ms / n, b_s)
         name = max(kern, key=lambda k: kern[k][0])
         ms, nbytes = kern[name]
         achieved = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        frame_bytes = sum(v[1] for v in kern.values())
+        frame_ms = sum(v[0] for v in kern.values())
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": pmc_traffic(args.config, name),
                     "algorithmic_bytes_per_launch": nbytes, "mean_launch_ms": round(ms, 5),
                     "kernels_ms": {k: round(v[0], 5) for k, v in kern.items()},
-                    "frame_algorithmic_bytes": b_p + b_s,
-                    "frame_frac": round((b_p + b_s) / ((p_ms + s_ms) / n * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                    "frame_algorithmic_bytes": frame_bytes,
+                    "frame_frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.config, cfg, rays_frame)
+        cpu = cpu_baseline(args.config, cfg, rays_step if F == 1 else meta["exact"]["rays"])
 
     if rank == 0:
         line = {
@@ -248,16 +287,17 @@ def main():
             if args.config == "dragon_1080" else f"Mrays/sec ({args.config})",
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(T / args.steps * 1e3, 5), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "real mesh from the reference repo (data/%s), static camera" % (cfg["obj"] or "procedural"),
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "real mesh from the reference repo (data/%s); frame 0 = static.cpp camera, frames 1.. = "
+                    "anim.cpp-style orbit about z" % (cfg["obj"] or "procedural"),
             "config": {"workload": f"{args.config}: {cfg['obj'] or 'proc'} {W}x{H} "
-                                   f"{'primary+shadow' if mode == pkg.MODE_FULL else 'primary only'}",
-                       "W": W, "H": H, "rays_per_frame": rays_frame, "hits_per_frame": hits_frame,
-                       "row_block": tiling.row_block, "parallelism": f"row-interleaved framebuffer x{world}"
-                       + (" + RCCL gather to rank 0" if world > 1 else ""),
+                                   f"{'primary+shadow' if mode == pkg.MODE_FULL else 'primary only'}, "
+                                   f"{F} orbit frame(s) per step",
+                       "W": W, "H": H, "frames_per_step": F, "rays_per_step": rays_step, "hits_per_step": hits_step,
+                       "row_block": row_block, "parallelism": f"row-interleaved frames x{world}"
+                       + (" + one RCCL gather per step to rank 0 (pipelined)" if world > 1 else ""),
                        "float_framebuffer": d_px is not None},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
-            "kernel_variant": os.environ.get("CERES_KERNEL", "twopass"),
         }
         print(json.dumps(line), flush=True)
     scene.close()

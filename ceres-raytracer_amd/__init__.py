@@ -34,8 +34,8 @@ SCENE_STATS = 1
 EXPORTED_SYMBOLS = (
     "ceres_obj_load", "ceres_proc_mesh", "ceres_rotate_triangles", "ceres_bvh_build", "ceres_camera_basis",
     "ceres_free", "ceres_scene_create", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
-    "ceres_render_device", "ceres_render_records", "ceres_tiling_local_rows", "ceres_scene_set_timing", "ceres_scene_read_timing",
-    "ceres_scene_wave_log",
+    "ceres_render_device", "ceres_render_batch_device", "ceres_render_records", "ceres_tiling_local_rows",
+    "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
 )
 
@@ -94,6 +94,8 @@ def lib():
     L.ceres_rotate_triangles.argtypes = [_fp, _sz, ctypes.c_int, ctypes.c_float]
     L.ceres_bvh_build.argtypes = [_fp, _sz, ctypes.POINTER(_u32p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p)]
     L.ceres_camera_basis.argtypes = [_fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp]
+    L.ceres_orbit_cameras.argtypes = [_fp, _fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp, ctypes.c_float,
+                                      ctypes.c_uint32, ctypes.c_int, _fp, _fp, _fp]
     L.ceres_free.argtypes = [_vp]
     L.ceres_free.restype = None
     L.ceres_scene_create.argtypes = [_fp, _sz, _fp, _vp, _sz, _u64p, ctypes.c_int, ctypes.c_uint32]
@@ -104,6 +106,9 @@ def lib():
     L.ceres_render_f32.argtypes = [_vp, _fp, _fp, ctypes.c_int, _fp, ctypes.POINTER(ctypes.c_uint8), _sz, _sz,
                                    ctypes.POINTER(_Stats)]
     L.ceres_render_device.argtypes = [_vp, _fp, _fp, ctypes.c_int, _sz, _sz, ctypes.POINTER(Tiling), _vp, _vp, _vp, _vp]
+    L.ceres_render_batch_device.argtypes = [_vp, ctypes.c_uint32, _fp, _fp, ctypes.c_int, _sz, _sz,
+                                            ctypes.POINTER(Tiling), _vp, _vp, _vp, _vp]
+    L.ceres_assemble_rgb8.argtypes = [_vp, _sz, _vp, ctypes.c_uint32, _sz, _sz, ctypes.c_uint32, ctypes.c_uint32, _vp]
     L.ceres_render_records.argtypes = [_vp, _fp, _fp, ctypes.c_int, _sz, _sz, ctypes.POINTER(ctypes.c_int32), _fp,
                                        ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(_Stats)]
     L.ceres_tiling_local_rows.argtypes = [_sz, ctypes.POINTER(Tiling)]
@@ -261,11 +266,25 @@ class Scene:
         _check(lib().ceres_render_device(self._h, _p(b, ctypes.c_float), _p(s, ctypes.c_float), int(mode), W, H, t,
                                          d_pixels or None, d_rgb8 or None, d_counters or None, stream or None))
 
+    def render_batch_device(self, basis12, sun3, W, H, mode=MODE_FULL, tiling=None, d_pixels=0, d_rgb8=0,
+                            d_counters=0, stream=0):
+        """ceres_render_batch_device: F frames (basis12 [F,12], sun3 [F,3]) in one launch pair.
+        Frame f's rows are at offset f*3*W*local_rows of d_pixels / d_rgb8."""
+        b = np.ascontiguousarray(basis12, np.float32).reshape(-1, 12)
+        s = np.ascontiguousarray(sun3, np.float32).reshape(-1, 3)
+        if b.shape[0] != s.shape[0]:
+            raise CeresError("render_batch_device: %d cameras but %d suns" % (b.shape[0], s.shape[0]))
+        t = ctypes.byref(tiling) if tiling is not None else None
+        _check(lib().ceres_render_batch_device(self._h, b.shape[0], _p(b, ctypes.c_float), _p(s, ctypes.c_float),
+                                               int(mode), W, H, t, d_pixels or None, d_rgb8 or None,
+                                               d_counters or None, stream or None))
+
     def set_timing(self, on):
         _check(lib().ceres_scene_set_timing(self._h, 1 if on else 0))
 
     def wave_log(self, max_waves=1 << 16):
-        """Diagnostic per-wavefront records of the last persistent-kernel frame (stats scenes)."""
+        """Diagnostic per-wavefront records of the last shadow launch (stats scenes): begin/end
+        wall clock, longest node-pair chain, stamped iterations, box/leaf/next clocks, pairs."""
         out = np.zeros(8 * max_waves, np.uint64)
         n = _sz()
         _check(lib().ceres_scene_wave_log(self._h, _p(out, ctypes.c_uint64), max_waves, ctypes.byref(n)))
@@ -275,6 +294,44 @@ class Scene:
         p, q, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
         _check(lib().ceres_scene_read_timing(self._h, ctypes.byref(p), ctypes.byref(q), ctypes.byref(n)))
         return p.value, q.value, n.value
+
+
+def orbit_cameras(camera, sun, W, H, n_frames, axis=(0, 1, 0), step_deg=None, rotate_first=True, want_dirs=False):
+    """anim.cpp:76-88 orbit: eye, dir and sun rotated by step_deg (default 360/n_frames, as
+    anim.cpp) about `axis` per frame.  Returns (basis12 [F,12] f32, sun3 [F,3] f32) and, with
+    want_dirs, the rotated camera dirs [F,3] as a third element."""
+    n = int(n_frames)
+    step = np.float32(360.0) / np.float32(n) if step_deg is None else np.float32(step_deg)
+    b = np.zeros((n, 12), np.float32)
+    s3 = np.zeros((n, 3), np.float32)
+    d3 = np.zeros((n, 3), np.float32)
+    ax = np.asarray(axis, np.float32)
+    sn = np.asarray(sun, np.float32)
+    _check(lib().ceres_orbit_cameras(_p(camera.eye, ctypes.c_float), _p(camera.dir, ctypes.c_float),
+                                     _p(camera.up, ctypes.c_float), _p(sn, ctypes.c_float), camera.fov, W, H,
+                                     _p(ax, ctypes.c_float), float(step), n, 1 if rotate_first else 0,
+                                     _p(b, ctypes.c_float), _p(s3, ctypes.c_float), _p(d3, ctypes.c_float)))
+    return (b, s3, d3) if want_dirs else (b, s3)
+
+
+def pose(cfg, frame=0):
+    """(Camera, sun) of a config: configs with "orbit": (axis, step_deg, count) are the anim.cpp
+    orbit pose after count + frame rotations; otherwise the config's camera rotated `frame`
+    times by configs.BENCH_ORBIT."""
+    cam = Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    axis, step = (cfg["orbit"][0], cfg["orbit"][1]) if cfg.get("orbit") else configs.BENCH_ORBIT
+    n = (cfg["orbit"][2] if cfg.get("orbit") else 0) + int(frame)
+    if n == 0:
+        return cam, np.asarray(cfg["sun"], np.float32)
+    b, s3, d3 = orbit_cameras(cam, cfg["sun"], cfg["W"], cfg["H"], n + 1, axis=axis, step_deg=step,
+                              rotate_first=False, want_dirs=True)
+    return Camera(b[n, :3], d3[n], cfg["up"], cfg["fov"]), s3[n].copy()
+
+
+def assemble_rgb8(d_gathered, rank_stride, d_out, frames, W, H, row_block, world, stream=0):
+    """ceres_assemble_rgb8 (device pointers): rank-major gathered batch rows -> F PPM bodies."""
+    _check(lib().ceres_assemble_rgb8(d_gathered, rank_stride, d_out, int(frames), W, H, int(row_block), int(world),
+                                     stream or None))
 
 
 def local_rows(H, tiling):
@@ -294,14 +351,15 @@ def row_map(H, row_block, world):
 
 
 def prepare(cfg):
-    """Scene prep of the reference app for a config (configs.CONFIGS entry): mesh, bvh, camera."""
+    """Scene prep of the reference app for a config (configs.CONFIGS entry): mesh, bvh, camera
+    (at the config's orbit pose; pose(cfg) also gives the sun)."""
     mesh = proc_mesh(cfg["proc"]) if cfg.get("proc") else load_obj(configs.obj_path(cfg))
     if len(mesh) == 0:
         raise CeresError("The given scene is empty or cannot be loaded")
     if cfg.get("rotate"):
         rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1])
     bvh = build_bvh(mesh)
-    cam = Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    cam, _ = pose(cfg)
     return mesh, bvh, cam
 
 

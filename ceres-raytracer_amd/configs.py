@@ -32,6 +32,7 @@ def _cfg(base, **kw):
     d.update(kw)
     d.setdefault("mode", "full")
     d.setdefault("proc", 0)
+    d.setdefault("orbit", None)
     return d
 
 
@@ -57,7 +58,14 @@ CONFIGS = {
     "tri1": _cfg(_TINY, obj="@golden/tri1.obj", W=64, H=48),
     "quad": _cfg(_TINY, obj="@golden/quad.obj", W=64, H=48),
     "degenerate": _cfg(_TINY, obj="@golden/degenerate.obj", W=64, H=48),
+    # anim.cpp:76-88 orbit poses: the C3 camera + sun after `count` Transform rotations of
+    # step_deg about the axis (the bench's weak-scaling frames are this orbit about z)
+    "dragon_orbit3_333x217": _cfg(_DRAGON, W=333, H=217, orbit=((0.0, 0.0, 1.0), 45.0, 3)),
+    "bunny_orbit7_160x120": _cfg(_BUNNY, W=160, H=120, orbit=((0.0, 1.0, 0.0), 6.0, 7)),
 }
+
+# bench.py weak scaling: frame k of a step is the C3 pose rotated k times by 45 degrees about z
+BENCH_ORBIT = ((0.0, 0.0, 1.0), 45.0)
 
 
 def obj_path(cfg):
@@ -81,6 +89,9 @@ def cli_args(cfg):
           "--fov", repr(cfg["fov"]), "--sun", *map(repr, cfg["sun"]), "--size", str(cfg["W"]), str(cfg["H"])]
     if cfg["rotate"]:
         a += ["--rotate", cfg["rotate"][0], repr(cfg["rotate"][1])]
+    if cfg.get("orbit"):
+        (ax, ay, az), step, count = cfg["orbit"]
+        a += ["--orbit", repr(ax), repr(ay), repr(az), repr(step), str(count)]
     if cfg["mode"] == "primary":
         a += ["--primary-only"]
     return a

@@ -16,7 +16,9 @@
 //   norms[]  36-B per-triangle vertex normals in ORIGINAL order (obj_norms.hpp:113-115),
 //            read only for lit pixels.
 #pragma once
+#include <cstddef>
 #include <cstdint>
+#include <vector>
 
 namespace ceres {
 
@@ -41,7 +43,7 @@ struct alignas(16) SiblingPair {
 static_assert(sizeof(SiblingPair) == 64, "SiblingPair");
 
 struct ShadowJob {             // one queued shadow ray (render.hpp:127-136), 32 B
-    uint32_t pixel;            // local pixel index = local_row * W + i
+    uint32_t pixel;            // batch pixel index = (frame * local_rows + local_row) * W + i
     uint32_t slot;             // leaf slot of the primary hit
     float u, v;                // barycentrics of the primary hit (reference convention)
     float px, py, pz;          // offset hit point = shadow ray origin
@@ -57,35 +59,44 @@ struct alignas(128) Shard {
     unsigned long long pairs;  // node-pair visits (stats variant)
     unsigned long long tests;  // triangle tests (stats variant)
     unsigned long long primary;
-    uint32_t tiles;            // persistent kernel: next chunk of this shard's tile band
-    uint32_t exhausted;        // persistent kernel (shard 0 only): bitmask of drained tile shards
+    uint32_t reserved[2];
     uint32_t pad[20];
 };
 static_assert(sizeof(Shard) == 128, "Shard");
 
-struct KParams {
+constexpr int kMaxFrames = 32;  // frames per batch launch (KParams stays well inside the 4 KB kernarg limit)
+struct FrameCam {              // one frame of a batch: eye + the render.hpp:91-97 basis + its sun
     float eye[3], dir[3], iu[3], iv[3], sun[3];
+};
+
+struct KParams {
+    FrameCam cam[kMaxFrames];
+    uint32_t frames;                             // frames in this batch (1..kMaxFrames)
     uint32_t W, H;
-    uint32_t row_block, rank, world, local_rows;
+    uint32_t row_block, rank, world, local_rows; // this rank's rows of every frame (ceres_tiling)
+    uint32_t row_blocks_per_frame;               // 16-row blocks of local rows per frame (primary grid.y)
     uint32_t stack_entries;
     uint32_t root_leaf_count, root_leaf_first;   // root is a leaf (single_ray_traverser.hpp:72-73)
-    uint32_t shard_capacity;                     // jobs per shard (twopass kernels)
-    uint32_t tiles_x, tiles_y, n_chunks;         // persistent kernel: 8x8 tiles, chunks of kChunkTiles
-    uint32_t pad_;
+    uint32_t shard_capacity;                     // jobs per shard
     const SiblingPair* pairs;
     const Tri48* tris;
     const uint32_t* orig;
     const float* norms;
-    float* pixels;
-    uint8_t* rgb8;
+    float* pixels;             // [frames][local_rows][W][3] floats, row 0 = bottom (render.hpp:107)
+    uint8_t* rgb8;             // [frames][local_rows][W][3] PPM body rows, top row first
     ShadowJob* jobs;
     Shard* shards;
-    // optional per-pixel hit records (G-buffer / parity output), local pixel order
+    // optional per-pixel hit records (G-buffer / parity output), batch pixel order
     int32_t* rec_prim;         // original triangle index, -1 on a primary miss
     float* rec_tuv;            // t, u, v of the primary hit
     int8_t* rec_shadow;        // -1 no shadow ray, 0 lit, 1 occluded
-    // diagnostic (stats scenes only): 8 x u64 per wavefront of the persistent kernel
+    // diagnostic (stats scenes only): 8 x u64 per wavefront of the shadow kernel
     unsigned long long* wave_log;
 };
+
+// host: reference BVH -> GPU layout (scene_host.cpp)
+int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri48* tris,
+                 std::vector<SiblingPair>& pairs, std::vector<Tri48>& leaf_tris, std::vector<uint32_t>& orig,
+                 uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first);
 
 }  // namespace ceres

@@ -8,6 +8,12 @@
 //   render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]
 //                [--rotate x|y|z deg] [--size W H] [-o|--out file.ppm] [--primary-only]
 //                [--proc N] [--device D] [--bench reps] [--json]
+//                [--orbit ax ay az step_deg count] [--frames N]
+//
+// --orbit / --frames are the anim.cpp:76-125 driver without Magick++: the camera eye, dir and
+// the sun are rotated by step_deg about the axis (transform.hpp:67-112) `count` times before
+// the first frame, and once more per further frame; N frames are written as
+// <out-stem>_000.ppm ... (one file when N = 1), "Total Rays" summed like anim.cpp:127.
 //
 // Exit status: 0 on success, 1 on a load/render error (message on stderr), 2 on bad usage.
 // There is no CPU fallback: without a gfx950 device the render step fails.
@@ -33,13 +39,15 @@ struct Opts {
     size_t W = 1920, H = 1080;
     int mode = CERES_MODE_FULL, proc = 0, device = 0, bench = 0;
     bool json = false;
+    float orbit_axis[3] = {0.f, 1.f, 0.f}, orbit_step = 0.f;
+    int orbit_count = 0, frames = 1;
 };
 
 int usage() {
     std::fprintf(stderr,
                  "usage: render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]\n"
                  "              [--rotate x|y|z deg] [--size W H] [-o out.ppm] [--primary-only] [--proc N]\n"
-                 "              [--device D] [--bench reps] [--json]\n");
+                 "              [--device D] [--bench reps] [--json] [--orbit ax ay az step_deg count] [--frames N]\n");
     return 2;
 }
 
@@ -70,6 +78,11 @@ bool parse(int argc, char** argv, Opts& o) {
         else if (a == "--device") { if (!have(1)) return false; o.device = std::atoi(argv[++i]); }
         else if (a == "--bench") { if (!have(1)) return false; o.bench = std::atoi(argv[++i]); }
         else if (a == "--json") o.json = true;
+        else if (a == "--orbit") {
+            if (!vec(o.orbit_axis) || !have(2) || !f(argv[i + 1], &o.orbit_step)) return false;
+            o.orbit_count = std::atoi(argv[i + 2]); i += 2;
+            if (o.orbit_count < 0) return false;
+        } else if (a == "--frames") { if (!have(1)) return false; o.frames = std::atoi(argv[++i]); if (o.frames < 1) return false; }
         else if (a == "-h" || a == "--help") return false;
         else if (!a.empty() && a[0] == '-' && a.size() > 1 && !std::isdigit((unsigned char)a[1])) { std::fprintf(stderr, "unknown flag %s\n", a.c_str()); return false; }
         else if (o.obj.empty()) o.obj = a;
@@ -102,34 +115,54 @@ int main(int argc, char** argv) {
     ceres_free(nodes); ceres_free(prim); ceres_free(tri); ceres_free(norm);
     if (!scene) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
 
-    float basis[12];
-    std::memcpy(basis, o.eye, sizeof o.eye);
-    ceres_camera_basis(o.eye, o.dir, o.up, o.fov, o.W, o.H, basis + 3);
+    // frame poses: count + k orbit rotations for frame k (count = 0, frames = 1: the plain camera)
+    const uint32_t n_pose = uint32_t(o.orbit_count + o.frames);
+    std::vector<float> bases(12 * size_t(n_pose)), suns(3 * size_t(n_pose));
+    if (ceres_orbit_cameras(o.eye, o.dir, o.up, o.sun, o.fov, o.W, o.H, o.orbit_axis, o.orbit_step, n_pose, 0,
+                            bases.data(), suns.data(), nullptr) != CERES_OK) {
+        std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1;
+    }
     std::vector<uint8_t> rgb(3 * o.W * o.H);
-    std::printf("Rendering image (%zux%zu) on HIP device %d...\n", o.W, o.H, o.device);
     ceres_stats st{};
-    const double t1 = now_s();
-    int rc = ceres_render_f32(scene, basis, o.sun, o.mode, nullptr, rgb.data(), o.W, o.H, &st);
-    const double t2 = now_s();
-    if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1; }
-    std::printf("%g\n", t2 - t1);
-    std::printf("Rays: %llu\tHits: %llu\n", (unsigned long long)st.rays, (unsigned long long)st.hits);   // anim.cpp:109
+    unsigned long long tot_rays = 0;
     std::vector<double> ms;
-    for (int r = 0; r < o.bench; ++r) {
-        ceres_stats s2{};
-        rc = ceres_render_f32(scene, basis, o.sun, o.mode, nullptr, rgb.data(), o.W, o.H, &s2);
+    for (int k = 0; k < o.frames; ++k) {
+        const float* basis = bases.data() + 12 * size_t(o.orbit_count + k);
+        const float* sun = suns.data() + 3 * size_t(o.orbit_count + k);
+        std::printf("Rendering image %d (%zux%zu) on HIP device %d...\n", k, o.W, o.H, o.device);
+        const double t1 = now_s();
+        int rc = ceres_render_f32(scene, basis, sun, o.mode, nullptr, rgb.data(), o.W, o.H, &st);
+        const double t2 = now_s();
         if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1; }
-        ms.push_back(s2.ms);
+        std::printf("%g\n", t2 - t1);
+        std::printf("Rays: %llu\tHits: %llu\n", (unsigned long long)st.rays, (unsigned long long)st.hits);   // anim.cpp:109
+        tot_rays += st.rays;
+        for (int r = 0; r < o.bench; ++r) {
+            ceres_stats s2{};
+            rc = ceres_render_f32(scene, basis, sun, o.mode, nullptr, rgb.data(), o.W, o.H, &s2);
+            if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1; }
+            ms.push_back(s2.ms);
+        }
+        std::string path = o.out;
+        if (o.frames > 1) {
+            char suffix[16];
+            std::snprintf(suffix, sizeof suffix, "_%03d", k);
+            const size_t dot = path.rfind('.');
+            const size_t slash = path.rfind('/');
+            if (dot == std::string::npos || (slash != std::string::npos && dot < slash)) path += suffix;
+            else path.insert(dot, suffix);
+        }
+        if (FILE* f = std::fopen(path.c_str(), "wb")) {              // static.cpp:135-147
+            std::fprintf(f, "P6 %zu %zu %d\n", o.W, o.H, 255);
+            std::fwrite(rgb.data(), 1, rgb.size(), f);
+            std::fclose(f);
+        } else {
+            std::fprintf(stderr, "error: cannot write %s\n", path.c_str());
+            ceres_scene_destroy(scene);
+            return 1;
+        }
     }
-    if (FILE* f = std::fopen(o.out.c_str(), "wb")) {                // static.cpp:135-147
-        std::fprintf(f, "P6 %zu %zu %d\n", o.W, o.H, 255);
-        std::fwrite(rgb.data(), 1, rgb.size(), f);
-        std::fclose(f);
-    } else {
-        std::fprintf(stderr, "error: cannot write %s\n", o.out.c_str());
-        ceres_scene_destroy(scene);
-        return 1;
-    }
+    if (o.frames > 1) std::printf("Total Rays: %llu\n", tot_rays);   // anim.cpp:127
     if (o.json) {
         double med = 0;
         if (!ms.empty()) { std::sort(ms.begin(), ms.end()); med = ms[ms.size() / 2]; }

@@ -6,21 +6,23 @@
 // the offset shadow ray (render.hpp:119-138) and smooth Blinn-Phong shading (render.hpp:46-84),
 // plus the PPM quantiser of static.cpp:135-147.
 //
-// Two kernels per frame (DESIGN.md "Kernels"):
+// Two kernels per batch of frames (DESIGN.md "Kernels"):
 //   ceres_primary  one lane per pixel, 8x8 pixel tile per wavefront (coherent primary rays),
 //                  closest-hit traversal; misses / primary-only pixels are written directly;
-//                  hits are COMPACTED into a sharded shadow-ray queue with a wave __ballot +
-//                  popcount prefix (one atomic per workgroup), so no lane idles on pixels
-//                  that missed while other lanes trace 28-node-pair shadow rays.
-//   ceres_shadow   one lane per queued shadow ray (dense waves), any-hit traversal (only the
-//                  boolean matters, render.hpp:139 -- result-identical to the reference's
+//                  hits are COMPACTED into a sharded shadow-ray queue with a wavefront
+//                  __ballot + popcount prefix (one queue atomic per wavefront), so no lane
+//                  idles on missed pixels while other lanes trace 28-node-pair shadow rays.
+//   ceres_shadow   one lane per queued shadow ray (dense wavefronts), any-hit traversal (only
+//                  the boolean matters, render.hpp:139 -- result-identical to the reference's
 //                  closest-hit with tmax = FLT_MAX), then smooth shading of lit pixels.
+// A batch is 1..kMaxFrames frames (own camera + sun each, e.g. the anim.cpp:93-110 orbit),
+// each restricted to this rank's rows (ceres_tiling): one launch pair per batch.
 // The traversal stack lives in LDS ([entries][threads], lane-contiguous = bank-conflict
 // free), sized from the BVH depth at scene creation (<= 63 entries for max_depth 64).
 //
 // Numerics: compiled with -ffp-contract=off and correctly rounded f32 div/sqrt, explicit
-// fmaf only where the reference calls fast_multiply_add, std::pow in double -- so every
-// float matches the reference compiled without contraction bit for bit.
+// fmaf only where the reference calls fast_multiply_add, x^24 in double-double for std::pow
+// (pow24.hpp) -- every float matches the reference compiled without contraction bit for bit.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,9 +31,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <new>
-#include <string>
 #include <vector>
 
 #include "ceres_render.h"
@@ -40,7 +40,6 @@
 #include "pow24.hpp"
 
 #pragma clang fp contract(off)
-
 
 namespace ceres {
 
@@ -52,7 +51,6 @@ char* error_buffer() {
 namespace dev {
 
 constexpr int kBlock = 256;            // 4 wavefronts of 64 lanes
-constexpr int kWaves = kBlock / 64;
 
 struct F3 { float x, y, z; };
 __device__ __forceinline__ F3 operator+(F3 a, F3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
@@ -61,8 +59,7 @@ __device__ __forceinline__ F3 operator*(F3 a, float s) { return {a.x * s, a.y * 
 __device__ __forceinline__ float dot(F3 a, F3 b) { float s = a.x * b.x; s += a.y * b.y; s += a.z * b.z; return s; }
 __device__ __forceinline__ F3 cross(F3 a, F3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 __device__ __forceinline__ F3 normalize(F3 v) { float inv = 1.0f / sqrtf(dot(v, v)); return v * inv; }
-__device__ __forceinline__ float rmax(float x, float y) { return x > y ? x : y; }   // robust_max, utilities.hpp:57-67
-__device__ __forceinline__ float rmin(float x, float y) { return x < y ? x : y; }
+__device__ __forceinline__ F3 f3(const float* p) { return {p[0], p[1], p[2]}; }
 
 struct TriV { F3 p0, e1, e2, n; };
 __device__ __forceinline__ TriV load_tri(const Tri48* t) {
@@ -71,11 +68,10 @@ __device__ __forceinline__ TriV load_tri(const Tri48* t) {
     return {{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, c.x}, {c.y, c.z, c.w}};
 }
 
-// Per-ray traversal state; the hit is "last accepted wins" like intersect_leaf (:54-60).
+// Per-ray hit; closest hit keeps the LAST accepted hit with t <= tmax (intersect_leaf :54-60).
 struct Hit { uint32_t slot; float t, u, v; };
 
-// Triangle::intersect (triangle.hpp:95-115, left-handed normal): on an accepted hit updates
-// best / tmax (closest hit keeps the LAST accepted hit with t <= tmax, intersect_leaf :54-60).
+// Triangle::intersect (triangle.hpp:95-115, left-handed normal).
 __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin, float tmax, float& t_out,
                                          float& u_out, float& v_out) {
     const F3 c = tr.p0 - o;
@@ -91,6 +87,16 @@ __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin,
     return false;
 }
 
+// Diagnostic section clocks (stats builds only): wave-uniform s_memtime sums per trace().
+struct Stamps { unsigned long long box = 0, leaf = 0, next = 0, iters = 0; };
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
 // Eager BVH2 traversal, single_ray_traverser.hpp:68-126 with FastNodeIntersector
 // (node_intersectors.hpp:35-47,83-103).  Exactly the reference's visiting order: both
 // children's slab tests use the tmax from before this step's leaves; left leaf triangles,
@@ -104,17 +110,7 @@ __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin,
 // whenever y is not NaN (y is tmin / tmax / a previous robust_max -- never NaN) up to the
 // sign of zero, which no comparison below can observe; likewise robust_min and fminf.  The
 // slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
-// Diagnostic section clocks (stats builds only): wave-uniform s_memtime sums per trace().
-struct Stamps { unsigned long long box = 0, leaf = 0, next = 0, iters = 0; };
-__device__ __forceinline__ unsigned long long stamp() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-
-template <bool kAnyHit, bool kStats, int kStride = kBlock, bool kPF = false>
+template <bool kAnyHit, bool kStats>
 __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* stk, Hit& best,
                                       uint32_t& n_pairs, uint32_t& n_tests, bool& overflow, Stamps* ss = nullptr) {
     const float tmin = 0.0f;
@@ -177,7 +173,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         if (go_l && go_r) {                                           // near first, ties left (:109-115)
             const bool swap = le > re;
             if (sp >= P.stack_entries) { overflow = true; return have; }
-            stk[sp * kStride] = swap ? L.y : L.w;
+            stk[sp * kBlock] = swap ? L.y : L.w;
             ++sp;
             cur = swap ? L.w : L.y;
         } else if (go_l || go_r) {
@@ -185,7 +181,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         } else {
             if (sp == 0) { if (kStats && ss) ss->next += stamp() - c2; break; }   // :118-121
             --sp;
-            cur = stk[sp * kStride];
+            cur = stk[sp * kBlock];
         }
         if (kStats && ss) ss->next += stamp() - c2;
     }
@@ -199,13 +195,18 @@ __device__ __forceinline__ uint8_t quantize(float x) {               // static.c
     return static_cast<uint8_t>(static_cast<int>(q));
 }
 
-__device__ __forceinline__ void store_pixel(const KParams& P, uint32_t lr, uint32_t i, float c0, float c1, float c2) {
+// Pixel (frame f, local row lr, column i): float RGB at batch pixel (f*rows + lr)*W + i with
+// row 0 at the bottom (render.hpp:107); RGB8 PPM body with local row lr stored at row
+// rows-1-lr of its frame (static.cpp:137, rows written top-down).
+__device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32_t lr, uint32_t i, float c0, float c1,
+                                            float c2) {
+    const size_t frame_base = size_t(f) * P.local_rows;
     if (P.pixels) {
-        float* q = P.pixels + 3 * (size_t(lr) * P.W + i);
+        float* q = P.pixels + 3 * ((frame_base + lr) * P.W + i);
         q[0] = c0; q[1] = c1; q[2] = c2;
     }
     if (P.rgb8) {
-        uint8_t* q = P.rgb8 + 3 * (size_t(P.local_rows - 1 - lr) * P.W + i);
+        uint8_t* q = P.rgb8 + 3 * ((frame_base + (P.local_rows - 1 - lr)) * P.W + i);
         q[0] = quantize(c0); q[1] = quantize(c1); q[2] = quantize(c2);
     }
 }
@@ -214,12 +215,12 @@ __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t lr) {
     return ((lr / P.row_block) * P.world + P.rank) * P.row_block + lr % P.row_block;
 }
 
-// Primary ray direction of pixel (i, j), render.hpp:109-111.
-__device__ __forceinline__ F3 primary_dir(const KParams& P, uint32_t i, uint32_t j) {
+// Primary ray direction of pixel (i, j) of frame f, render.hpp:109-111.
+__device__ __forceinline__ F3 primary_dir(const KParams& P, uint32_t f, uint32_t i, uint32_t j) {
     const float u = 2 * (float(i) + 0.5f) / float(P.W) - 1.0f;
     const float v = 2 * (float(j) + 0.5f) / float(P.H) - 1.0f;
-    const F3 iu{P.iu[0], P.iu[1], P.iu[2]}, iv{P.iv[0], P.iv[1], P.iv[2]}, dir{P.dir[0], P.dir[1], P.dir[2]};
-    return normalize(iu * u + iv * v + dir);
+    const FrameCam& c = P.cam[f];
+    return normalize(f3(c.iu) * u + f3(c.iv) * v + f3(c.dir));
 }
 
 // smooth_shading, render.hpp:46-84 (pow in double: std::pow(float, int) promotes).
@@ -248,35 +249,42 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 }
 
 // ---------------------------------------------------------------- primary kernel
-// kBS threads per workgroup (64: one 8x8 tile per workgroup; 256: 16x16 pixels as 2x2 wave
-// tiles).  Every wavefront is independent: no workgroup barrier, one queue atomic per wave.
-template <int kMode, bool kStats, int kBS, bool kPF>
-__device__ __forceinline__ void primary_tile(const KParams& P, uint32_t* stk, uint32_t lane, uint32_t wave_id,
-                                             uint32_t i, uint32_t lr) {
+// grid.x: 16-pixel column blocks; grid.y: frames x 16-row blocks of this rank's rows.  The
+// four wavefronts of a workgroup take the 2x2 8x8 tiles of its 16x16 pixels.  Every wavefront
+// is independent: no workgroup barrier, one queue atomic per wavefront.
+template <int kMode, bool kStats>
+__global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t* stk = lds + tid;                                       // [entries][kBlock]
+    const uint32_t f = blockIdx.y / P.row_blocks_per_frame;          // workgroup-uniform frame
+    const uint32_t by = blockIdx.y - f * P.row_blocks_per_frame;
+    const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const uint32_t lr = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     const bool active = i < P.W && lr < P.local_rows;
+    const uint32_t px = (f * P.local_rows + lr) * P.W + i;          // batch pixel (< 2^32, host-checked)
     bool hit = false, job = false;
     Hit h{0, 0.f, 0.f, 0.f};
     uint32_t n_pairs = 0, n_tests = 0;
     bool overflow = false;
     F3 shadow_o{0.f, 0.f, 0.f};
     if (active) {
-        const uint32_t j = global_row(P, lr);
-        const F3 eye{P.eye[0], P.eye[1], P.eye[2]};
-        const F3 view = primary_dir(P, i, j);
-        hit = trace<false, kStats, kBS, kPF>(P, eye, view, stk, h, n_pairs, n_tests, overflow);
+        const F3 view = primary_dir(P, f, i, global_row(P, lr));
+        hit = trace<false, kStats>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
-            const size_t px = size_t(lr) * P.W + i;
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
-            P.rec_tuv[3 * px] = hit ? h.t : 0.f; P.rec_tuv[3 * px + 1] = hit ? h.u : 0.f; P.rec_tuv[3 * px + 2] = hit ? h.v : 0.f;
+            P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
+            P.rec_tuv[3 * size_t(px) + 1] = hit ? h.u : 0.f;
+            P.rec_tuv[3 * size_t(px) + 2] = hit ? h.v : 0.f;
             P.rec_shadow[px] = -1;
         }
         if (!hit) {
-            store_pixel(P, lr, i, 0.f, 0.f, 0.f);                    // render.hpp:116-117
+            store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);                 // render.hpp:116-117
         } else {
             const TriV tr = load_tri(P.tris + h.slot);
             const F3 normal = normalize(tr.n);
             if (kMode == CERES_MODE_PRIMARY) {                       // render.hpp:123-125
-                store_pixel(P, lr, i, fabsf(normal.x), fabsf(normal.y), fabsf(normal.z));
+                store_pixel(P, f, lr, i, fabsf(normal.x), fabsf(normal.y), fabsf(normal.z));
             } else {                                                 // render.hpp:127-133
                 const F3 p1 = tr.p0 - tr.e1, p2 = tr.p0 + tr.e2;
                 F3 p = tr.p0 * h.u + p1 * h.v + p2 * (1 - h.u - h.v);
@@ -288,6 +296,7 @@ __device__ __forceinline__ void primary_tile(const KParams& P, uint32_t* stk, ui
         }
     }
     // wave-level compaction of the shadow rays: ballot + popcount prefix, one atomic per wave
+    const uint32_t wave_id = (blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave;
     const uint32_t shard = wave_id % kShards;
     const unsigned long long jm = __ballot(job);
     const uint32_t nh = __popcll(__ballot(hit));
@@ -301,7 +310,7 @@ __device__ __forceinline__ void primary_tile(const KParams& P, uint32_t* stk, ui
         if (job) {
             const uint32_t off = base + __popcll(jm & ((1ull << lane) - 1ull));
             float4* q = reinterpret_cast<float4*>(P.jobs + size_t(shard) * P.shard_capacity + off);
-            q[0] = make_float4(__uint_as_float(lr * P.W + i), __uint_as_float(h.slot), h.u, h.v);
+            q[0] = make_float4(__uint_as_float(px), __uint_as_float(h.slot), h.u, h.v);
             q[1] = make_float4(shadow_o.x, shadow_o.y, shadow_o.z, 0.f);
         }
     }
@@ -315,45 +324,34 @@ __device__ __forceinline__ void primary_tile(const KParams& P, uint32_t* stk, ui
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
 }
 
-
-template <int kMode, bool kStats, int kBS, bool kPF>
-__global__ __launch_bounds__(kBS) void ceres_primary(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t* stk = lds + tid;                                       // [entries][kBS]
-    if (kBS == 64) {
-        // one wavefront per workgroup; tiles_per_wave 8x8 tiles, interleaved over the grid
-        const uint32_t n_tiles = P.tiles_x * P.tiles_y;
-        for (uint32_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-            const uint32_t ty = t / P.tiles_x, tx = t - ty * P.tiles_x;
-            primary_tile<kMode, kStats, kBS, kPF>(P, stk, lane, t, tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
-        }
-    } else {
-        const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-        const uint32_t lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-        primary_tile<kMode, kStats, kBS, kPF>(P, stk, lane, (blockIdx.y * gridDim.x + blockIdx.x) * (kBS / 64) + wave, i, lr);
-    }
-}
-
 // ---------------------------------------------------------------- shadow kernel
-template <bool kStats, int kBS, bool kPF>
-__global__ __launch_bounds__(kBS) void ceres_shadow(const KParams P) {
+template <bool kStats>
+__global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* stk = lds + tid;
-    // per-shard job prefix, read by every wave from the shard counters (scalar loads)
-    uint32_t pre[kShards + 1];
-    pre[0] = 0;
+    // per-shard job prefix in LDS (a per-lane binary search over a register array would be
+    // dynamically indexed and spill to scratch): wave 0 scans the 32 shard counters
+    __shared__ uint32_t pre[kShards + 1];
+    if (wave == 0) {
+        uint32_t x = lane < kShards ? P.shards[lane].queued : 0u;
 #pragma unroll
-    for (int s = 0; s < kShards; ++s) pre[s + 1] = pre[s] + __builtin_amdgcn_readfirstlane(P.shards[s].queued);
+        for (int off = 1; off < kShards; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, 64);
+            if (lane >= uint32_t(off)) x += y;
+        }
+        if (lane < kShards) pre[lane + 1] = x;
+        if (lane == 0) pre[0] = 0;
+    }
+    __syncthreads();
     const uint32_t total = pre[kShards];
-    const F3 sun{P.sun[0], P.sun[1], P.sun[2]};
+    const uint32_t frame_pixels = P.local_rows * P.W;
     uint32_t occluded = 0, n_pairs = 0, n_tests = 0;
     bool overflow = false;
     unsigned long long t_begin = 0;
     Stamps stamps;
     if (kStats) t_begin = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t g = blockIdx.x * kBS + tid; g < total; g += gridDim.x * kBS) {
+    for (uint32_t g = blockIdx.x * kBlock + tid; g < total; g += gridDim.x * kBlock) {
         uint32_t s = 0;                                              // shard holding global job g
 #pragma unroll
         for (uint32_t step = 16; step > 0; step >>= 1)
@@ -362,209 +360,40 @@ __global__ __launch_bounds__(kBS) void ceres_shadow(const KParams P) {
         const float4 J0 = q[0], J1 = q[1];
         const uint32_t pix = __float_as_uint(J0.x), slot = __float_as_uint(J0.y);
         const float hu = J0.z, hv = J0.w;
+        const uint32_t f = P.frames > 1 ? pix / frame_pixels : 0;
+        const uint32_t rem = pix - f * frame_pixels;
+        const uint32_t lr = rem / P.W, i = rem - lr * P.W;
         const F3 o{J1.x, J1.y, J1.z};
-        const F3 sun_line = normalize(sun - o);                      // render.hpp:135
+        const F3 sun_line = normalize(f3(P.cam[f].sun) - o);        // render.hpp:135
         Hit h2{0, 0.f, 0.f, 0.f};
-        const bool blocked = trace<true, kStats, kBS, kPF>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow,
-                                                           kStats ? &stamps : nullptr);
-        const uint32_t lr = pix / P.W, i = pix - lr * P.W;
+        const bool blocked = trace<true, kStats>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow,
+                                                 kStats ? &stamps : nullptr);
         if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
         if (blocked) {                                               // render.hpp:147-150
             ++occluded;
-            store_pixel(P, lr, i, 0.f, 0.f, 0.f);
+            store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);
         } else {                                                     // render.hpp:139-146
-            const F3 view = primary_dir(P, i, global_row(P, lr));
+            const F3 view = primary_dir(P, f, i, global_row(P, lr));
             float c[3];
             shade(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
-            store_pixel(P, lr, i, c[0], c[1], c[2]);
+            store_pixel(P, f, lr, i, c[0], c[1], c[2]);
         }
     }
     const uint32_t wo = wave_sum(occluded);
-    const uint32_t shard = (blockIdx.x * (kBS / 64) + wave) % kShards;
+    const uint32_t shard = (blockIdx.x * (kBlock / 64) + wave) % kShards;
     if (lane == 0 && wo) atomicAdd(&P.shards[shard].hits, (unsigned long long)wo);
     if (kStats) {
         const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
-        uint32_t mp = n_pairs;                                       // max chain in the wave
+        uint32_t mp = n_pairs;                                       // longest chain in the wave
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) mp = max(mp, __shfl_xor(mp, off, 64));
         if (lane == 0) {
             atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
             atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
             if (P.wave_log) {                                        // diagnostic wave timeline
-                unsigned long long* w = P.wave_log + 8 * size_t(blockIdx.x * (kBS / 64) + wave);
-                uint32_t xcc = 0, hw = 0;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                unsigned long long* w = P.wave_log + 8 * size_t(blockIdx.x * (kBlock / 64) + wave);
                 w[0] = t_begin; w[1] = __builtin_amdgcn_s_memrealtime(); w[2] = mp; w[3] = stamps.iters;
                 w[4] = stamps.box; w[5] = stamps.leaf; w[6] = stamps.next; w[7] = wp;
-            }
-        }
-    }
-    if (overflow) atomicOr(&P.shards[shard].error, 1u);
-}
-
-// ---------------------------------------------------------------- persistent frame kernel
-// One launch per frame.  Each wavefront is an independent worker with a private LDS region:
-//   [stack: entries x 64 lanes][shadow-ray queue: 7 x 128 words (pixel, slot, u, v, px, py, pz)]
-// Loop: fetch a chunk of 8x8 tiles (dynamic, sharded counters); trace the tile's primary rays
-// (one pixel per lane, closest hit); write misses; COMPACT the hits' shadow rays into the
-// wave's LDS queue with __ballot + popcount prefix; whenever >= 64 are queued, trace a FULL
-// wavefront of shadow rays (any-hit) and shade them.  The queue is flushed when the work runs
-// out.  No global queue, no block barriers, no second launch; shadow rays stay coherent
-// (they come from the same tiles) and waves stay dense.
-constexpr int kFrameBlock = 128;          // 2 independent wavefronts per workgroup
-constexpr int kQueue = 128;               // shadow-ray queue capacity per wavefront
-constexpr int kQueueWords = 7 * kQueue;
-constexpr int kChunkTiles = 2;            // tiles per dynamic fetch
-constexpr int kTileShards = 16;           // tile counters (bands of the tile grid)
-
-__device__ __forceinline__ uint32_t band_begin(uint32_t s, uint32_t n_chunks) {
-    return uint32_t((uint64_t(n_chunks) * s) / kTileShards);
-}
-
-// Lane 0 claims the next chunk: its own band first, then the others (skipping drained ones).
-__device__ __forceinline__ uint32_t fetch_chunk(const KParams& P, uint32_t home, uint32_t lane) {
-    uint32_t got = 0xffffffffu;
-    if (lane == 0) {
-        uint32_t dead = __hip_atomic_load(&P.shards[0].exhausted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t k = 0; k < kTileShards; ++k) {
-            const uint32_t s = (home + k) % kTileShards;
-            if (dead & (1u << s)) continue;
-            const uint32_t b0 = band_begin(s, P.n_chunks), b1 = band_begin(s + 1, P.n_chunks);
-            const uint32_t v = atomicAdd(&P.shards[s].tiles, 1u);
-            if (v < b1 - b0) { got = b0 + v; break; }
-            atomicOr(&P.shards[0].exhausted, 1u << s);
-        }
-    }
-    return __builtin_amdgcn_readfirstlane(__shfl(got, 0, 64));
-}
-
-template <bool kStats>
-__device__ __forceinline__ void shade_queued(const KParams& P, uint32_t* q, uint32_t base, uint32_t count,
-                                             uint32_t lane, uint32_t* stk, uint32_t& occluded, uint32_t& traced,
-                                             uint32_t& n_pairs, uint32_t& n_tests, bool& overflow) {
-    if (lane >= count) return;
-    const uint32_t e = base + lane;
-    const uint32_t pix = q[e], slot = q[kQueue + e];
-    const float hu = __uint_as_float(q[2 * kQueue + e]), hv = __uint_as_float(q[3 * kQueue + e]);
-    const F3 o{__uint_as_float(q[4 * kQueue + e]), __uint_as_float(q[5 * kQueue + e]), __uint_as_float(q[6 * kQueue + e])};
-    const F3 sun{P.sun[0], P.sun[1], P.sun[2]};
-    const F3 sun_line = normalize(sun - o);                          // render.hpp:135
-    Hit h2{0, 0.f, 0.f, 0.f};
-    const bool blocked = trace<true, kStats, 64>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow);
-    ++traced;
-    const uint32_t lr = pix / P.W, i = pix - lr * P.W;
-    if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
-    if (blocked) {                                                   // render.hpp:147-150
-        ++occluded;
-        store_pixel(P, lr, i, 0.f, 0.f, 0.f);
-    } else {                                                         // render.hpp:139-146
-        const F3 view = primary_dir(P, i, global_row(P, lr));
-        float c[3];
-        shade(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
-        store_pixel(P, lr, i, c[0], c[1], c[2]);
-    }
-}
-
-template <int kMode, bool kStats>
-__global__ __launch_bounds__(kFrameBlock) void ceres_frame(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t lane = threadIdx.x & 63, wslot = threadIdx.x >> 6;
-    const uint32_t per_wave = P.stack_entries * 64 + kQueueWords;
-    uint32_t* base = lds + wslot * per_wave;
-    uint32_t* stk = base + lane;                                     // entry k of this lane at stk[k * 64]
-    uint32_t* q = base + P.stack_entries * 64;
-    const uint32_t wave_id = blockIdx.x * (kFrameBlock / 64) + wslot;
-    const uint32_t home = wave_id % kTileShards;
-    const F3 eye{P.eye[0], P.eye[1], P.eye[2]};
-    uint32_t qn = 0;                                                 // queued shadow rays (wave-uniform)
-    uint32_t hits = 0, occluded = 0, traced = 0, n_pairs = 0, n_tests = 0;
-    bool overflow = false;
-    // diagnostic stamps (stats build only): wall clock (100 MHz) + shader-clock fetch time
-    unsigned long long t_begin = 0, fetch_clk = 0, n_chunk = 0, n_batch = 0;
-    if (kStats) t_begin = __builtin_amdgcn_s_memrealtime();
-    auto fetch = [&]() {
-        unsigned long long c0 = 0;
-        if (kStats) c0 = __builtin_amdgcn_s_memtime();
-        const uint32_t r = fetch_chunk(P, home, lane);
-        if (kStats) { fetch_clk += __builtin_amdgcn_s_memtime() - c0; ++n_chunk; }
-        return r;
-    };
-    for (uint32_t chunk = fetch(); chunk < P.n_chunks; chunk = fetch()) {
-#pragma unroll 1
-        for (uint32_t t = chunk * kChunkTiles; t < (chunk + 1) * kChunkTiles && t < P.tiles_x * P.tiles_y; ++t) {
-            const uint32_t ty = t / P.tiles_x, tx = t - ty * P.tiles_x;
-            const uint32_t i = tx * 8 + (lane & 7), lr = ty * 8 + (lane >> 3);
-            bool job = false;
-            Hit h{0, 0.f, 0.f, 0.f};
-            F3 so{0.f, 0.f, 0.f};
-            if (i < P.W && lr < P.local_rows) {
-                const F3 view = primary_dir(P, i, global_row(P, lr));
-                const bool hit = trace<false, kStats, 64>(P, eye, view, stk, h, n_pairs, n_tests, overflow);
-                if (P.rec_prim) {
-                    const size_t px = size_t(lr) * P.W + i;
-                    P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
-                    P.rec_tuv[3 * px] = hit ? h.t : 0.f; P.rec_tuv[3 * px + 1] = hit ? h.u : 0.f; P.rec_tuv[3 * px + 2] = hit ? h.v : 0.f;
-                    P.rec_shadow[px] = -1;
-                }
-                if (!hit) {
-                    store_pixel(P, lr, i, 0.f, 0.f, 0.f);            // render.hpp:116-117
-                } else {
-                    ++hits;
-                    const TriV tr = load_tri(P.tris + h.slot);
-                    const F3 normal = normalize(tr.n);
-                    if (kMode == CERES_MODE_PRIMARY) {               // render.hpp:123-125
-                        store_pixel(P, lr, i, fabsf(normal.x), fabsf(normal.y), fabsf(normal.z));
-                    } else {                                         // render.hpp:127-133
-                        const F3 p1 = tr.p0 - tr.e1, p2 = tr.p0 + tr.e2;
-                        F3 p = tr.p0 * h.u + p1 * h.v + p2 * (1 - h.u - h.v);
-                        const float scale = -0.00001;
-                        so = p + normal * scale;
-                        job = true;
-                    }
-                }
-            }
-            if (kMode == CERES_MODE_FULL) {
-                const unsigned long long m = __ballot(job);
-                if (job) {                                           // append to the wave's LDS queue
-                    const uint32_t e = qn + __popcll(m & ((1ull << lane) - 1ull));
-                    q[e] = lr * P.W + i; q[kQueue + e] = h.slot;
-                    q[2 * kQueue + e] = __float_as_uint(h.u); q[3 * kQueue + e] = __float_as_uint(h.v);
-                    q[4 * kQueue + e] = __float_as_uint(so.x); q[5 * kQueue + e] = __float_as_uint(so.y);
-                    q[6 * kQueue + e] = __float_as_uint(so.z);
-                }
-                qn += __popcll(m);
-                __builtin_amdgcn_wave_barrier();
-                if (qn >= 64) {                                      // a full wavefront of shadow rays
-                    qn -= 64;
-                    if (kStats) ++n_batch;
-                    shade_queued<kStats>(P, q, qn, 64, lane, stk, occluded, traced, n_pairs, n_tests, overflow);
-                    __builtin_amdgcn_wave_barrier();
-                }
-            }
-        }
-    }
-    if (kMode == CERES_MODE_FULL && qn > 0)
-        shade_queued<kStats>(P, q, 0, qn, lane, stk, occluded, traced, n_pairs, n_tests, overflow);
-    // one set of counter atomics per wavefront
-    const uint32_t wh = wave_sum(hits + occluded), wq = wave_sum(traced);
-    const uint32_t shard = wave_id % kShards;
-    if (lane == 0) {
-        if (wh) atomicAdd(&P.shards[shard].hits, (unsigned long long)wh);
-        if (wq) atomicAdd(&P.shards[shard].queued, wq);
-    }
-    if (kStats) {
-        const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
-        if (lane == 0) {
-            atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
-            atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
-            if (P.wave_log) {
-                unsigned long long* w = P.wave_log + 8 * size_t(wave_id);
-                uint32_t xcc = 0, hw = 0;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-                w[0] = t_begin; w[1] = __builtin_amdgcn_s_memrealtime(); w[2] = n_chunk; w[3] = n_batch;
-                w[4] = fetch_clk; w[5] = wp; w[6] = (unsigned long long)xcc << 32 | hw; w[7] = wave_sum(traced);
             }
         }
     }
@@ -579,6 +408,39 @@ __global__ void ceres_finalize(const Shard* shards, uint64_t primary_rays, uint6
     for (int s = 0; s < kShards; ++s) { q += shards[s].queued; h += shards[s].hits; p += shards[s].pairs; t += shards[s].tests; err |= shards[s].error; }
     out[0] = primary_rays + q; out[1] = h; out[2] = primary_rays; out[3] = q;
     out[4] = p; out[5] = t; out[6] = err; out[7] = 0;
+}
+
+// ---------------------------------------------------------------- multi-GPU frame assembly
+// Un-interleaves the rank-major gathered RGB8 rows of a batch into F PPM
+// bodies: rank r's buffer (at r * rank_stride) holds its F frames back to back, n_r local rows
+// each, local row k at position n_r - 1 - k (as ceres_primary / ceres_shadow store them).
+// Output row y of frame f is global row j = H - 1 - y.  Pure copy: HBM-bound, 16-B vectors.
+__device__ __forceinline__ uint32_t rank_rows(uint32_t H, uint32_t rb, uint32_t r, uint32_t world) {
+    const uint32_t nb = (H + rb - 1) / rb;
+    if (r >= nb) return 0;
+    const uint32_t mine = (nb - 1 - r) / world + 1;                  // blocks r, r + world, ...
+    const bool has_last = (nb - 1) % world == r;                     // the possibly partial last block
+    return mine * rb - (has_last ? nb * rb - H : 0);
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(256) void ceres_assemble(const uint8_t* __restrict__ src, size_t rank_stride,
+                                                      uint8_t* __restrict__ dst, uint32_t frames, uint32_t H,
+                                                      uint32_t row_bytes, uint32_t rb, uint32_t world) {
+    const uint32_t units = kVec ? row_bytes / 16 : row_bytes;
+    for (uint32_t oy = blockIdx.y; oy < frames * H; oy += gridDim.y) {
+        const uint32_t f = oy / H, y = oy - f * H;
+        const uint32_t j = H - 1 - y;
+        const uint32_t b = j / rb, r = b % world;
+        const uint32_t k = (b / world) * rb + j % rb;
+        const uint32_t n = rank_rows(H, rb, r, world);
+        const uint8_t* s = src + r * rank_stride + (size_t(f) * n + (n - 1 - k)) * row_bytes;
+        uint8_t* d = dst + size_t(oy) * row_bytes;
+        for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+            if (kVec) reinterpret_cast<uint4*>(d)[u] = reinterpret_cast<const uint4*>(s)[u];
+            else d[u] = s[u];
+        }
+    }
 }
 
 }  // namespace dev
@@ -609,10 +471,6 @@ struct ceres_scene {
     int num_cus = 256;
     unsigned long long* d_wave_log = nullptr;   // stats scenes: per-wave diagnostic records
     size_t wave_log_waves = 0, last_grid_waves = 0;
-    int variant = 0;                   // kVariantTwoPass (default); kVariantWave / kVariantFrame via CERES_KERNEL
-    int frame_blocks_per_cu[4] = {0, 0, 0, 0};
-    uint32_t tiles_per_wave = 1;       // primary kernel (wave variant): 8x8 tiles per wavefront
-    bool pf_primary = false, pf_shadow = false; // (reserved variant bit, currently identical code)
     // optional per-kernel device timing (bench.py roofline leg)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -620,8 +478,6 @@ struct ceres_scene {
 };
 
 namespace {
-
-constexpr int kVariantTwoPass = 0, kVariantWave = 1, kVariantFrame = 2;
 
 #define HIP_TRY(expr)                                                                         \
     do {                                                                                      \
@@ -638,7 +494,7 @@ void scene_release(ceres_scene* s) {
     dfree(s->d_pairs); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
-    for (auto e : s->ev_used) if (e) (void)hipEventDestroy(e);
+    for (auto e : s->ev_used) (void)hipEventDestroy(e);
     s->ev_pool.clear(); s->ev_used.clear();
     if (s->stream) (void)hipStreamDestroy(s->stream);
     s->stream = nullptr;
@@ -649,72 +505,6 @@ size_t local_rows_of(size_t H, uint32_t rb, uint32_t rank, uint32_t world) {
     size_t rows = 0;
     for (size_t b = rank; b < nblocks; b += world) rows += std::min<size_t>(rb, H - b * rb);
     return rows;
-}
-
-// Re-lay the reference BVH (nodes32 + prim64) as depth-first SiblingPair records and the
-// triangles in leaf order.  Validates the structure (ranges, cycles) on the way.
-int relayout(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri48* tris,
-             std::vector<SiblingPair>& pairs, std::vector<Tri48>& leaf_tris, std::vector<uint32_t>& orig,
-             uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first) {
-    leaf_tris.resize(n_tri);
-    orig.resize(n_tri);
-    for (size_t k = 0; k < n_tri; ++k) {
-        if (prim[k] >= n_tri) return set_error(CERES_EINVAL, "primitive_indices[%zu] = %llu out of range", k, (unsigned long long)prim[k]);
-        leaf_tris[k] = tris[prim[k]];
-        orig[k] = uint32_t(prim[k]);
-    }
-    auto check_leaf = [&](const RefNode& n) -> bool {
-        return size_t(n.first_child_or_primitive) + n.primitive_count <= n_tri;
-    };
-    depth = 0;
-    root_leaf_count = root_leaf_first = 0;
-    if (nodes[0].primitive_count) {
-        if (!check_leaf(nodes[0])) return set_error(CERES_EINVAL, "root leaf range out of bounds");
-        root_leaf_count = nodes[0].primitive_count;
-        root_leaf_first = nodes[0].first_child_or_primitive;
-        pairs.assign(1, SiblingPair{});
-        return CERES_OK;
-    }
-    // pre-order DFS over inner nodes; each inner node's children become one record
-    struct Item { uint32_t node, pair, level; };
-    pairs.clear();
-    pairs.reserve(n_nodes / 2 + 1);
-    std::vector<Item> st;
-    if (size_t(nodes[0].first_child_or_primitive) + 1 >= n_nodes) return set_error(CERES_EINVAL, "root child index out of range");
-    pairs.emplace_back();
-    st.push_back({0, 0, 1});
-    size_t visited = 0;
-    while (!st.empty()) {
-        const Item it = st.back(); st.pop_back();
-        if (++visited > n_nodes) return set_error(CERES_EINVAL, "BVH has a cycle");
-        const RefNode& n = nodes[it.node];
-        const uint32_t c = n.first_child_or_primitive;
-        depth = std::max(depth, it.level);
-        SiblingPair& rec = pairs[it.pair];
-        std::memcpy(rec.lb, nodes[c].bounds, 24);
-        std::memcpy(rec.rb, nodes[c + 1].bounds, 24);
-        const RefNode* ch[2] = {&nodes[c], &nodes[c + 1]};
-        uint32_t cnt[2], first[2];
-        Item push[2]; int npush = 0;
-        for (int k = 0; k < 2; ++k) {
-            cnt[k] = ch[k]->primitive_count;
-            if (cnt[k]) {
-                if (!check_leaf(*ch[k])) return set_error(CERES_EINVAL, "leaf range out of bounds");
-                first[k] = ch[k]->first_child_or_primitive;
-            } else {
-                const uint32_t gc = ch[k]->first_child_or_primitive;
-                if (size_t(gc) + 1 >= n_nodes) return set_error(CERES_EINVAL, "child index out of range");
-                first[k] = uint32_t(pairs.size());
-                pairs.emplace_back();
-                push[npush++] = {c + uint32_t(k), first[k], it.level + 1};
-            }
-        }
-        SiblingPair& r2 = pairs[it.pair];                            // (emplace_back may have moved rec)
-        r2.lcount = cnt[0]; r2.lfirst = first[0];
-        r2.rcount = cnt[1]; r2.rfirst = first[1];
-        for (int k = npush - 1; k >= 0; --k) st.push_back(push[k]);   // left subtree first
-    }
-    return CERES_OK;
 }
 
 int ensure_workspace(ceres_scene* s, size_t jobs, size_t px, bool want_px, bool want_rgb) {
@@ -732,45 +522,50 @@ int ensure_workspace(ceres_scene* s, size_t jobs, size_t px, bool want_px, bool 
     return CERES_OK;
 }
 
-int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode, size_t W, size_t H,
+// One batch: `frames` cameras (basis12 = frames x {eye, dir, iu, iv}) and suns (frames x 3).
+int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* sun, int mode, size_t W, size_t H,
            const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream,
            int32_t* d_rec_prim = nullptr, float* d_rec_tuv = nullptr, int8_t* d_rec_shadow = nullptr) {
     if (!s || !basis12 || !sun) return set_error(CERES_EINVAL, "render: null argument");
+    if (frames == 0 || frames > uint32_t(kMaxFrames))
+        return set_error(CERES_EINVAL, "render: %u frames per batch (1..%d)", frames, kMaxFrames);
     if (mode != CERES_MODE_FULL && mode != CERES_MODE_PRIMARY) return set_error(CERES_EINVAL, "render: bad mode %d", mode);
     if (W == 0 || H == 0 || W > 65535u * 16u || H > 0xffffffu) return set_error(CERES_EINVAL, "render: bad size %zux%zu", W, H);
     ceres_tiling t{uint32_t(H), 0, 1};
     if (tiling) t = *tiling;
     if (t.world == 0 || t.rank >= t.world || t.row_block == 0) return set_error(CERES_EINVAL, "render: bad tiling");
     const size_t rows = local_rows_of(H, t.row_block, t.rank, t.world);
-    if (W * rows > 0xffffffffull) return set_error(CERES_EINVAL, "render: more than 2^32 pixels per rank");
-    HIP_TRY(hipSetDevice(s->device));
-    const bool twopass = s->variant != kVariantFrame;
+    if (size_t(frames) * W * rows > 0xffffffffull) return set_error(CERES_EINVAL, "render: more than 2^32 pixels per batch");
     const uint32_t bx = uint32_t((W + 15) / 16), by = uint32_t((rows + 15) / 16);
-    const size_t nblocks = size_t(bx) * by;
-    const uint32_t cap = uint32_t(((nblocks + kShards - 1) / kShards) * dev::kBlock);
-    if (twopass)
-        if (int rc = ensure_workspace(s, size_t(cap) * kShards, 0, false, false)) return rc;
+    if (size_t(by) * frames > 65535u) return set_error(CERES_EINVAL, "render: frames x row blocks exceeds the grid limit");
+    if ((d_rec_prim != nullptr) != (d_rec_tuv != nullptr) || (d_rec_prim != nullptr) != (d_rec_shadow != nullptr))
+        return set_error(CERES_EINVAL, "render: hit records need all three arrays");
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t nwaves = size_t(bx) * by * frames * (dev::kBlock / 64);
+    const uint32_t cap = uint32_t(((nwaves + kShards - 1) / kShards) * 64);   // <= 64 jobs per wavefront
+    if (int rc = ensure_workspace(s, size_t(cap) * kShards, 0, false, false)) return rc;
 
     KParams P{};
-    std::memcpy(P.eye, basis12, 12); std::memcpy(P.dir, basis12 + 3, 12);
-    std::memcpy(P.iu, basis12 + 6, 12); std::memcpy(P.iv, basis12 + 9, 12);
-    std::memcpy(P.sun, sun, 12);
+    for (uint32_t f = 0; f < frames; ++f) {
+        FrameCam& c = P.cam[f];
+        std::memcpy(c.eye, basis12 + 12 * f, 12); std::memcpy(c.dir, basis12 + 12 * f + 3, 12);
+        std::memcpy(c.iu, basis12 + 12 * f + 6, 12); std::memcpy(c.iv, basis12 + 12 * f + 9, 12);
+        std::memcpy(c.sun, sun + 3 * f, 12);
+    }
+    P.frames = frames;
     P.W = uint32_t(W); P.H = uint32_t(H);
     P.row_block = t.row_block; P.rank = t.rank; P.world = t.world; P.local_rows = uint32_t(rows);
+    P.row_blocks_per_frame = by;
     P.stack_entries = s->stack_entries;
     P.root_leaf_count = s->root_leaf_count; P.root_leaf_first = s->root_leaf_first;
     P.shard_capacity = cap;
-    P.tiles_x = uint32_t((W + 7) / 8); P.tiles_y = uint32_t((rows + 7) / 8);
-    P.n_chunks = uint32_t((size_t(P.tiles_x) * P.tiles_y + dev::kChunkTiles - 1) / dev::kChunkTiles);
     P.pairs = s->d_pairs; P.tris = s->d_tris; P.orig = s->d_orig; P.norms = s->d_norms;
     P.pixels = d_pixels; P.rgb8 = d_rgb8; P.jobs = s->d_jobs; P.shards = s->d_shards;
     P.rec_prim = d_rec_prim; P.rec_tuv = d_rec_tuv; P.rec_shadow = d_rec_shadow;
-    if ((d_rec_prim != nullptr) != (d_rec_tuv != nullptr) || (d_rec_prim != nullptr) != (d_rec_shadow != nullptr))
-        return set_error(CERES_EINVAL, "render: hit records need all three arrays");
 
     const bool stats = (s->flags & CERES_SCENE_STATS) != 0;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-    if (s->timing) {
+    if (s->timing && rows) {
         while (s->ev_pool.size() < 3) { hipEvent_t e; HIP_TRY(hipEventCreate(&e)); s->ev_pool.push_back(e); }
         e0 = s->ev_pool.back(); s->ev_pool.pop_back();
         e1 = s->ev_pool.back(); s->ev_pool.pop_back();
@@ -778,65 +573,25 @@ int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode
         s->ev_used.push_back(e0); s->ev_used.push_back(e1); s->ev_used.push_back(e2);
     }
     HIP_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, stream));
-    if (e0) HIP_TRY(hipEventRecord(e0, stream));
-    if (!twopass) {
-        // persistent frame kernel: one resident grid of independent wavefronts
-        const size_t lds = size_t(dev::kFrameBlock / 64) * (size_t(s->stack_entries) * 64 + dev::kQueueWords) * 4;
-        const int mi = (mode == CERES_MODE_PRIMARY ? 1 : 0) * 2 + (stats ? 1 : 0);
-        const void* fn[4] = {reinterpret_cast<const void*>(dev::ceres_frame<CERES_MODE_FULL, false>),
-                             reinterpret_cast<const void*>(dev::ceres_frame<CERES_MODE_FULL, true>),
-                             reinterpret_cast<const void*>(dev::ceres_frame<CERES_MODE_PRIMARY, false>),
-                             reinterpret_cast<const void*>(dev::ceres_frame<CERES_MODE_PRIMARY, true>)};
-        if (s->frame_blocks_per_cu[mi] <= 0) {
-            int nb = 0;
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn[mi], dev::kFrameBlock, lds));
-            s->frame_blocks_per_cu[mi] = std::max(1, nb);
-        }
-        const size_t want_waves = size_t(P.n_chunks);                 // never more waves than chunks
-        size_t grid = size_t(s->num_cus) * size_t(s->frame_blocks_per_cu[mi]);
-        grid = std::max<size_t>(1, std::min(grid, (want_waves + 1) / 2));
-        if (stats && s->wave_log_waves < grid * 2) {
-            dfree(s->d_wave_log);
-            HIP_TRY(hipMalloc(&s->d_wave_log, grid * 2 * 64));
-            s->wave_log_waves = grid * 2;
-        }
-        P.wave_log = stats ? s->d_wave_log : nullptr;
-        s->last_grid_waves = grid * 2;
-        switch (mi) {
-            case 0: hipLaunchKernelGGL((dev::ceres_frame<CERES_MODE_FULL, false>), dim3(uint32_t(grid)), dim3(dev::kFrameBlock), lds, stream, P); break;
-            case 1: hipLaunchKernelGGL((dev::ceres_frame<CERES_MODE_FULL, true>), dim3(uint32_t(grid)), dim3(dev::kFrameBlock), lds, stream, P); break;
-            case 2: hipLaunchKernelGGL((dev::ceres_frame<CERES_MODE_PRIMARY, false>), dim3(uint32_t(grid)), dim3(dev::kFrameBlock), lds, stream, P); break;
-            default: hipLaunchKernelGGL((dev::ceres_frame<CERES_MODE_PRIMARY, true>), dim3(uint32_t(grid)), dim3(dev::kFrameBlock), lds, stream, P); break;
-        }
-        HIP_TRY(hipGetLastError());
-        if (e1) HIP_TRY(hipEventRecord(e1, stream));
-        if (e2) { s->ev_used.back() = nullptr; s->ev_pool.push_back(e2); }   // single kernel: no shadow interval
-    } else {
-        const bool w64 = s->variant == kVariantWave;
-        const int bs = w64 ? 64 : dev::kBlock;
-        const size_t lds = size_t(s->stack_entries) * bs * 4;
-        dim3 grid(uint32_t((W + 15) / 16), uint32_t((rows + 15) / 16)), block(bs);
-        if (w64) grid = dim3(uint32_t((size_t(P.tiles_x) * P.tiles_y + s->tiles_per_wave - 1) / s->tiles_per_wave));
-#define CERES_PRIMARY(MODE, ST, BS, PF) hipLaunchKernelGGL((dev::ceres_primary<MODE, ST, BS, PF>), grid, block, lds, stream, P)
-#define CERES_PRIMARY_PF(MODE, ST, BS) do { if (s->pf_primary) CERES_PRIMARY(MODE, ST, BS, true); else CERES_PRIMARY(MODE, ST, BS, false); } while (0)
-        if (w64) {
-            if (mode == CERES_MODE_PRIMARY) { if (stats) CERES_PRIMARY_PF(CERES_MODE_PRIMARY, true, 64); else CERES_PRIMARY_PF(CERES_MODE_PRIMARY, false, 64); }
-            else { if (stats) CERES_PRIMARY_PF(CERES_MODE_FULL, true, 64); else CERES_PRIMARY_PF(CERES_MODE_FULL, false, 64); }
+    if (rows) {                                                      // a rank may own no rows
+        if (e0) HIP_TRY(hipEventRecord(e0, stream));
+        const size_t lds = size_t(s->stack_entries) * dev::kBlock * 4;
+        const dim3 grid(bx, by * frames), block(dev::kBlock);
+        if (mode == CERES_MODE_PRIMARY) {
+            if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, true>), grid, block, lds, stream, P);
+            else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, false>), grid, block, lds, stream, P);
         } else {
-            if (mode == CERES_MODE_PRIMARY) { if (stats) CERES_PRIMARY_PF(CERES_MODE_PRIMARY, true, 256); else CERES_PRIMARY_PF(CERES_MODE_PRIMARY, false, 256); }
-            else { if (stats) CERES_PRIMARY_PF(CERES_MODE_FULL, true, 256); else CERES_PRIMARY_PF(CERES_MODE_FULL, false, 256); }
+            if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, true>), grid, block, lds, stream, P);
+            else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, false>), grid, block, lds, stream, P);
         }
-#undef CERES_PRIMARY_PF
-#undef CERES_PRIMARY
         HIP_TRY(hipGetLastError());
         if (e1) HIP_TRY(hipEventRecord(e1, stream));
         if (mode == CERES_MODE_FULL) {
-            const size_t max_jobs = W * rows;
-            const size_t want = (max_jobs + bs - 1) / bs;
-            const size_t cap_blocks = size_t(s->num_cus) * (w64 ? 32 : 8);
-            const uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, cap_blocks)));
+            // one lane per queued shadow ray (at most one per pixel), grid-stride beyond 8 workgroups/CU
+            const size_t want = (size_t(frames) * W * rows + dev::kBlock - 1) / dev::kBlock;
+            const uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, size_t(s->num_cus) * 8)));
             if (stats) {
-                const size_t waves = size_t(sgrid) * (bs / 64);
+                const size_t waves = size_t(sgrid) * (dev::kBlock / 64);
                 if (s->wave_log_waves < waves) {
                     dfree(s->d_wave_log);
                     HIP_TRY(hipMalloc(&s->d_wave_log, waves * 64));
@@ -845,22 +600,26 @@ int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode
                 HIP_TRY(hipMemsetAsync(s->d_wave_log, 0, waves * 64, stream));
                 P.wave_log = s->d_wave_log;
                 s->last_grid_waves = waves;
+                hipLaunchKernelGGL((dev::ceres_shadow<true>), dim3(sgrid), block, lds, stream, P);
+            } else {
+                hipLaunchKernelGGL((dev::ceres_shadow<false>), dim3(sgrid), block, lds, stream, P);
             }
-#define CERES_SHADOW(ST, BS, PF) hipLaunchKernelGGL((dev::ceres_shadow<ST, BS, PF>), dim3(sgrid), block, lds, stream, P)
-#define CERES_SHADOW_PF(ST, BS) do { if (s->pf_shadow) CERES_SHADOW(ST, BS, true); else CERES_SHADOW(ST, BS, false); } while (0)
-            if (w64) { if (stats) CERES_SHADOW_PF(true, 64); else CERES_SHADOW_PF(false, 64); }
-            else { if (stats) CERES_SHADOW_PF(true, 256); else CERES_SHADOW_PF(false, 256); }
-#undef CERES_SHADOW_PF
-#undef CERES_SHADOW
             HIP_TRY(hipGetLastError());
         }
         if (e2) HIP_TRY(hipEventRecord(e2, stream));
     }
     if (d_counters) {
-        hipLaunchKernelGGL(dev::ceres_finalize, dim3(1), dim3(64), 0, stream, s->d_shards, uint64_t(W * rows), d_counters);
+        hipLaunchKernelGGL(dev::ceres_finalize, dim3(1), dim3(64), 0, stream, s->d_shards,
+                           uint64_t(frames) * W * rows, d_counters);
         HIP_TRY(hipGetLastError());
     }
     return CERES_OK;
+}
+
+void fill_stats(ceres_stats* st, const uint64_t c[8], double ms) {
+    if (!st) return;
+    st->rays = c[0]; st->hits = c[1]; st->primary_rays = c[2]; st->shadow_rays = c[3];
+    st->node_pairs = c[4]; st->tri_tests = c[5]; st->ms = ms;
 }
 
 }  // namespace
@@ -868,8 +627,8 @@ int launch(ceres_scene* s, const float basis12[12], const float sun[3], int mode
 extern "C" {
 
 const char* ceres_last_error(void) { return error_buffer(); }
-const char* ceres_version(void) { return "ceres-mi355x 0.1 (gfx950)"; }
-const char* ceres_kernel_names(void) { return "ceres_frame,ceres_primary,ceres_shadow,ceres_finalize"; }
+const char* ceres_version(void) { return "ceres-mi355x 0.2 (gfx950)"; }
+const char* ceres_kernel_names(void) { return "ceres_primary,ceres_shadow,ceres_finalize,ceres_assemble"; }
 
 size_t ceres_tiling_local_rows(size_t height, const ceres_tiling* t) {
     if (!t) return height;
@@ -888,25 +647,18 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     std::vector<Tri48> leaf_tris;
     std::vector<uint32_t> orig;
     uint32_t depth = 0, rlc = 0, rlf = 0;
-    if (relayout(static_cast<const RefNode*>(nodes32), n_nodes, prim64, n_tri, reinterpret_cast<const Tri48*>(tri48),
-                 pairs, leaf_tris, orig, depth, rlc, rlf))
+    if (relayout_bvh(static_cast<const RefNode*>(nodes32), n_nodes, prim64, n_tri, reinterpret_cast<const Tri48*>(tri48),
+                     pairs, leaf_tris, orig, depth, rlc, rlf))
         return nullptr;
     auto* s = new (std::nothrow) ceres_scene;
     if (!s) { set_error(CERES_ENOMEM, "out of host memory"); return nullptr; }
     s->device = device; s->flags = flags; s->n_tri = n_tri; s->n_pairs = pairs.size();
     s->depth = depth; s->root_leaf_count = rlc; s->root_leaf_first = rlf;
     s->stack_entries = std::max<uint32_t>(1, depth);                 // stack <= depth - 1 entries
-    if (const char* v = std::getenv("CERES_KERNEL"))
-        s->variant = std::strcmp(v, "wave") == 0 ? kVariantWave : std::strcmp(v, "frame") == 0 ? kVariantFrame : kVariantTwoPass;
-    if (const char* v = std::getenv("CERES_TPW")) s->tiles_per_wave = std::max(1, std::atoi(v));
-    if (const char* v = std::getenv("CERES_PF")) {                   // "pf_primary pf_shadow" bits, e.g. "01"
-        s->pf_primary = v[0] == '1';
-        s->pf_shadow = v[0] && v[1] ? v[1] == '1' : s->pf_primary;
-    }
-    auto fail = [&](int rc) -> ceres_scene* { (void)rc; scene_release(s); delete s; return nullptr; };
+    auto fail = [&]() -> ceres_scene* { scene_release(s); delete s; return nullptr; };
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { set_error(CERES_EHIP, "no HIP device available"); return fail(0); }
-    if (device < 0 || device >= ndev) { set_error(CERES_EINVAL, "device %d out of range (%d devices)", device, ndev); return fail(0); }
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { set_error(CERES_EHIP, "no HIP device available"); return fail(); }
+    if (device < 0 || device >= ndev) { set_error(CERES_EINVAL, "device %d out of range (%d devices)", device, ndev); return fail(); }
     auto body = [&]() -> int {
         HIP_TRY(hipSetDevice(device));
         hipDeviceProp_t prop;
@@ -927,7 +679,7 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
         HIP_TRY(hipMemcpy(s->d_norms, norm36, n_tri * 36, hipMemcpyHostToDevice));
         return CERES_OK;
     };
-    if (body()) return fail(0);
+    if (body()) return fail();
     return s;
 }
 
@@ -948,7 +700,40 @@ int ceres_scene_info(const ceres_scene* s, uint32_t* depth, uint32_t* stack_entr
 
 int ceres_render_device(ceres_scene* s, const float basis12[12], const float sun[3], int mode, size_t W, size_t H,
                         const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, void* stream) {
-    return launch(s, basis12, sun, mode, W, H, tiling, d_pixels, d_rgb8, d_counters, static_cast<hipStream_t>(stream));
+    return launch(s, 1, basis12, sun, mode, W, H, tiling, d_pixels, d_rgb8, d_counters, static_cast<hipStream_t>(stream));
+}
+
+int ceres_render_batch_device(ceres_scene* s, uint32_t frames, const float* basis12, const float* sun3, int mode,
+                              size_t W, size_t H, const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8,
+                              uint64_t* d_counters, void* stream) {
+    return launch(s, frames, basis12, sun3, mode, W, H, tiling, d_pixels, d_rgb8, d_counters,
+                  static_cast<hipStream_t>(stream));
+}
+
+int ceres_assemble_rgb8(const uint8_t* d_gathered, size_t rank_stride_bytes, uint8_t* d_out, uint32_t frames,
+                        size_t W, size_t H, uint32_t row_block, uint32_t world, void* stream) {
+    if (!d_gathered || !d_out || frames == 0 || W == 0 || H == 0 || row_block == 0 || world == 0)
+        return set_error(CERES_EINVAL, "ceres_assemble_rgb8: bad argument");
+    if (3 * W > 0xffffffffull || size_t(frames) * H > 0xffffffffull)
+        return set_error(CERES_EINVAL, "ceres_assemble_rgb8: frame too large");
+    const size_t max_rows = local_rows_of(H, row_block, 0, world);     // rank 0 owns the most rows
+    if (rank_stride_bytes < size_t(frames) * max_rows * 3 * W)
+        return set_error(CERES_EINVAL, "ceres_assemble_rgb8: rank stride smaller than a rank's batch");
+    const uint32_t row_bytes = uint32_t(3 * W);
+    const bool vec = row_bytes % 16 == 0 && rank_stride_bytes % 16 == 0 &&
+                     reinterpret_cast<uintptr_t>(d_gathered) % 16 == 0 && reinterpret_cast<uintptr_t>(d_out) % 16 == 0;
+    const uint32_t units = vec ? row_bytes / 16 : row_bytes;
+    const dim3 grid(uint32_t(std::min<size_t>((units + 255) / 256, 64)),
+                    uint32_t(std::min<size_t>(size_t(frames) * H, 65535)));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (vec)
+        hipLaunchKernelGGL(dev::ceres_assemble<true>, grid, dim3(256), 0, st, d_gathered, rank_stride_bytes, d_out,
+                           frames, uint32_t(H), row_bytes, row_block, world);
+    else
+        hipLaunchKernelGGL(dev::ceres_assemble<false>, grid, dim3(256), 0, st, d_gathered, rank_stride_bytes, d_out,
+                           frames, uint32_t(H), row_bytes, row_block, world);
+    HIP_TRY(hipGetLastError());
+    return CERES_OK;
 }
 
 int ceres_render_f32(ceres_scene* s, const float basis12[12], const float sun[3], int mode, float* pixels,
@@ -960,7 +745,7 @@ int ceres_render_f32(ceres_scene* s, const float basis12[12], const float sun[3]
     HIP_TRY(hipEventCreate(&a));
     HIP_TRY(hipEventCreate(&b));
     HIP_TRY(hipEventRecord(a, s->stream));
-    int rc = launch(s, basis12, sun, mode, W, H, nullptr, pixels ? s->d_pixels : nullptr, rgb8 ? s->d_rgb8 : nullptr,
+    int rc = launch(s, 1, basis12, sun, mode, W, H, nullptr, pixels ? s->d_pixels : nullptr, rgb8 ? s->d_rgb8 : nullptr,
                     s->d_counters, s->stream);
     if (rc) { (void)hipEventDestroy(a); (void)hipEventDestroy(b); return rc; }
     HIP_TRY(hipEventRecord(b, s->stream));
@@ -973,10 +758,7 @@ int ceres_render_f32(ceres_scene* s, const float basis12[12], const float sun[3]
     HIP_TRY(hipEventElapsedTime(&ms, a, b));
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    if (stats) {
-        stats->rays = c[0]; stats->hits = c[1]; stats->primary_rays = c[2]; stats->shadow_rays = c[3];
-        stats->node_pairs = c[4]; stats->tri_tests = c[5]; stats->ms = ms;
-    }
+    fill_stats(stats, c, ms);
     if (c[6]) return set_error(CERES_ESTACK, "traversal stack overflow");
     return CERES_OK;
 }
@@ -992,7 +774,7 @@ int ceres_render_records(ceres_scene* s, const float basis12[12], const float su
         cleanup();
         return set_error(CERES_ENOMEM, "ceres_render_records: device allocation failed");
     }
-    int rc = launch(s, basis12, sun, mode, W, H, nullptr, nullptr, nullptr, s->d_counters, s->stream, dp, dt, ds);
+    int rc = launch(s, 1, basis12, sun, mode, W, H, nullptr, nullptr, nullptr, s->d_counters, s->stream, dp, dt, ds);
     uint64_t c[8] = {0};
     if (!rc) {
         if (hipMemcpyAsync(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
@@ -1004,19 +786,16 @@ int ceres_render_records(ceres_scene* s, const float basis12[12], const float su
     }
     cleanup();
     if (rc) return rc;
-    if (stats) {
-        stats->rays = c[0]; stats->hits = c[1]; stats->primary_rays = c[2]; stats->shadow_rays = c[3];
-        stats->node_pairs = c[4]; stats->tri_tests = c[5]; stats->ms = 0;
-    }
+    fill_stats(stats, c, 0.0);
     if (c[6]) return set_error(CERES_ESTACK, "traversal stack overflow");
     return CERES_OK;
 }
 
 int ceres_scene_wave_log(ceres_scene* s, uint64_t* out, size_t max_waves, size_t* n_waves) {
     if (!s || !out || !n_waves) return set_error(CERES_EINVAL, "ceres_scene_wave_log: null argument");
-    if (!s->d_wave_log) return set_error(CERES_EINVAL, "wave log needs a CERES_SCENE_STATS scene and a persistent-kernel render");
+    if (!s->d_wave_log) return set_error(CERES_EINVAL, "wave log needs a CERES_SCENE_STATS scene and a full-mode render");
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(hipStreamSynchronize(nullptr));
+    HIP_TRY(hipDeviceSynchronize());
     const size_t n = std::min(max_waves, s->last_grid_waves);
     HIP_TRY(hipMemcpy(out, s->d_wave_log, n * 64, hipMemcpyDeviceToHost));
     *n_waves = n;
@@ -1024,7 +803,7 @@ int ceres_scene_wave_log(ceres_scene* s, uint64_t* out, size_t max_waves, size_t
 }
 
 // Per-kernel device timing for the roofline leg of bench.py: while enabled, every render
-// records HIP events around ceres_primary and ceres_shadow on the caller's stream.
+// records HIP events around ceres_primary and ceres_shadow on the launch stream.
 int ceres_scene_set_timing(ceres_scene* s, int enable) {
     if (!s) return set_error(CERES_EINVAL, "null scene");
     s->timing = enable != 0;
@@ -1039,13 +818,13 @@ int ceres_scene_read_timing(ceres_scene* s, double* primary_ms, double* shadow_m
     const size_t n = s->ev_used.size() / 3;
     for (size_t k = 0; k < n; ++k) {
         hipEvent_t e0 = s->ev_used[3 * k], e1 = s->ev_used[3 * k + 1], e2 = s->ev_used[3 * k + 2];
-        HIP_TRY(hipEventSynchronize(e2 ? e2 : e1));
+        HIP_TRY(hipEventSynchronize(e2));
         float a = 0.f, b = 0.f;
         HIP_TRY(hipEventElapsedTime(&a, e0, e1));
-        if (e2) HIP_TRY(hipEventElapsedTime(&b, e1, e2));
+        HIP_TRY(hipEventElapsedTime(&b, e1, e2));
         p += a; q += b;
     }
-    for (auto e : s->ev_used) if (e) s->ev_pool.push_back(e);
+    for (auto e : s->ev_used) s->ev_pool.push_back(e);
     s->ev_used.clear();
     if (primary_ms) *primary_ms = p;
     if (shadow_ms) *shadow_ms = q;

@@ -262,6 +262,74 @@ struct SahBuild {
 };
 
 }  // namespace
+
+// Re-lay the reference BVH (nodes32 + prim64) as depth-first SiblingPair records and the
+// triangles in leaf order (DESIGN.md "Data layout in HBM"), validating ranges and cycles.
+int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri48* tris,
+             std::vector<SiblingPair>& pairs, std::vector<Tri48>& leaf_tris, std::vector<uint32_t>& orig,
+             uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first) {
+    leaf_tris.resize(n_tri);
+    orig.resize(n_tri);
+    for (size_t k = 0; k < n_tri; ++k) {
+        if (prim[k] >= n_tri) return set_error(CERES_EINVAL, "primitive_indices[%zu] = %llu out of range", k, (unsigned long long)prim[k]);
+        leaf_tris[k] = tris[prim[k]];
+        orig[k] = uint32_t(prim[k]);
+    }
+    auto check_leaf = [&](const RefNode& n) -> bool {
+        return size_t(n.first_child_or_primitive) + n.primitive_count <= n_tri;
+    };
+    depth = 0;
+    root_leaf_count = root_leaf_first = 0;
+    if (nodes[0].primitive_count) {
+        if (!check_leaf(nodes[0])) return set_error(CERES_EINVAL, "root leaf range out of bounds");
+        root_leaf_count = nodes[0].primitive_count;
+        root_leaf_first = nodes[0].first_child_or_primitive;
+        pairs.assign(1, SiblingPair{});
+        return CERES_OK;
+    }
+    // pre-order DFS over inner nodes; each inner node's children become one record
+    struct Item { uint32_t node, pair, level; };
+    pairs.clear();
+    pairs.reserve(n_nodes / 2 + 1);
+    std::vector<Item> st;
+    if (size_t(nodes[0].first_child_or_primitive) + 1 >= n_nodes) return set_error(CERES_EINVAL, "root child index out of range");
+    pairs.emplace_back();
+    st.push_back({0, 0, 1});
+    size_t visited = 0;
+    while (!st.empty()) {
+        const Item it = st.back(); st.pop_back();
+        if (++visited > n_nodes) return set_error(CERES_EINVAL, "BVH has a cycle");
+        const RefNode& n = nodes[it.node];
+        const uint32_t c = n.first_child_or_primitive;
+        depth = std::max(depth, it.level);
+        SiblingPair& rec = pairs[it.pair];
+        std::memcpy(rec.lb, nodes[c].bounds, 24);
+        std::memcpy(rec.rb, nodes[c + 1].bounds, 24);
+        const RefNode* ch[2] = {&nodes[c], &nodes[c + 1]};
+        uint32_t cnt[2], first[2];
+        Item push[2]; int npush = 0;
+        for (int k = 0; k < 2; ++k) {
+            cnt[k] = ch[k]->primitive_count;
+            if (cnt[k]) {
+                if (!check_leaf(*ch[k])) return set_error(CERES_EINVAL, "leaf range out of bounds");
+                first[k] = ch[k]->first_child_or_primitive;
+            } else {
+                const uint32_t gc = ch[k]->first_child_or_primitive;
+                if (size_t(gc) + 1 >= n_nodes) return set_error(CERES_EINVAL, "child index out of range");
+                first[k] = uint32_t(pairs.size());
+                pairs.emplace_back();
+                push[npush++] = {c + uint32_t(k), first[k], it.level + 1};
+            }
+        }
+        SiblingPair& r2 = pairs[it.pair];                            // (emplace_back may have moved rec)
+        r2.lcount = cnt[0]; r2.lfirst = first[0];
+        r2.rcount = cnt[1]; r2.rfirst = first[1];
+        for (int k = npush - 1; k >= 0; --k) st.push_back(push[k]);   // left subtree first
+    }
+    return CERES_OK;
+}
+
+
 }  // namespace ceres
 
 using namespace ceres;
@@ -377,6 +445,48 @@ int ceres_camera_basis(const float eye[3], const float dir[3], const float up[3]
     v = scale(scale(v, w), ratio);
     const float o[9] = {d.x, d.y, d.z, u.x, u.y, u.z, v.x, v.y, v.z};
     std::memcpy(out9, o, sizeof o);
+    return CERES_OK;
+}
+
+// The orbit of anim.cpp:76-88: t = Transform<float>().rotate(axis, step / 180 * pi)
+// (transform.hpp:67-104, Markley-Crassidis matrix composed onto the identity) applied to the
+// camera eye, camera dir and sun once per frame; `up` is not rotated.  rotate_first = 1 is
+// anim.cpp's order (rotate, then render); 0 renders frame 0 at the start pose.
+int ceres_orbit_cameras(const float eye[3], const float dir[3], const float up[3], const float sun[3], float fov_deg,
+                        size_t width, size_t height, const float axis[3], float step_deg, uint32_t n_frames,
+                        int rotate_first, float* basis12, float* sun3, float* dir3) {
+    if (!eye || !dir || !up || !sun || !axis || !basis12 || !sun3 || !width || !height)
+        return set_error(CERES_EINVAL, "ceres_orbit_cameras: bad argument");
+    const float pi = float(3.14159265359);
+    const float angle = step_deg / 180.0f * pi;
+    const Vec n = vnormalize({axis[0], axis[1], axis[2]});
+    const float s = std::sin(angle), c = std::cos(angle);
+    const float m[3][3] = {
+        {c + (1 - c) * n.x * n.x, (1 - c) * n.x * n.y + s * n.z, (1 - c) * n.x * n.z - s * n.y},
+        {(1 - c) * n.y * n.x - s * n.z, c + (1 - c) * n.y * n.y, (1 - c) * n.y * n.z + s * n.x},
+        {(1 - c) * n.z * n.x + s * n.y, (1 - c) * n.z * n.y - s * n.x, c + (1 - c) * n.z * n.z}};
+    float a[3][3];                                          // identity * m, summed like transform.hpp:96-102
+    const float id[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int r = 0; r < 3; ++r)
+        for (int col = 0; col < 3; ++col) {
+            float acc = 0;
+            for (int i = 0; i < 3; ++i) acc += id[r][i] * m[i][col];
+            a[r][col] = acc;
+        }
+    auto apply = [&](Vec p) -> Vec {                        // operator(), transform.hpp:106-112 (v = 0)
+        return {a[0][0] * p.x + a[0][1] * p.y + a[0][2] * p.z + 0.0f,
+                a[1][0] * p.x + a[1][1] * p.y + a[1][2] * p.z + 0.0f,
+                a[2][0] * p.x + a[2][1] * p.y + a[2][2] * p.z + 0.0f};
+    };
+    Vec e{eye[0], eye[1], eye[2]}, d{dir[0], dir[1], dir[2]}, l{sun[0], sun[1], sun[2]};
+    for (uint32_t f = 0; f < n_frames; ++f) {
+        if (rotate_first || f > 0) { e = apply(e); d = apply(d); l = apply(l); }
+        const float ev[3] = {e.x, e.y, e.z}, dv[3] = {d.x, d.y, d.z};
+        basis12[12 * f] = e.x; basis12[12 * f + 1] = e.y; basis12[12 * f + 2] = e.z;
+        if (int rc = ceres_camera_basis(ev, dv, up, fov_deg, width, height, basis12 + 12 * f + 3)) return rc;
+        sun3[3 * f] = l.x; sun3[3 * f + 1] = l.y; sun3[3 * f + 2] = l.z;
+        if (dir3) { dir3[3 * f] = d.x; dir3[3 * f + 1] = d.y; dir3[3 * f + 2] = d.z; }
+    }
     return CERES_OK;
 }
 

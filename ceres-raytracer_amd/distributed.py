@@ -3,11 +3,14 @@
 One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on ROCm).  Rows are
 dealt in blocks of `row_block` rows round-robin over ranks (block b -> rank b % world), which
 balances the load: a mesh covers only the central rows of a frame, so contiguous bands
-would leave most ranks idle.  Every rank renders its rows with ceres_render_device
-(ceres_tiling) into a compact local RGB8 buffer (local row k stored at position n_k - 1 - k),
-and ONE collective per frame -- a gather of those buffers to rank 0 -- assembles the PPM
-body there.  The scene itself is replicated (uploaded per device, outside the timed region).
-The reference has no distributed code at all (render.hpp:104 is an OpenMP loop).
+would leave most ranks idle.  A step renders a BATCH of F frames (e.g. the anim.cpp orbit):
+every rank renders its rows of all F frames with ONE ceres_render_batch_device launch pair
+into a compact RGB8 buffer (frame-major, local row k of a frame at position n - 1 - k), and
+ONE collective per step -- a gather of those buffers to rank 0 -- brings all F frames there,
+where ceres_assemble_rgb8 un-interleaves them into F PPM bodies.  BatchGather is
+double-buffered: the gather (RCCL stream) and assembly (side stream) of step k overlap the
+render of step k + 1.  The scene is replicated (uploaded per device, outside the timed
+region).  The reference has no distributed code (render.hpp:104 is an OpenMP loop).
 """
 import numpy as np
 
@@ -22,50 +25,140 @@ def row_map(H, row_block, world):
     return out
 
 
-def ppm_row_permutation(H, row_block, world):
-    """Index into the concatenation of all ranks' padded local buffers (rank-major, `maxrows`
-    rows each) giving, for every PPM row (top-down), the source row."""
+def rank_rows(H, row_block, rank, world):
+    """Closed form of len(row_map(...)[rank]) -- the formula ceres_assemble uses on the device."""
+    nb = (H + row_block - 1) // row_block
+    if rank >= nb:
+        return 0
+    mine = (nb - 1 - rank) // world + 1
+    return mine * row_block - ((nb * row_block - H) if (nb - 1) % world == rank else 0)
+
+
+def batch_row_permutation(H, row_block, world, frames):
+    """For every output row (frame-major, PPM rows top-down), its row in the rank-major
+    concatenation of the gathered buffers (each rank: `frames * maxrows` rows, its frames
+    back to back with n_r rows each).  Returns (src [frames*H], maxrows)."""
     rows = row_map(H, row_block, world)
     maxrows = max(len(r) for r in rows)
-    src = np.empty(H, np.int64)
-    for r, jr in enumerate(rows):
-        n = len(jr)
-        k = np.arange(n)
-        # local row k sits at position n-1-k; global row j is PPM row H-1-j
-        src[H - 1 - jr] = r * maxrows + (n - 1 - k)
+    src = np.empty(frames * H, np.int64)
+    for f in range(frames):
+        for r, jr in enumerate(rows):
+            n = len(jr)
+            k = np.arange(n)
+            # local row k of frame f sits at f*n + n-1-k; global row j is PPM row H-1-j
+            src[f * H + H - 1 - jr] = r * frames * maxrows + f * n + (n - 1 - k)
     return src, maxrows
 
 
-class FrameGather:
-    """Gathers per-rank RGB8 row buffers into the full PPM body on rank `dst` (one collective)."""
+def ppm_row_permutation(H, row_block, world):
+    """Single-frame batch_row_permutation (rank buffers of `maxrows` rows)."""
+    return batch_row_permutation(H, row_block, world, 1)
 
-    def __init__(self, W, H, row_block, rank, world, device, dst=0, group=None):
+
+class BatchGather:
+    """Per-rank RGB8 buffers of an F-frame batch -> F PPM bodies on rank `dst`.
+
+    slots: number of buffer sets (2 = double buffering: fill slot k%2 while slot (k-1)%2 is
+    in flight).  On a GPU the un-interleave is ceres_assemble_rgb8 on a side stream; on CPU
+    (gloo tests) it is the same permutation applied with index_select.
+    """
+
+    def __init__(self, W, H, row_block, rank, world, frames=1, device="cpu", dst=0, group=None, slots=2):
         import torch
         self.W, self.H, self.rank, self.world, self.dst, self.group = W, H, rank, world, dst, group
-        src, self.maxrows = ppm_row_permutation(H, row_block, world)
-        self.local_rows = len(row_map(H, row_block, world)[rank])
+        self.frames, self.row_block, self.slots = frames, row_block, slots
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        src, self.maxrows = batch_row_permutation(H, row_block, world, frames)
+        self.local_rows = rank_rows(H, row_block, rank, world)
         self.row_bytes = 3 * W
-        # each rank renders into a padded buffer of maxrows rows; only the first local_rows are used
-        self.local = torch.zeros((self.maxrows, self.row_bytes), dtype=torch.uint8, device=device)
-        if rank == dst:
-            self.recv = [torch.zeros_like(self.local) for _ in range(world)]
-            self.perm = torch.as_tensor(src, device=device)
-            self.full = torch.empty((H, self.row_bytes), dtype=torch.uint8, device=device)
-        else:
-            self.recv = None
+        rows = frames * self.maxrows
+        # each rank's batch fills the first frames*local_rows rows; the rest pads to equal size
+        self.bufs = [torch.zeros((rows, self.row_bytes), dtype=torch.uint8, device=self.device)
+                     for _ in range(slots)]
+        self.is_dst = rank == dst
+        self.work = [None] * slots
+        if self.is_dst and world > 1:
+            self.recv = [torch.zeros((world, rows, self.row_bytes), dtype=torch.uint8, device=self.device)
+                         for _ in range(slots)]
+            self.full = [torch.empty((frames, H, self.row_bytes), dtype=torch.uint8, device=self.device)
+                         for _ in range(slots)]
+            self.perm = torch.as_tensor(src, device=self.device)
+            if self.cuda:
+                self.side = torch.cuda.Stream(device=self.device)
+                self.assembled = [torch.cuda.Event() for _ in range(slots)]
+                self.reused = [False] * slots
 
-    def local_ptr(self):
-        return self.local.data_ptr()
+    def local_ptr(self, slot=0):
+        return self.bufs[slot].data_ptr()
 
-    def gather(self):
-        """Collective: returns the (H, 3W) PPM body on dst, None elsewhere (asynchronous on GPU)."""
+    def frame_view(self, slot=0):
+        """World-1 output: the local buffer already is F PPM bodies."""
+        return self.bufs[slot][: self.frames * self.H].view(self.frames, self.H, self.row_bytes)
+
+    def start(self, slot=0):
+        """Launch the gather of `slot` (call after the render into bufs[slot] is enqueued)."""
         import torch
         import torch.distributed as dist
         if self.world == 1:
-            return self.local[: self.H]
-        dist.gather(self.local, self.recv if self.rank == self.dst else None, dst=self.dst, group=self.group)
-        if self.rank != self.dst:
+            return
+        if self.is_dst and self.cuda and self.reused[slot]:
+            # recv[slot] must not be overwritten before the previous assembly read it
+            torch.cuda.current_stream(self.device).wait_event(self.assembled[slot])
+        recv = list(self.recv[slot].unbind(0)) if self.is_dst else None
+        self.work[slot] = dist.gather(self.bufs[slot], recv, dst=self.dst, group=self.group, async_op=True)
+
+    def finish(self, slot=0):
+        """Complete `slot`: returns the (F, H, 3W) PPM bodies on dst (asynchronously, on the
+        side stream for GPUs), None elsewhere.  Also makes local[slot] safe to overwrite."""
+        import torch
+        if self.world == 1:
+            return self.frame_view(slot)
+        w = self.work[slot]
+        self.work[slot] = None
+        if w is None:
+            raise RuntimeError("BatchGather.finish without start")
+        if not self.cuda:
+            w.wait()
+            if not self.is_dst:
+                return None
+            flat = self.recv[slot].view(-1, self.row_bytes)
+            torch.index_select(flat, 0, self.perm, out=self.full[slot].view(-1, self.row_bytes))
+            return self.full[slot]
+        w.wait()                      # current stream: bufs[slot] may be reused after the send
+        if not self.is_dst:
             return None
-        stacked = torch.cat(self.recv, dim=0)
-        torch.index_select(stacked, 0, self.perm, out=self.full)
-        return self.full
+        import ceres_raytracer_amd as pkg
+        with torch.cuda.stream(self.side):
+            w.wait()                  # side stream waits for the collective
+            pkg.assemble_rgb8(self.recv[slot].data_ptr(), self.recv[slot][0].numel(), self.full[slot].data_ptr(),
+                              self.frames, self.W, self.H, self.row_block, self.world, self.side.cuda_stream)
+            self.assembled[slot].record(self.side)
+        self.reused[slot] = True
+        return self.full[slot]
+
+    def wait_assembled(self):
+        """Make the current stream wait for every issued assembly (end of a timed region)."""
+        import torch
+        if self.is_dst and self.world > 1 and self.cuda:
+            for s, used in enumerate(self.reused):
+                if used:
+                    torch.cuda.current_stream(self.device).wait_event(self.assembled[s])
+
+
+class FrameGather(BatchGather):
+    """Single frame, single buffer: gather() = start() + finish() -> (H, 3W) PPM body on dst."""
+
+    def __init__(self, W, H, row_block, rank, world, device, dst=0, group=None):
+        super().__init__(W, H, row_block, rank, world, frames=1, device=device, dst=dst, group=group, slots=1)
+        self.local = self.bufs[0]          # (maxrows, 3W): local row k at position local_rows-1-k
+
+    def gather(self):
+        self.start(0)
+        out = self.finish(0)
+        if out is None:
+            return None
+        if self.cuda and self.is_dst and self.world > 1:
+            import torch
+            torch.cuda.current_stream(self.device).wait_event(self.assembled[0])
+        return out[0]

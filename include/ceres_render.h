@@ -85,6 +85,14 @@ int ceres_bvh_build(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t
 /* Camera basis of render.hpp:91-97: out = {dir[3], image_u*w[3], image_v*w*ratio[3]}. */
 int ceres_camera_basis(const float eye[3], const float dir[3], const float up[3], float fov_deg,
                        size_t width, size_t height, float out9[9]);
+/* The camera/sun orbit of anim.cpp:76-88 (Transform::rotate, transform.hpp:67-112): per frame,
+ * eye, dir and sun are rotated by step_deg about `axis` (up is not); rotate_first = 1 rotates
+ * before frame 0 like anim.cpp, 0 starts at the given pose.  Writes n_frames x basis12
+ * ({eye, dir, image_u, image_v}, as ceres_camera_basis), n_frames x sun3 and, when dir3 is
+ * not NULL, n_frames x the rotated (un-normalised) camera dir. */
+int ceres_orbit_cameras(const float eye[3], const float dir[3], const float up[3], const float sun[3],
+                        float fov_deg, size_t width, size_t height, const float axis[3], float step_deg,
+                        uint32_t n_frames, int rotate_first, float* basis12, float* sun3, float* dir3);
 void ceres_free(void* p);
 
 /* ---- device scene ---- */
@@ -122,6 +130,23 @@ int ceres_render_f32(ceres_scene* scene, const float basis12[12], const float su
 int ceres_render_device(ceres_scene* scene, const float basis12[12], const float sun[3], int mode,
                         size_t width, size_t height, const ceres_tiling* tiling,
                         float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, void* stream);
+/* A batch of `frames` (1..32) frames of one scene in ONE launch pair -- the render() call
+ * that anim.cpp:93-110 makes once per orbit frame, batched.  basis12 = frames x 12 floats
+ * (eye, dir, iu, iv per frame), sun3 = frames x 3 floats.  Frame f of the batch occupies
+ * d_pixels[f*3*W*local_rows ...] / d_rgb8[f*3*W*local_rows ...], each laid out exactly as
+ * ceres_render_device's; counters are summed over the batch.  Every frame keeps its own
+ * camera and sun, and its pixels are bit-identical to a single-frame render. */
+int ceres_render_batch_device(ceres_scene* scene, uint32_t frames, const float* basis12,
+                              const float* sun3, int mode, size_t width, size_t height,
+                              const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8,
+                              uint64_t* d_counters, void* stream);
+/* Multi-GPU frame assembly (device pointers, async on `stream`): d_gathered holds `world`
+ * rank buffers, rank r at byte offset r * rank_stride_bytes, each = that rank's d_rgb8 output
+ * of a ceres_render_batch_device call with tiling {row_block, r, world} (F frames back to
+ * back).  Writes F PPM bodies (F x 3*W*H bytes) to d_out.  This is the un-interleave after the
+ * RCCL gather to rank 0; the reference renders on one host (render.hpp:104). */
+int ceres_assemble_rgb8(const uint8_t* d_gathered, size_t rank_stride_bytes, uint8_t* d_out, uint32_t frames,
+                        size_t width, size_t height, uint32_t row_block, uint32_t world, void* stream);
 /* Per-pixel hit records of one render (host buffers, W*H entries each, pixel = j*W + i):
  * prim = ORIGINAL triangle index of the primary hit or -1 (render.hpp:120), tuv = {t, u, v}
  * of that hit (triangle.hpp:95-115 convention), shadow = -1 (no shadow ray), 0 (lit) or

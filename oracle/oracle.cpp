@@ -442,6 +442,37 @@ int oracle_build_bvh(const float* tri48, size_t n, uint32_t** nodes32, size_t* n
     return 0;
 }
 
+// anim.cpp:76-88 orbit step: Transform<float>().rotate(axis, step/180*pi) (transform.hpp:67-104)
+// then operator() (transform.hpp:106-112) on eye, dir and sun, `count` times, in place.
+void oracle_orbit(const float axis[3], float step_deg, int count, float eye[3], float dir[3], float sun[3]) {
+    const float pi = float(3.14159265359);
+    const float angle = step_deg / 180.0f * pi;
+    const V3 n = normalize(V3{axis[0], axis[1], axis[2]});
+    const float nv[3] = {n.x, n.y, n.z};
+    const float s = std::sin(angle), c = std::cos(angle);
+    float m[3][3];
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) m[r][k] = (1 - c) * nv[r] * nv[k];
+    // Markley-Crassidis: diagonal c + (1-c) n_r n_r; off-diagonal (1-c) n_r n_k -/+ s n_j
+    m[0][0] = c + m[0][0]; m[1][1] = c + m[1][1]; m[2][2] = c + m[2][2];
+    m[0][1] = m[0][1] + s * nv[2]; m[0][2] = m[0][2] - s * nv[1];
+    m[1][0] = m[1][0] - s * nv[2]; m[1][2] = m[1][2] + s * nv[0];
+    m[2][0] = m[2][0] + s * nv[1]; m[2][1] = m[2][1] - s * nv[0];
+    float a[3][3];
+    for (int r = 0; r < 3; ++r)                    // ret.a = identity * mat, accumulated from 0
+        for (int k = 0; k < 3; ++k) {
+            float acc = 0.0f;
+            for (int i = 0; i < 3; ++i) acc += (r == i ? 1.0f : 0.0f) * m[i][k];
+            a[r][k] = acc;
+        }
+    auto apply = [&](float* p) {
+        float q[3];
+        for (int r = 0; r < 3; ++r) q[r] = a[r][0] * p[0] + a[r][1] * p[1] + a[r][2] * p[2] + 0.0f;
+        p[0] = q[0]; p[1] = q[1]; p[2] = q[2];
+    };
+    for (int k = 0; k < count; ++k) { apply(eye); apply(dir); apply(sun); }
+}
+
 // Camera basis, render.hpp:91-97.  out = {dir, image_u*w, image_v*w*ratio}.
 void oracle_camera_basis(const float eye[3], const float dir[3], const float up[3], float fov,
                          size_t W, size_t H, float out[9]) {

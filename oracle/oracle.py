@@ -42,6 +42,8 @@ def lib():
         L.oracle_build_bvh.argtypes = [_fp, _sz, ctypes.POINTER(_u32p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p)]
         L.oracle_camera_basis.argtypes = [_fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp]
         L.oracle_camera_basis.restype = None
+        L.oracle_orbit.argtypes = [_fp, ctypes.c_float, ctypes.c_int, _fp, _fp, _fp]
+        L.oracle_orbit.restype = None
         L.oracle_render.argtypes = [_fp, _fp, _sz, _u32p, _sz, _u64p, _fp, _fp, _fp, ctypes.c_int, _sz, _sz,
                                     _fp, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int32), _fp,
                                     ctypes.POINTER(ctypes.c_int8), _u64p, ctypes.c_int, _u32p]
@@ -107,6 +109,27 @@ def camera_basis(eye, dir, up, fov, W, H):
     return out
 
 
+def orbit(axis, step_deg, count, eye, dir, sun):
+    """anim.cpp:76-88: eye, dir, sun after `count` Transform rotations (oracle restatement)."""
+    f3 = lambda v: np.array(v, np.float32)  # noqa: E731
+    a, e, d, s = f3(axis), f3(eye), f3(dir), f3(sun)
+    lib().oracle_orbit(_ptr(a, ctypes.c_float), float(np.float32(step_deg)), int(count), _ptr(e, ctypes.c_float),
+                       _ptr(d, ctypes.c_float), _ptr(s, ctypes.c_float))
+    return e, d, s
+
+
+def pose(cfg, frame=0):
+    """(eye, dir, sun) of a config; configs with "orbit": (axis, step_deg, count) are rotated
+    count + frame times like anim.cpp's camera/sun."""
+    eye, dir, sun = cfg["eye"], cfg["dir"], cfg["sun"]
+    n = (cfg["orbit"][2] if cfg.get("orbit") else 0) + frame
+    if n:
+        axis, step = (cfg["orbit"][0], cfg["orbit"][1]) if cfg.get("orbit") else (cfg["orbit_axis"], cfg["orbit_step"])
+        return orbit(axis, step, n, eye, dir, sun)
+    f3 = lambda v: np.array(v, np.float32)  # noqa: E731
+    return f3(eye), f3(dir), f3(sun)
+
+
 def prepare(cfg):
     """Scene prep of the reference app (obj load, rotate, BVH build, camera basis) for a config dict."""
     import sys
@@ -118,16 +141,19 @@ def prepare(cfg):
     if cfg.get("rotate"):
         rotate(tri, cfg["rotate"][0], cfg["rotate"][1])
     nodes, prim = build_bvh(tri)
-    basis = camera_basis(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"], cfg["W"], cfg["H"])
-    return dict(tri=tri, norm=nor, nodes=nodes, prim=prim, basis=basis)
+    eye, dir, sun = pose(cfg)
+    basis = camera_basis(eye, dir, cfg["up"], cfg["fov"], cfg["W"], cfg["H"])
+    return dict(tri=tri, norm=nor, nodes=nodes, prim=prim, basis=basis, eye=eye, sun=sun)
 
 
-def render(scene, cfg, basis=None, want_pixels=True, want_ppm=True, want_records=False, threads=0, want_pairs=False):
+def render(scene, cfg, basis=None, want_pixels=True, want_ppm=True, want_records=False, threads=0, want_pairs=False,
+           eye=None, sun=None):
+    """oracle_render of one frame; basis (9 floats), eye and sun default to the config's pose."""
     L = lib()
     W, H = cfg["W"], cfg["H"]
     basis = scene["basis"] if basis is None else np.asarray(basis, np.float32)
-    eye = np.asarray(cfg["eye"], np.float32)
-    sun = np.asarray(cfg["sun"], np.float32)
+    eye = np.asarray(scene.get("eye", cfg["eye"]) if eye is None else eye, np.float32)
+    sun = np.asarray(scene.get("sun", cfg["sun"]) if sun is None else sun, np.float32)
     px = np.zeros(3 * W * H, np.float32) if want_pixels else None
     ppm = np.zeros(3 * W * H, np.uint8) if want_ppm else None
     rp = np.zeros(W * H, np.int32) if want_records else None

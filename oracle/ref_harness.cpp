@@ -18,6 +18,8 @@
 //                  from render.hpp:105-150 with the reference traverser directly
 //   --stats        node-pair visits / triangle tests per ray type via the Statistics
 //                  overload (single_ray_traverser.hpp:132-135,161-163)
+//   --orbit ax ay az step count   apply anim.cpp:76-88's camera/sun Transform (transform.hpp)
+//                  `count` times before rendering (eye, dir, sun rotate; up does not)
 //   --dump p       write p.tri48 (rotated Triangle[]), p.norm36, p.nodes32, p.prim64
 //   --primary-only render.hpp:123-125 (commented-out normal visualisation) as the
 //                  primary-rays-only mode: pixel = |normalize(tri.n)|
@@ -40,6 +42,7 @@
 
 #include "render.hpp"
 #include "obj_norms.hpp"
+#include "transform.hpp"
 
 using Scalar   = float;
 using Vector3  = bvh::Vector3<Scalar>;
@@ -60,6 +63,8 @@ struct Args {
     int reps = 1;
     bool stats = false, primary_only = false;
     int proc = 0;  // >0: procedural heightfield with proc x proc vertices instead of an OBJ
+    Vector3 orbit_axis{0.f, 1.f, 0.f};
+    float orbit_step = 0.f; int orbit_count = 0;   // --orbit: anim.cpp camera/sun rotations
 };
 
 static Vector3 v3(char** a) { return Vector3(std::strtof(a[0], nullptr), std::strtof(a[1], nullptr), std::strtof(a[2], nullptr)); }
@@ -83,6 +88,7 @@ static bool parse(int argc, char** argv, Args& a) {
         else if (s == "--stats") a.stats = true;
         else if (s == "--primary-only") a.primary_only = true;
         else if (s == "--proc") { need(1); a.proc = std::atoi(argv[++i]); }
+        else if (s == "--orbit") { need(5); a.orbit_axis = v3(argv + i + 1); a.orbit_step = std::strtof(argv[i + 4], nullptr); a.orbit_count = std::atoi(argv[i + 5]); i += 5; }
         else if (s[0] == '-') { std::fprintf(stderr, "unknown flag %s\n", s.c_str()); return false; }
         else a.obj = s;
     }
@@ -124,7 +130,7 @@ int main(int argc, char** argv) {
     Args a;
     if (!parse(argc, argv, a)) {
         std::fprintf(stderr, "usage: ref_render <obj>|--proc N [--eye x y z] [--dir x y z] [--up x y z] [--fov f] [--sun x y z] "
-                             "[--rotate x|y|z deg] [--size W H] [--out f.ppm] [--float f] [--records f] [--dump p] [--reps n] [--stats] [--primary-only]\n");
+                             "[--rotate x|y|z deg] [--orbit ax ay az step_deg count] [--size W H] [--out f.ppm] [--float f] [--records f] [--dump p] [--reps n] [--stats] [--primary-only]\n");
         return 2;
     }
     std::vector<Triangle> triangles;
@@ -165,6 +171,17 @@ int main(int argc, char** argv) {
     }
 
     Camera<Scalar> camera{a.eye, a.dir, a.up, a.fov};
+    if (a.orbit_count > 0) {
+        // anim.cpp:76-88: the reference's own Transform applied orbit_count times
+        constexpr Scalar pi = Scalar(3.14159265359);
+        auto t_cam = Transform<Scalar>().rotate(a.orbit_axis, a.orbit_step / 180.0f * pi);
+        auto t_sun = Transform<Scalar>().rotate(a.orbit_axis, a.orbit_step / 180.0f * pi);
+        for (int k = 0; k < a.orbit_count; ++k) {
+            camera.eye = t_cam(camera.eye);
+            camera.dir = t_cam(camera.dir);
+            a.sun = t_sun(a.sun);
+        }
+    }
     const size_t W = a.W, H = a.H;
     std::vector<Scalar> pixels(3 * W * H);
 
@@ -280,7 +297,9 @@ int main(int argc, char** argv) {
     std::sort(times.begin(), times.end());
     double med = times.empty() ? 0.0 : times[times.size() / 2];
     double best = times.empty() ? 0.0 : times[0];
-    char h[9][16];
+    char h[15][16];
+    hexf(h[9], camera.eye[0]); hexf(h[10], camera.eye[1]); hexf(h[11], camera.eye[2]);
+    hexf(h[12], a.sun[0]); hexf(h[13], a.sun[1]); hexf(h[14], a.sun[2]);
     hexf(h[0], dir[0]); hexf(h[1], dir[1]); hexf(h[2], dir[2]);
     hexf(h[3], image_u[0]); hexf(h[4], image_u[1]); hexf(h[5], image_u[2]);
     hexf(h[6], image_v[0]); hexf(h[7], image_v[1]); hexf(h[8], image_v[2]);
@@ -291,11 +310,12 @@ int main(int argc, char** argv) {
     std::printf("{\"n_tri\": %zu, \"n_nodes\": %zu, \"W\": %zu, \"H\": %zu, \"rays\": %d, \"hits\": %d, "
                 "\"render_ms_median\": %.4f, \"render_ms_best\": %.4f, \"reps\": %zu, \"threads\": %d, "
                 "\"load_ms\": %.3f, \"build_ms\": %.3f, "
-                "\"basis_dir\": [%s, %s, %s], \"basis_u\": [%s, %s, %s], \"basis_v\": [%s, %s, %s]",
+                "\"basis_dir\": [%s, %s, %s], \"basis_u\": [%s, %s, %s], \"basis_v\": [%s, %s, %s], "
+                "\"eye\": [%s, %s, %s], \"sun\": [%s, %s, %s]",
                 triangles.size(), bvh.node_count, W, H, rh.first, rh.second, med, best, times.size(), threads,
                 std::chrono::duration<double, std::milli>(t_load1 - t_load0).count(),
                 std::chrono::duration<double, std::milli>(t_b1 - t_b0).count(),
-                h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
+                h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13], h[14]);
     if (need_loop)
         std::printf(", \"loop_rays\": %zu, \"loop_hits\": %zu, \"loop_vs_render_mismatch\": %zu, "
                     "\"primary_pairs\": %zu, \"primary_tests\": %zu, \"shadow_rays\": %zu, \"shadow_pairs\": %zu, \"shadow_tests\": %zu",

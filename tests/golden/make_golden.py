@@ -115,6 +115,7 @@ def make(name):
                                        "shadow_pairs", "shadow_tests", "loop_vs_render_mismatch")},
         "ref": {k: j_ref[k] for k in ("rays", "hits")},
         "basis": {"dir": j_ex["basis_dir"], "u": j_ex["basis_u"], "v": j_ex["basis_v"]},
+        "pose": {"eye": j_ex["eye"], "sun": j_ex["sun"]},
         "ppm_sha256": {"exact": sha(ppm_ex), "ref": sha(ppm_ref)},
         "ppm_bytes_differing_ref_vs_exact": int(np.count_nonzero(diff)),
         "ppm_max_abs_diff_ref_vs_exact": int(np.abs(diff).max()) if diff.size else 0,

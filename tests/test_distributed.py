@@ -69,6 +69,77 @@ def test_gather_reassembles_reference_frame(world, row_block):
     assert q.get(timeout=10) is True
 
 
+def _batch_worker(rank, world, port, W, H, row_block, frames, q):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import import_package as ip
+    ip()
+    import ceres_raytracer_amd.distributed as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bodies = []
+        for name in ("dragon_333x217", "dragon_orbit3_333x217"):
+            with open(os.path.join(GOLDEN, name + ".exact.ppm.gz"), "rb") as f:
+                ppm = gzip.decompress(f.read())
+            hdr = len(b"P6 %d %d 255\n" % (W, H))
+            bodies.append(np.frombuffer(ppm[hdr:], np.uint8).reshape(H, 3 * W))
+        rng = np.random.default_rng(7)
+        while len(bodies) < 2 * frames:
+            bodies.append(rng.integers(0, 256, size=(H, 3 * W), dtype=np.uint8))
+        g = D.BatchGather(W, H, row_block, rank, world, frames=frames, device="cpu", slots=2)
+        rows = D.row_map(H, row_block, world)[rank]
+        n = len(rows)
+        assert g.local_rows == n
+        for slot in range(2):                      # two steps in flight (double buffering)
+            for f in range(frames):
+                body = bodies[slot * frames + f]
+                for k, j in enumerate(rows):
+                    g.bufs[slot][f * n + n - 1 - k] = torch.from_numpy(body[H - 1 - j].copy())
+            g.start(slot)
+        ok = True
+        for slot in range(2):
+            full = g.finish(slot)
+            if rank == 0:
+                for f in range(frames):
+                    ok &= bool(np.array_equal(full[f].numpy(), bodies[slot * frames + f]))
+            else:
+                ok &= full is None
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,row_block,frames", [(2, 16, 2), (3, 7, 3), (4, 16, 4)])
+def test_batch_gather_double_buffered(world, row_block, frames):
+    """F-frame batches (the bench's weak-scaling step), two steps in flight, gloo on CPU."""
+    import_package()
+    W, H = 333, 217
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batch_worker, args=(r, world, port, W, H, row_block, frames, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert all(res.values()), res
+
+
+def test_rank_rows_closed_form():
+    import_package()
+    import ceres_raytracer_amd.distributed as D
+    for H in (1, 7, 16, 17, 217, 1080, 4096):
+        for world in (1, 2, 3, 5, 8):
+            for rb in (1, 5, 16, 1000):
+                for r in range(world):
+                    assert D.rank_rows(H, rb, r, world) == len(D.row_map(H, rb, world)[r])
+
+
 def test_row_map_covers_every_row_once():
     pkg = import_package()
     import ceres_raytracer_amd.distributed as D

@@ -44,10 +44,18 @@ def scene_for(pkg, name, stats=False):
     return _scenes[key]
 
 
+def _hexf(hx):
+    return np.asarray([int(h, 16) for h in hx], np.uint32).view(np.float32)
+
+
 def pinned_basis(meta, cfg):
     """Camera basis from the fixture's hex bits (never trust the box's libm)."""
-    bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
-    return np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
+    eye = _hexf(meta["pose"]["eye"]) if "pose" in meta else np.asarray(cfg["eye"], np.float32)
+    return np.concatenate([eye, _hexf(meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"])])
+
+
+def pinned_sun(meta, cfg):
+    return _hexf(meta["pose"]["sun"]) if "pose" in meta else np.asarray(cfg["sun"], np.float32)
 
 
 @pytest.mark.parametrize("name", ALL)
@@ -62,7 +70,7 @@ def test_frame_matches_reference(gpu, name):
         import warnings
         warnings.warn("host libm camera basis differs from the fixture; rendering with the pinned basis")
     mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
-    px, rgb, st = scene.render(basis, cfg["sun"], W, H, mode=mode)
+    px, rgb, st = scene.render(basis, pinned_sun(meta, cfg), W, H, mode=mode)
     assert (st["rays"], st["hits"]) == (meta["exact"]["rays"], meta["exact"]["hits"])
     body = pkg.ppm(W, H, rgb)
     assert hashlib.sha256(body).hexdigest() == meta["ppm_sha256"]["exact"]
@@ -74,7 +82,7 @@ def test_frame_matches_reference(gpu, name):
 
 
 @pytest.mark.parametrize("name", ["bunny_640", "dragon_640", "proc_101", "dragon_333x217", "bunny_97x61_primary",
-                                  "tri1", "quad", "degenerate", "dragon_1080"])
+                                  "tri1", "quad", "degenerate", "dragon_1080", "dragon_orbit3_333x217"])
 def test_hit_records_match_reference(gpu, name):
     """prim / t / u / v / shadow per pixel, bit-exact vs the reference records (all pixels when small)."""
     pkg = gpu
@@ -83,7 +91,7 @@ def test_hit_records_match_reference(gpu, name):
     W, H = cfg["W"], cfg["H"]
     scene, _, _, _ = scene_for(pkg, name)
     mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
-    prim, tuv, sh, st = scene.records(pinned_basis(meta, cfg), cfg["sun"], W, H, mode=mode)
+    prim, tuv, sh, st = scene.records(pinned_basis(meta, cfg), pinned_sun(meta, cfg), W, H, mode=mode)
     pix = rec["pixel"].astype(np.int64)
     np.testing.assert_array_equal(prim[pix], rec["prim"])
     np.testing.assert_array_equal(sh[pix], rec["shadow"])
@@ -154,6 +162,116 @@ def test_row_tiling_reassembles_frame(gpu, world, row_block):
     body = pkg.ppm(W, H, full)
     assert hashlib.sha256(body).hexdigest() == meta["ppm_sha256"]["exact"]
     assert (rays, hits) == (meta["exact"]["rays"], meta["exact"]["hits"])
+
+
+def _oracle_frame(oracle_mod, sc, cfg, basis12, sun3):
+    return oracle_mod.render(sc, cfg, basis=basis12[3:], eye=basis12[:3], sun=sun3, want_pixels=False)
+
+
+@pytest.mark.parametrize("world,row_block,frames", [(1, 1080, 4), (3, 16, 3), (2, 5, 5)])
+def test_batch_orbit_frames_match_oracle(gpu, oracle_mod, world, row_block, frames):
+    """ceres_render_batch_device: F orbit frames (configs.BENCH_ORBIT, the bench's weak-scaling
+    batch) in one launch pair, each rank's rows of each frame, == per-frame oracle renders; frame
+    3 is the dragon_orbit3 fixture pose (reference Transform) and must match its PPM sha."""
+    import torch
+    pkg = gpu
+    import ceres_raytracer_amd.distributed as D
+    name = "dragon_333x217"
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    scene, _, _, _ = scene_for(pkg, name)
+    cam0 = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    axis, step = configs.BENCH_ORBIT
+    b12, s3 = pkg.orbit_cameras(cam0, cfg["sun"], W, H, frames, axis=axis, step_deg=step, rotate_first=False)
+    src, maxrows = D.ppm_row_permutation(H, row_block, world)
+    counters = torch.zeros(8, dtype=torch.int64, device="cuda")
+    per_rank = []
+    rays = hits = 0
+    for r in range(world):
+        t = pkg.Tiling(row_block, r, world)
+        rows = pkg.local_rows(H, t)
+        buf = torch.zeros((frames, maxrows, 3 * W), dtype=torch.uint8, device="cuda")
+        tight = torch.zeros((frames * rows * 3 * W,), dtype=torch.uint8, device="cuda")
+        scene.render_batch_device(b12, s3, W, H, tiling=t, d_rgb8=tight.data_ptr(), d_counters=counters.data_ptr(),
+                                  stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        buf[:, :rows] = tight.view(frames, rows, 3 * W)
+        c = counters.cpu().numpy()
+        rays += int(c[0]); hits += int(c[1])
+        per_rank.append(buf)
+    idx = torch.as_tensor(src, device="cuda")
+    sc = oracle_mod.prepare(cfg)
+    o_rays = o_hits = 0
+    for f in range(frames):
+        full = torch.cat([b[f] for b in per_rank])[idx].cpu().numpy().reshape(-1)
+        o = _oracle_frame(oracle_mod, sc, cfg, b12[f], s3[f])
+        o_rays += o["rays"]; o_hits += o["hits"]
+        np.testing.assert_array_equal(full, o["ppm"], err_msg=f"frame {f}")
+        if f == 3:
+            meta, _, _ = load_golden("dragon_orbit3_333x217")
+            assert hashlib.sha256(pkg.ppm(W, H, full)).hexdigest() == meta["ppm_sha256"]["exact"]
+    assert (rays, hits) == (o_rays, o_hits)
+
+
+def test_batch_float_pixels_match_single_frames(gpu):
+    """Batch float framebuffer == single-frame ceres_render_f32 per frame, bit for bit."""
+    import torch
+    pkg = gpu
+    name = "dragon_640"
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    scene, _, _, _ = scene_for(pkg, name)
+    cam0 = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    b12, s3 = pkg.orbit_cameras(cam0, cfg["sun"], W, H, 8, axis=configs.BENCH_ORBIT[0],
+                                step_deg=configs.BENCH_ORBIT[1], rotate_first=False)
+    px = torch.zeros((8, H, W, 3), dtype=torch.float32, device="cuda")
+    scene.render_batch_device(b12, s3, W, H, d_pixels=px.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = px.cpu().numpy()
+    for f in range(8):
+        ref, _, _ = scene.render(b12[f], s3[f], W, H, want_rgb8=False)
+        np.testing.assert_array_equal(got[f].reshape(-1).view(np.uint32), ref.view(np.uint32), err_msg=f"frame {f}")
+
+
+@pytest.mark.parametrize("W,H,row_block,world,frames", [(64, 48, 16, 3, 2), (333, 217, 7, 3, 3), (1920, 1080, 8, 8, 8),
+                                                        (16, 5, 16, 4, 1)])
+def test_assemble_kernel_matches_permutation(gpu, W, H, row_block, world, frames):
+    """ceres_assemble_rgb8 (16-B vector and byte paths) == the host permutation of distributed.py."""
+    import torch
+    pkg = gpu
+    import ceres_raytracer_amd.distributed as D
+    src, maxrows = D.batch_row_permutation(H, row_block, world, frames)
+    g = torch.randint(0, 256, (world, frames * maxrows, 3 * W), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((frames, H, 3 * W), dtype=torch.uint8, device="cuda")
+    pkg.assemble_rgb8(g.data_ptr(), g[0].numel(), out.data_ptr(), frames, W, H, row_block, world,
+                      torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = g.view(-1, 3 * W)[torch.as_tensor(src, device="cuda")].view(frames, H, 3 * W)
+    assert torch.equal(out, ref)
+
+
+def test_batch_rejects_bad_frame_counts(gpu):
+    pkg = gpu
+    scene, _, _, _ = scene_for(pkg, "tri1")
+    with pytest.raises(pkg.CeresError):
+        scene.render_batch_device(np.zeros((33, 12), np.float32), np.zeros((33, 3), np.float32), 8, 8)
+    with pytest.raises(pkg.CeresError):
+        scene.render_batch_device(np.zeros((2, 12), np.float32), np.zeros((3, 3), np.float32), 8, 8)
+
+
+def test_cli_orbit_frames(gpu, tmp_path):
+    """./render --orbit ... --frames 2 writes the anim.cpp orbit frames; frame 0 = fixture pose."""
+    pkg = gpu
+    name = "dragon_orbit3_333x217"
+    meta, _, ppm = load_golden(name)
+    out = tmp_path / "orbit.ppm"
+    args = configs.cli_args(configs.CONFIGS[name])
+    r = subprocess.run([pkg.CLI_PATH] + args + ["--frames", "2", "-o", str(out)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "orbit_000.ppm").read_bytes() == ppm["exact"]
+    assert (tmp_path / "orbit_001.ppm").exists()
+    assert "Total Rays:" in r.stdout
 
 
 def test_repeat_renders_are_deterministic(gpu):

@@ -29,8 +29,34 @@ def test_product_scene_prep_matches_reference(pkg, name):
     assert make_golden.canonical_bvh_sha(bvh.nodes.tobytes(), bvh.prim.tobytes()) == meta["bvh_canonical_sha256"]
     assert bvh.nodes.shape[0] == meta["n_nodes"]
     b = cam.basis(cfg["W"], cfg["H"])
-    assert hexbits(b[:3]) == hexbits(np.asarray(cfg["eye"], np.float32))
+    eye = meta["pose"]["eye"] if "pose" in meta else hexbits(np.asarray(cfg["eye"], np.float32))
+    assert hexbits(b[:3]) == eye
     assert hexbits(b[3:]) == meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]
+    if "pose" in meta:
+        assert hexbits(pkg.pose(cfg)[1]) == meta["pose"]["sun"]
+
+
+@pytest.mark.parametrize("name", ["dragon_orbit3_333x217", "bunny_orbit7_160x120"])
+def test_orbit_frames_match_reference_transform(pkg, oracle_mod, name):
+    """anim.cpp orbit (transform.hpp): the product's multi-frame orbit equals the reference pose
+    pinned by the fixture at frame `count`, and the oracle's restatement at every frame."""
+    meta, _, _ = load_golden(name)
+    cfg = configs.CONFIGS[name]
+    (axis, step, count) = cfg["orbit"]
+    cam0 = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    n = count + 4
+    b, s3 = pkg.orbit_cameras(cam0, cfg["sun"], cfg["W"], cfg["H"], n, axis=axis, step_deg=step, rotate_first=False)
+    assert hexbits(b[count, :3]) == meta["pose"]["eye"]
+    assert hexbits(b[count, 3:]) == meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]
+    assert hexbits(s3[count]) == meta["pose"]["sun"]
+    for k in range(n):
+        e, d, s = oracle_mod.orbit(axis, step, k, cfg["eye"], cfg["dir"], cfg["sun"])
+        assert hexbits(b[k, :3]) == hexbits(e) and hexbits(s3[k]) == hexbits(s)
+        assert hexbits(b[k, 3:]) == hexbits(oracle_mod.camera_basis(e, d, cfg["up"], cfg["fov"], cfg["W"], cfg["H"]))
+    # rotate_first (anim.cpp's own order) is the same sequence shifted by one frame
+    b1, s1 = pkg.orbit_cameras(cam0, cfg["sun"], cfg["W"], cfg["H"], n - 1, axis=axis, step_deg=step)
+    np.testing.assert_array_equal(b1.view(np.uint32), b[1:].view(np.uint32))
+    np.testing.assert_array_equal(s1.view(np.uint32), s3[1:].view(np.uint32))
 
 
 def test_product_matches_oracle_on_c5_mesh(pkg, oracle_mod):

@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
-"""A/B kernel variants in ONE process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
+"""A/B kernel builds in ONE process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
 
-usage: python tools/ab.py [config] [rounds] [variant ...]   (variants: wave twopass frame)
-Prints per-variant device ms per frame (HIP events around the launches), median and min,
-and checks every variant renders the reference PPM.
+usage: python tools/ab.py [config] [rounds] [lib.so ...]
+Each argument is a build of libceres_hip.so (default: the in-tree one), e.g. one made with
+`make -C ceres-raytracer_amd/csrc variant VARIANT=x DEFS=-DFOO`.  Every build is loaded as its
+own module instance (own ctypes handle, own HIP code object) and renders the config
+alternately; prints device ms per frame (HIP events), median and min, and PPM parity.
 """
 import hashlib
+import importlib.util
 import json
 import os
 import sys
@@ -13,45 +16,48 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(REPO, "ceres-raytracer_amd")
 sys.path.insert(0, os.path.join(REPO, "tests"))
-from conftest import import_package, load_golden  # noqa: E402
+from conftest import load_golden  # noqa: E402
+
+
+def load_build(path, tag):
+    spec = importlib.util.spec_from_file_location(f"ceres_ab_{tag}", os.path.join(PKG_DIR, "__init__.py"),
+                                                  submodule_search_locations=[PKG_DIR])
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.LIB_PATH = os.path.abspath(path)
+    mod.lib()
+    return mod
 
 
 def main():
+    import torch  # noqa: F401  (one HIP runtime for every build)
     name = sys.argv[1] if len(sys.argv) > 1 else "dragon_1080"
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    variants = sys.argv[3:] or ["wave", "twopass", "frame"]
-    pkg = import_package()
-    cfg = pkg.configs.CONFIGS[name]
+    libs = sys.argv[3:] or [os.path.join(PKG_DIR, "libceres_hip.so")]
     meta, _, _ = load_golden(name)
-    mesh, bvh, cam = pkg.prepare(cfg)
+    builds = {os.path.basename(p): load_build(p, i) for i, p in enumerate(libs)}
+    first = next(iter(builds.values()))
+    cfg = first.configs.CONFIGS[name]
+    mesh, bvh, cam = first.prepare(cfg)
     bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
     basis = np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
-    mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
-    scenes = {}
-    for v in variants:
-        # "kernel[:tiles_per_wave[:pf_bits]]", e.g. "wave:1:01" = wave variant, prefetch in shadow only
-        parts = v.split(":")
-        os.environ["CERES_KERNEL"] = parts[0]
-        os.environ["CERES_TPW"] = parts[1] if len(parts) > 1 and parts[1] else "1"
-        if len(parts) > 2:
-            os.environ["CERES_PF"] = parts[2]
-        else:
-            os.environ.pop("CERES_PF", None)
-        scenes[v] = pkg.Scene(mesh, bvh)
-    res = {v: [] for v in variants}
+    mode = first.MODE_PRIMARY if cfg["mode"] == "primary" else first.MODE_FULL
+    scenes = {k: m.Scene(mesh, bvh) for k, m in builds.items()}
     ok = {}
-    for v, sc in scenes.items():
+    for k, sc in scenes.items():
         _, rgb, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=False)
-        ok[v] = hashlib.sha256(pkg.ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
+        ok[k] = hashlib.sha256(builds[k].ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
     want_px = os.environ.get("AB_FLOAT", "1") == "1"
+    res = {k: [] for k in scenes}
     for _ in range(rounds):
-        for v, sc in scenes.items():
+        for k, sc in scenes.items():
             _, _, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=want_px, want_rgb8=True)
-            res[v].append(st["ms"])
-    out = {v: {"median_ms": round(float(np.median(r)), 4), "min_ms": round(float(np.min(r)), 4),
-               "mrays_s_median": round(meta["exact"]["rays"] / (np.median(r) * 1e3), 1), "parity": ok[v]}
-           for v, r in res.items()}
+            res[k].append(st["ms"])
+    out = {k: {"median_ms": round(float(np.median(r)), 4), "min_ms": round(float(np.min(r)), 4),
+               "mrays_s_median": round(meta["exact"]["rays"] / (np.median(r) * 1e3), 1), "parity": ok[k]}
+           for k, r in res.items()}
     print(json.dumps({"config": name, "rounds": rounds, "results": out}))
 
 
