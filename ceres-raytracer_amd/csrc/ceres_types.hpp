@@ -42,6 +42,17 @@ struct alignas(16) SiblingPair {
 };
 static_assert(sizeof(SiblingPair) == 64, "SiblingPair");
 
+// Shadow-ray BVH4 record (build_shadow_bvh4, scene_host.cpp): 4 child boxes as SoA float4
+// rows, then per-child count (0 inner -> first = Node4 index; kNode4Empty unused slot;
+// else leaf of `count` triangles from leaf slot `first`).  128 B = one L2 line.
+constexpr uint32_t kNode4Empty = 0xffffffffu;
+struct alignas(128) Node4 {
+    float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
+    uint32_t count[4];
+    uint32_t first[4];
+};
+static_assert(sizeof(Node4) == 128, "Node4");
+
 struct ShadowJob {             // one queued shadow ray (render.hpp:127-136), 32 B
     uint32_t pixel;            // batch pixel index = (frame * local_rows + local_row) * W + i
     uint32_t slot;             // leaf slot of the primary hit
@@ -78,7 +89,10 @@ struct KParams {
     uint32_t stack_entries;
     uint32_t root_leaf_count, root_leaf_first;   // root is a leaf (single_ray_traverser.hpp:72-73)
     uint32_t shard_capacity;                     // jobs per shard
+    uint32_t shadow_stack_entries;               // BVH4 traversal stack (shadow kernel)
+    uint32_t pad0_;
     const SiblingPair* pairs;
+    const Node4* nodes4;                         // shadow-ray BVH4 over the same leaf slots
     const Tri48* tris;
     const uint32_t* orig;
     const float* norms;
@@ -98,5 +112,7 @@ struct KParams {
 int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri48* tris,
                  std::vector<SiblingPair>& pairs, std::vector<Tri48>& leaf_tris, std::vector<uint32_t>& orig,
                  uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first);
+int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>& out, uint32_t& stack_bound,
+                      uint32_t& not_collapsed);
 
 }  // namespace ceres

@@ -188,6 +188,87 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
     return have;
 }
 
+// Any-hit traversal of the shadow BVH4 (build_shadow_bvh4): result-identical to trace<true>
+// (see the equivalence argument there).  Per step: one 128-B record, four slab tests with the
+// same fma/min/max restatement as trace(), the triangles of every passing leaf, then descend
+// into the nearest passing inner child and push the others.  The order only changes how soon
+// an occluder is found, never whether one is.
+template <bool kStats>
+__device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, uint32_t* stk, uint32_t& n_pairs,
+                                           uint32_t& n_tests, bool& overflow) {
+    const float tmin = 0.0f, tmax = FLT_MAX;
+    if (P.root_leaf_count) {
+        Hit h;
+        return trace<true, kStats>(P, o, d, stk, h, n_pairs, n_tests, overflow);
+    }
+    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
+    const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
+    const float sx = (-o.x) * ix, sy = (-o.y) * iy, sz = (-o.z) * iz;
+    uint32_t sp = 0, cur = 0;
+    while (true) {
+        if (kStats) ++n_pairs;
+        const float4* q = reinterpret_cast<const float4*>(P.nodes4 + cur);
+        const float4 LX = q[0], HX = q[1], LY = q[2], HY = q[3], LZ = q[4], HZ = q[5];
+        const uint4 CNT = reinterpret_cast<const uint4*>(q)[6];
+        const uint4 FST = reinterpret_cast<const uint4*>(q)[7];
+        float e[4], x[4];
+        const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
+        const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
+        const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
+        const uint32_t cnt[4] = {CNT.x, CNT.y, CNT.z, CNT.w}, fst[4] = {FST.x, FST.y, FST.z, FST.w};
+        uint32_t leaf_mask = 0, inner_mask = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float a0 = __builtin_fmaf(lx[c], ix, sx), a1 = __builtin_fmaf(hx[c], ix, sx);
+            const float b0 = __builtin_fmaf(ly[c], iy, sy), b1 = __builtin_fmaf(hy[c], iy, sy);
+            const float c0 = __builtin_fmaf(lz[c], iz, sz), c1 = __builtin_fmaf(hz[c], iz, sz);
+            e[c] = fmaxf(fminf(a0, a1), fmaxf(fminf(b0, b1), fmaxf(fminf(c0, c1), tmin)));
+            x[c] = fminf(fmaxf(a0, a1), fminf(fmaxf(b0, b1), fminf(fmaxf(c0, c1), tmax)));
+            const bool hit = e[c] <= x[c] && cnt[c] != kNode4Empty;
+            leaf_mask |= (hit && cnt[c] != 0) ? (1u << c) : 0u;
+            inner_mask |= (hit && cnt[c] == 0) ? (1u << c) : 0u;
+        }
+        // triangles of every passing leaf child, as one flattened loop (wave-coherent trip count)
+        uint32_t k = 0, k_end = 0;
+        while (true) {
+            if (k >= k_end) {
+                if (!leaf_mask) break;
+                const uint32_t c = __builtin_ctz(leaf_mask);
+                leaf_mask &= leaf_mask - 1;
+                k = c == 0 ? fst[0] : c == 1 ? fst[1] : c == 2 ? fst[2] : fst[3];
+                k_end = k + (c == 0 ? cnt[0] : c == 1 ? cnt[1] : c == 2 ? cnt[2] : cnt[3]);
+                if (kStats) n_tests += k_end - k;
+            }
+            float t, u, v;
+            if (tri_test(load_tri(P.tris + k), o, d, tmin, tmax, t, u, v)) return true;
+            ++k;
+        }
+        if (inner_mask) {
+            // nearest passing inner child next; the others go on the stack
+            uint32_t best = __builtin_ctz(inner_mask);
+            float be = e[0];
+            be = best == 1 ? e[1] : best == 2 ? e[2] : best == 3 ? e[3] : be;
+#pragma unroll
+            for (int c = 1; c < 4; ++c)
+                if ((inner_mask >> c & 1u) && e[c] < be) { be = e[c]; best = c; }
+            uint32_t rest = inner_mask & ~(1u << best);
+            if (sp + __builtin_popcount(rest) > P.shadow_stack_entries) { overflow = true; return false; }
+            while (rest) {
+                const uint32_t c = __builtin_ctz(rest);
+                rest &= rest - 1;
+                stk[sp * kBlock] = c == 0 ? fst[0] : c == 1 ? fst[1] : c == 2 ? fst[2] : fst[3];
+                ++sp;
+            }
+            cur = best == 0 ? fst[0] : best == 1 ? fst[1] : best == 2 ? fst[2] : fst[3];
+        } else {
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * kBlock];
+        }
+    }
+    return false;
+}
+
 __device__ __forceinline__ uint8_t quantize(float x) {               // static.cpp:141-143
     const float a = x * 255;
     const float m = (255.0f < a) ? 255.0f : a;                       // std::min(a, 255)
@@ -365,9 +446,13 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
         const uint32_t lr = rem / P.W, i = rem - lr * P.W;
         const F3 o{J1.x, J1.y, J1.z};
         const F3 sun_line = normalize(f3(P.cam[f].sun) - o);        // render.hpp:135
+#ifdef CERES_SHADOW_BVH2
         Hit h2{0, 0.f, 0.f, 0.f};
         const bool blocked = trace<true, kStats>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow,
                                                  kStats ? &stamps : nullptr);
+#else
+        const bool blocked = trace_any4<kStats>(P, o, sun_line, stk, n_pairs, n_tests, overflow);
+#endif
         if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
         if (blocked) {                                               // render.hpp:147-150
             ++occluded;
@@ -456,7 +541,10 @@ struct ceres_scene {
     uint32_t flags = 0;
     size_t n_tri = 0, n_pairs = 0;
     uint32_t depth = 0, stack_entries = 1, root_leaf_count = 0, root_leaf_first = 0;
+    uint32_t shadow_stack_entries = 1;
+    size_t n_nodes4 = 0;
     SiblingPair* d_pairs = nullptr;
+    Node4* d_nodes4 = nullptr;
     Tri48* d_tris = nullptr;
     uint32_t* d_orig = nullptr;
     float* d_norms = nullptr;
@@ -491,7 +579,7 @@ void dfree(T*& p) { if (p) { (void)hipFree(p); p = nullptr; } }
 void scene_release(ceres_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
-    dfree(s->d_pairs); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
+    dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
     for (auto e : s->ev_used) (void)hipEventDestroy(e);
@@ -557,9 +645,10 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     P.row_block = t.row_block; P.rank = t.rank; P.world = t.world; P.local_rows = uint32_t(rows);
     P.row_blocks_per_frame = by;
     P.stack_entries = s->stack_entries;
+    P.shadow_stack_entries = s->shadow_stack_entries;
     P.root_leaf_count = s->root_leaf_count; P.root_leaf_first = s->root_leaf_first;
     P.shard_capacity = cap;
-    P.pairs = s->d_pairs; P.tris = s->d_tris; P.orig = s->d_orig; P.norms = s->d_norms;
+    P.pairs = s->d_pairs; P.nodes4 = s->d_nodes4; P.tris = s->d_tris; P.orig = s->d_orig; P.norms = s->d_norms;
     P.pixels = d_pixels; P.rgb8 = d_rgb8; P.jobs = s->d_jobs; P.shards = s->d_shards;
     P.rec_prim = d_rec_prim; P.rec_tuv = d_rec_tuv; P.rec_shadow = d_rec_shadow;
 
@@ -590,6 +679,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             // one lane per queued shadow ray (at most one per pixel), grid-stride beyond 8 workgroups/CU
             const size_t want = (size_t(frames) * W * rows + dev::kBlock - 1) / dev::kBlock;
             const uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, size_t(s->num_cus) * 8)));
+            const size_t slds = size_t(std::max(s->stack_entries, s->shadow_stack_entries)) * dev::kBlock * 4;
             if (stats) {
                 const size_t waves = size_t(sgrid) * (dev::kBlock / 64);
                 if (s->wave_log_waves < waves) {
@@ -600,9 +690,9 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
                 HIP_TRY(hipMemsetAsync(s->d_wave_log, 0, waves * 64, stream));
                 P.wave_log = s->d_wave_log;
                 s->last_grid_waves = waves;
-                hipLaunchKernelGGL((dev::ceres_shadow<true>), dim3(sgrid), block, lds, stream, P);
+                hipLaunchKernelGGL((dev::ceres_shadow<true>), dim3(sgrid), block, slds, stream, P);
             } else {
-                hipLaunchKernelGGL((dev::ceres_shadow<false>), dim3(sgrid), block, lds, stream, P);
+                hipLaunchKernelGGL((dev::ceres_shadow<false>), dim3(sgrid), block, slds, stream, P);
             }
             HIP_TRY(hipGetLastError());
         }
@@ -650,8 +740,14 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     if (relayout_bvh(static_cast<const RefNode*>(nodes32), n_nodes, prim64, n_tri, reinterpret_cast<const Tri48*>(tri48),
                      pairs, leaf_tris, orig, depth, rlc, rlf))
         return nullptr;
+    std::vector<Node4> nodes4;
+    uint32_t stack4 = 0, not_collapsed = 0;
+    if (!rlc && build_shadow_bvh4(pairs, nodes4, stack4, not_collapsed)) return nullptr;
+    if (nodes4.empty()) nodes4.emplace_back();
     auto* s = new (std::nothrow) ceres_scene;
     if (!s) { set_error(CERES_ENOMEM, "out of host memory"); return nullptr; }
+    s->n_nodes4 = nodes4.size();
+    s->shadow_stack_entries = std::max<uint32_t>(1, stack4);
     s->device = device; s->flags = flags; s->n_tri = n_tri; s->n_pairs = pairs.size();
     s->depth = depth; s->root_leaf_count = rlc; s->root_leaf_first = rlf;
     s->stack_entries = std::max<uint32_t>(1, depth);                 // stack <= depth - 1 entries
@@ -668,6 +764,8 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
         s->num_cus = prop.multiProcessorCount;
         HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         HIP_TRY(hipMalloc(&s->d_pairs, pairs.size() * sizeof(SiblingPair)));
+        HIP_TRY(hipMalloc(&s->d_nodes4, nodes4.size() * sizeof(Node4)));
+        HIP_TRY(hipMemcpy(s->d_nodes4, nodes4.data(), nodes4.size() * sizeof(Node4), hipMemcpyHostToDevice));
         HIP_TRY(hipMalloc(&s->d_tris, n_tri * sizeof(Tri48)));
         HIP_TRY(hipMalloc(&s->d_orig, n_tri * sizeof(uint32_t)));
         HIP_TRY(hipMalloc(&s->d_norms, n_tri * 36));
@@ -694,7 +792,8 @@ int ceres_scene_info(const ceres_scene* s, uint32_t* depth, uint32_t* stack_entr
     if (depth) *depth = s->depth;
     if (stack_entries) *stack_entries = s->stack_entries;
     if (n_pairs) *n_pairs = s->n_pairs;
-    if (device_bytes) *device_bytes = s->n_pairs * sizeof(SiblingPair) + s->n_tri * (sizeof(Tri48) + 4 + 36);
+    if (device_bytes)
+        *device_bytes = s->n_pairs * sizeof(SiblingPair) + s->n_nodes4 * sizeof(Node4) + s->n_tri * (sizeof(Tri48) + 4 + 36);
     return CERES_OK;
 }
 

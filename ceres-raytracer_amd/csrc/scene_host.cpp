@@ -330,6 +330,72 @@ int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, siz
 }
 
 
+// Shadow-ray BVH4: each record holds up to 4 boxes, obtained by collapsing a sibling pair's
+// inner children into THEIR children (the grandchildren) when both grandchild boxes lie inside
+// the child's box (exact float comparison).  The slab test is monotone in the box bounds, so
+// with containment a grandchild box passing implies its parent box passing, and an any-hit
+// traversal of the BVH4 tests exactly the triangles of the leaves whose own boxes pass -- the
+// same set, with the same per-triangle arithmetic, as the BVH2 traversal of
+// single_ray_traverser.hpp:68-126 with tmax fixed at FLT_MAX (any-hit never lowers it before
+// it returns).  A child whose grandchildren are not contained (e.g. a box quirk of the builder's
+// quantile fallback) stays an entry of its own, so the equivalence holds unconditionally.
+// stack_bound: the most entries the traversal can ever hold (pushes along any root-leaf path).
+int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>& out, uint32_t& stack_bound,
+                      uint32_t& not_collapsed) {
+    struct Entry { const float* box; uint32_t count, first; };   // count 0: first = pair index
+    auto inside = [](const float* c, const float* p) {
+        return c[0] >= p[0] && c[1] <= p[1] && c[2] >= p[2] && c[3] <= p[3] && c[4] >= p[4] && c[5] <= p[5];
+    };
+    out.clear();
+    out.reserve(pairs.size() / 2 + 1);
+    stack_bound = 0;
+    not_collapsed = 0;
+    struct Item { uint32_t pair, node4, acc; };
+    std::vector<Item> st;
+    out.emplace_back();
+    st.push_back({0, 0, 0});
+    while (!st.empty()) {
+        const Item it = st.back(); st.pop_back();
+        const SiblingPair& P = pairs[it.pair];
+        Entry ents[4];
+        int n = 0;
+        const float* side_box[2] = {P.lb, P.rb};
+        const uint32_t side_cnt[2] = {P.lcount, P.rcount}, side_first[2] = {P.lfirst, P.rfirst};
+        for (int k = 0; k < 2; ++k) {
+            if (side_cnt[k]) { ents[n++] = {side_box[k], side_cnt[k], side_first[k]}; continue; }
+            const SiblingPair& Q = pairs[side_first[k]];
+            if (inside(Q.lb, side_box[k]) && inside(Q.rb, side_box[k])) {
+                ents[n++] = {Q.lb, Q.lcount, Q.lfirst};
+                ents[n++] = {Q.rb, Q.rcount, Q.rfirst};
+            } else {
+                ents[n++] = {side_box[k], 0, side_first[k]};
+                ++not_collapsed;
+            }
+        }
+        int inner = 0;
+        for (int c = 0; c < n; ++c) inner += ents[c].count == 0;
+        const uint32_t acc = it.acc + uint32_t(std::max(0, inner - 1));
+        stack_bound = std::max(stack_bound, acc);
+        Node4 rec{};
+        for (int c = 0; c < 4; ++c) {
+            if (c >= n) { rec.count[c] = kNode4Empty; rec.first[c] = 0; continue; }
+            rec.lo_x[c] = ents[c].box[0]; rec.hi_x[c] = ents[c].box[1];
+            rec.lo_y[c] = ents[c].box[2]; rec.hi_y[c] = ents[c].box[3];
+            rec.lo_z[c] = ents[c].box[4]; rec.hi_z[c] = ents[c].box[5];
+            rec.count[c] = ents[c].count;
+            if (ents[c].count) {
+                rec.first[c] = ents[c].first;
+            } else {
+                rec.first[c] = uint32_t(out.size());
+                out.emplace_back();
+                st.push_back({ents[c].first, rec.first[c], acc});
+            }
+        }
+        out[it.node4] = rec;
+    }
+    return CERES_OK;
+}
+
 }  // namespace ceres
 
 using namespace ceres;
