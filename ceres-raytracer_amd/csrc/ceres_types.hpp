@@ -70,7 +70,8 @@ struct alignas(128) Shard {
     unsigned long long pairs;  // node-pair visits (stats variant)
     unsigned long long tests;  // triangle tests (stats variant)
     unsigned long long primary;
-    uint32_t reserved[2];
+    uint32_t taken;            // persistent shadow kernel: jobs of this shard claimed so far
+    uint32_t reserved;
     uint32_t pad[20];
 };
 static_assert(sizeof(Shard) == 128, "Shard");

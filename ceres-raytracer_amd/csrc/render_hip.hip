@@ -193,6 +193,15 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
 // same fma/min/max restatement as trace(), the triangles of every passing leaf, then descend
 // into the nearest passing inner child and push the others.  The order only changes how soon
 // an occluder is found, never whether one is.
+struct N4 { float4 lx, hx, ly, hy, lz, hz; uint4 cnt, fst; };
+__device__ __forceinline__ N4 load_n4(const Node4* n) {
+    const float4* q = reinterpret_cast<const float4*>(n);
+    const uint4* u = reinterpret_cast<const uint4*>(n);
+    return {q[0], q[1], q[2], q[3], q[4], q[5], u[6], u[7]};
+}
+__device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
+__device__ __forceinline__ uint32_t pick(uint4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
+
 template <bool kStats>
 __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, uint32_t* stk, uint32_t& n_pairs,
                                            uint32_t& n_tests, bool& overflow) {
@@ -405,6 +414,15 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
 }
 
+#ifndef CERES_SHADOW_KERNEL
+#define CERES_SHADOW_KERNEL 1    // 0: one shadow ray per lane (ceres_shadow), 1: + intra-wavefront work stealing
+#endif
+#if CERES_SHADOW_KERNEL == 1
+#define CERES_SHADOW_FN ceres_shadow_steal
+#else
+#define CERES_SHADOW_FN ceres_shadow
+#endif
+
 // ---------------------------------------------------------------- shadow kernel
 template <bool kStats>
 __global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
@@ -480,6 +498,210 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
                 w[0] = t_begin; w[1] = __builtin_amdgcn_s_memrealtime(); w[2] = mp; w[3] = stamps.iters;
                 w[4] = stamps.box; w[5] = stamps.leaf; w[6] = stamps.next; w[7] = wp;
             }
+        }
+    }
+    if (overflow) atomicOr(&P.shards[shard].error, 1u);
+}
+
+// ---------------------------------------------------------------- work-stealing shadow kernel
+// One shadow ray per lane like ceres_shadow, but the wavefront shares the work of its rays:
+// a shadow ray is any-hit, so the subtrees left on a ray's stack may be traversed in any
+// order and by any lane, and the ray is occluded iff ANY of those pieces finds a triangle hit
+// (the same set of leaf tests as trace_any4, see build_shadow_bvh4).  After every step, lanes
+// that have finished their own piece take the BOTTOM entry (the largest pending subtree) of a
+// lane that still has stacked subtrees, together with that ray's origin / inverse direction
+// (cross-lane shuffles); a hit marks the owning lane's pixel occluded in LDS and cancels the
+// ray's other pieces.  A single long ray -- 60+ BVH4 steps on C3, which set the kernel's
+// duration in ceres_shadow -- is thus traversed by up to 64 lanes at once.  Pixels are shaded
+// together once the wavefront has no work left.  Stacks are per-lane ring buffers in LDS.
+struct RayWork {
+    F3 o, d;
+    float ix, iy, iz, sx, sy, sz;
+};
+
+template <bool kStats>
+__global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ uint32_t pre[kShards + 1];
+    __shared__ uint32_t s_blocked[kBlock];
+    __shared__ uint32_t s_mail[kBlock];                          // stolen node, by thief rank
+    __shared__ uint32_t s_from[kBlock];                          // donor lane, by thief rank
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wbase = wave * 64;
+    uint32_t* stk = lds + tid;
+    const uint32_t cap = P.shadow_stack_entries;
+    if (wave == 0) {
+        uint32_t x = lane < kShards ? P.shards[lane].queued : 0u;
+#pragma unroll
+        for (int off = 1; off < kShards; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, 64);
+            if (lane >= uint32_t(off)) x += y;
+        }
+        if (lane < kShards) pre[lane + 1] = x;
+        if (lane == 0) pre[0] = 0;
+    }
+    __syncthreads();
+    const uint32_t total = pre[kShards];
+    const uint32_t frame_pixels = P.local_rows * P.W;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    uint32_t occluded = 0, n_pairs = 0, n_tests = 0;
+    bool overflow = false;
+    const float tmin = 0.0f, tmax = FLT_MAX;
+    for (uint32_t g0 = blockIdx.x * kBlock; g0 < total; g0 += gridDim.x * kBlock) {
+        const uint32_t g = g0 + tid;
+        const bool has_job = g < total;
+        uint32_t pix = 0, slot = 0, f = 0;
+        float hu = 0.f, hv = 0.f;
+        RayWork w{};
+        if (has_job) {
+            uint32_t sh = 0;
+#pragma unroll
+            for (uint32_t step = 16; step > 0; step >>= 1)
+                if (pre[sh + step] <= g) sh += step;
+            const float4* q = reinterpret_cast<const float4*>(P.jobs + size_t(sh) * P.shard_capacity + (g - pre[sh]));
+            const float4 J0 = q[0], J1 = q[1];
+            pix = __float_as_uint(J0.x); slot = __float_as_uint(J0.y); hu = J0.z; hv = J0.w;
+            f = P.frames > 1 ? pix / frame_pixels : 0;
+            w.o = F3{J1.x, J1.y, J1.z};
+            w.d = normalize(f3(P.cam[f].sun) - w.o);                 // render.hpp:135
+            auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
+            w.ix = safe_inv(w.d.x); w.iy = safe_inv(w.d.y); w.iz = safe_inv(w.d.z);
+            w.sx = (-w.o.x) * w.ix; w.sy = (-w.o.y) * w.iy; w.sz = (-w.o.z) * w.iz;
+        }
+        const F3 sun_line = w.d;
+        s_blocked[tid] = 0;
+        bool active = has_job;
+        uint32_t owner = tid, cur = 0, top = 0, bot = 0, cnt = 0;
+        if (P.root_leaf_count) {                                       // single-leaf scene
+            if (has_job) {
+                Hit h;
+                s_blocked[tid] = trace<true, kStats>(P, w.o, w.d, stk, h, n_pairs, n_tests, overflow) ? 1u : 0u;
+            }
+            active = false;
+        }
+        __builtin_amdgcn_wave_barrier();
+        while (__ballot(active)) {
+            if (active && s_blocked[owner]) active = false;             // another piece found an occluder
+            if (active) {
+                if (kStats) ++n_pairs;
+                const N4 n = load_n4(P.nodes4 + cur);
+                float e[4];
+                uint32_t leaf_mask = 0, inner_mask = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float a0 = __builtin_fmaf(pick(n.lx, c), w.ix, w.sx), a1 = __builtin_fmaf(pick(n.hx, c), w.ix, w.sx);
+                    const float b0 = __builtin_fmaf(pick(n.ly, c), w.iy, w.sy), b1 = __builtin_fmaf(pick(n.hy, c), w.iy, w.sy);
+                    const float c0 = __builtin_fmaf(pick(n.lz, c), w.iz, w.sz), c1 = __builtin_fmaf(pick(n.hz, c), w.iz, w.sz);
+                    e[c] = fmaxf(fminf(a0, a1), fmaxf(fminf(b0, b1), fmaxf(fminf(c0, c1), tmin)));
+                    const float x = fminf(fmaxf(a0, a1), fminf(fmaxf(b0, b1), fminf(fmaxf(c0, c1), tmax)));
+                    const uint32_t cn = pick(n.cnt, c);
+                    const bool hit = e[c] <= x && cn != kNode4Empty;
+                    leaf_mask |= (hit && cn != 0) ? (1u << c) : 0u;
+                    inner_mask |= (hit && cn == 0) ? (1u << c) : 0u;
+                }
+                bool found = false;
+                uint32_t k = 0, k_end = 0;
+                while (true) {
+                    if (k >= k_end) {
+                        if (!leaf_mask) break;
+                        const uint32_t c = __builtin_ctz(leaf_mask);
+                        leaf_mask &= leaf_mask - 1;
+                        k = pick(n.fst, c);
+                        k_end = k + pick(n.cnt, c);
+                        if (kStats) n_tests += k_end - k;
+                    }
+                    float t, u, v;
+                    if (tri_test(load_tri(P.tris + k), w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
+                    ++k;
+                }
+                if (found) {
+                    s_blocked[owner] = 1u;
+                    active = false;
+                } else if (inner_mask) {
+                    uint32_t best = __builtin_ctz(inner_mask);
+                    float be = best == 0 ? e[0] : best == 1 ? e[1] : best == 2 ? e[2] : e[3];
+#pragma unroll
+                    for (int c = 1; c < 4; ++c)
+                        if ((inner_mask >> c & 1u) && e[c] < be) { be = e[c]; best = c; }
+                    uint32_t rest = inner_mask & ~(1u << best);
+                    if (cnt + __builtin_popcount(rest) > cap) { overflow = true; rest = 0; }
+                    while (rest) {
+                        const uint32_t c = __builtin_ctz(rest);
+                        rest &= rest - 1;
+                        stk[top * kBlock] = pick(n.fst, c);
+                        top = top + 1 == cap ? 0 : top + 1;
+                        ++cnt;
+                    }
+                    cur = pick(n.fst, best);
+                } else if (cnt) {
+                    top = (top == 0 ? cap : top) - 1;
+                    cur = stk[top * kBlock];
+                    --cnt;
+                } else {
+                    active = false;                                   // this piece is done, no hit
+                }
+            }
+            // idle lanes take the bottom stack entry of lanes with pending subtrees
+            const unsigned long long idle = __ballot(!active);
+            const unsigned long long donors = __ballot(active && cnt > 0);
+            if (idle && donors) {
+                const uint32_t n_idle = __popcll(idle), n_don = __popcll(donors);
+                if (active && cnt > 0) {
+                    const uint32_t r = __popcll(donors & lt_mask);
+                    if (r < n_idle) {
+                        s_mail[wbase + r] = stk[bot * kBlock];
+                        s_from[wbase + r] = lane;
+                        bot = bot + 1 == cap ? 0 : bot + 1;
+                        --cnt;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint32_t mail = 0, donor = 0;
+                const uint32_t r = __popcll(idle & lt_mask);
+                const bool thief = !active && r < n_don;
+                if (thief) { mail = s_mail[wbase + r]; donor = s_from[wbase + r]; }
+                // every lane runs the shuffles; only thieves keep the values
+                const float ox = __shfl(w.o.x, donor, 64), oy = __shfl(w.o.y, donor, 64), oz = __shfl(w.o.z, donor, 64);
+                const float dx = __shfl(w.d.x, donor, 64), dy = __shfl(w.d.y, donor, 64), dz = __shfl(w.d.z, donor, 64);
+                const float jx = __shfl(w.ix, donor, 64), jy = __shfl(w.iy, donor, 64), jz = __shfl(w.iz, donor, 64);
+                const float tx = __shfl(w.sx, donor, 64), ty = __shfl(w.sy, donor, 64), tz = __shfl(w.sz, donor, 64);
+                const uint32_t down = __shfl(owner, donor, 64);
+                if (thief) {
+                    w.o = F3{ox, oy, oz}; w.d = F3{dx, dy, dz};
+                    w.ix = jx; w.iy = jy; w.iz = jz; w.sx = tx; w.sy = ty; w.sz = tz;
+                    owner = down;
+                    cur = mail;
+                    top = bot = cnt = 0;
+                    active = true;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (has_job) {                                                   // shade every pixel together
+            const bool blocked = s_blocked[tid] != 0;
+            const uint32_t rem = pix - f * frame_pixels;
+            const uint32_t lr = rem / P.W, i = rem - lr * P.W;
+            if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
+            if (blocked) {                                               // render.hpp:147-150
+                ++occluded;
+                store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);
+            } else {                                                     // render.hpp:139-146
+                const F3 view = primary_dir(P, f, i, global_row(P, lr));
+                float c[3];
+                shade(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
+                store_pixel(P, f, lr, i, c[0], c[1], c[2]);
+            }
+        }
+        __syncthreads();                                                 // s_blocked reuse next round
+    }
+    const uint32_t wo = wave_sum(occluded);
+    const uint32_t shard = (blockIdx.x * (kBlock / 64) + wave) % kShards;
+    if (lane == 0 && wo) atomicAdd(&P.shards[shard].hits, (unsigned long long)wo);
+    if (kStats) {
+        const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
+        if (lane == 0) {
+            atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
+            atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
         }
     }
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
@@ -678,7 +900,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         if (mode == CERES_MODE_FULL) {
             // one lane per queued shadow ray (at most one per pixel), grid-stride beyond 8 workgroups/CU
             const size_t want = (size_t(frames) * W * rows + dev::kBlock - 1) / dev::kBlock;
-            const uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, size_t(s->num_cus) * 8)));
+            uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, size_t(s->num_cus) * 8)));
             const size_t slds = size_t(std::max(s->stack_entries, s->shadow_stack_entries)) * dev::kBlock * 4;
             if (stats) {
                 const size_t waves = size_t(sgrid) * (dev::kBlock / 64);
@@ -690,9 +912,9 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
                 HIP_TRY(hipMemsetAsync(s->d_wave_log, 0, waves * 64, stream));
                 P.wave_log = s->d_wave_log;
                 s->last_grid_waves = waves;
-                hipLaunchKernelGGL((dev::ceres_shadow<true>), dim3(sgrid), block, slds, stream, P);
+                hipLaunchKernelGGL((dev::CERES_SHADOW_FN<true>), dim3(sgrid), block, slds, stream, P);
             } else {
-                hipLaunchKernelGGL((dev::ceres_shadow<false>), dim3(sgrid), block, slds, stream, P);
+                hipLaunchKernelGGL((dev::CERES_SHADOW_FN<false>), dim3(sgrid), block, slds, stream, P);
             }
             HIP_TRY(hipGetLastError());
         }
