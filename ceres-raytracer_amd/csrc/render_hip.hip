@@ -68,6 +68,23 @@ __device__ __forceinline__ TriV load_tri(const Tri48* t) {
     return {{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, c.x}, {c.y, c.z, c.w}};
 }
 
+// Correctly rounded 1/x (IEEE division, as the reference's `1 / dot(n, d)`), fast path: one
+// Newton step r1 = fma(fma(-x, r0, 1), r0, r0) on the hardware estimate r0 = v_rcp_f32(x) is
+// bit-identical to the IEEE quotient for every normal |x| in [2^-126, 2^126) -- checked
+// exhaustively over all 2^32 inputs on gfx950 (tools/probes/rcp_exhaustive.hip,
+// tests/test_gpu_parity.py::test_fast_reciprocal_is_exact).  Zero, denormal, huge, inf and NaN
+// inputs take the full v_div_scale/fmas/fixup division.
+__device__ __forceinline__ float rcp_exact(float x) {
+#ifdef CERES_SLOW_RCP
+    return 1.0f / x;
+#else
+    const uint32_t m = __float_as_uint(x) & 0x7fffffffu;
+    if (__builtin_expect(m - 0x00800000u >= 0x7e000000u - 0x00800000u, 0)) return 1.0f / x;
+    const float r0 = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+#endif
+}
+
 // Per-ray hit; closest hit keeps the LAST accepted hit with t <= tmax (intersect_leaf :54-60).
 struct Hit { uint32_t slot; float t, u, v; };
 
@@ -76,7 +93,7 @@ __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin,
                                          float& u_out, float& v_out) {
     const F3 c = tr.p0 - o;
     const F3 r = cross(d, c);
-    const float inv_det = 1.0f / dot(tr.n, d);
+    const float inv_det = rcp_exact(dot(tr.n, d));
     const float u = dot(r, tr.e2) * inv_det;
     const float v = dot(r, tr.e1) * inv_det;
     const float w = 1.0f - u - v;
@@ -414,6 +431,9 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
 }
 
+#ifndef CERES_FUSED
+#define CERES_FUSED 1            // full mode as ONE kernel (ceres_fused) instead of primary + shadow
+#endif
 #ifndef CERES_SHADOW_KERNEL
 #define CERES_SHADOW_KERNEL 1    // 0: one shadow ray per lane (ceres_shadow), 1: + intra-wavefront work stealing
 #endif
@@ -519,16 +539,168 @@ struct RayWork {
     float ix, iy, iz, sx, sy, sz;
 };
 
+// LDS scratch of the work-stealing loop, per workgroup
+struct StealLds {
+    uint32_t blocked[kBlock];        // pixel of lane tid occluded (set by any piece of its ray)
+    uint32_t mail[kBlock];           // stolen node, by thief rank within the wavefront
+    uint32_t from[kBlock];           // donor lane, by thief rank
+};
+
+// Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
+// intra-wavefront work stealing; on return L.blocked[tid] holds the lane's answer.  Must be
+// reached by all 64 lanes of the wavefront (it loops on wavefront ballots).
+template <bool kStats>
+__device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, uint32_t* stk, StealLds& L,
+                                               uint32_t tid, uint32_t lane, uint32_t& n_pairs, uint32_t& n_tests,
+                                               bool& overflow) {
+    const float tmin = 0.0f, tmax = FLT_MAX;
+    const uint32_t cap = P.shadow_stack_entries;
+    const uint32_t wbase = tid & ~63u;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    L.blocked[tid] = 0;
+    bool active = has_job;
+    uint32_t owner = tid, cur = 0, top = 0, bot = 0, cnt = 0;
+    if (P.root_leaf_count) {                                           // single-leaf scene
+        if (has_job) {
+            Hit h;
+            L.blocked[tid] = trace<true, kStats>(P, w.o, w.d, stk, h, n_pairs, n_tests, overflow) ? 1u : 0u;
+        }
+        active = false;
+    }
+    __builtin_amdgcn_wave_barrier();
+    while (__ballot(active)) {
+        if (active && L.blocked[owner]) active = false;                 // another piece found an occluder
+        if (active) {
+            if (kStats) ++n_pairs;
+            const N4 n = load_n4(P.nodes4 + cur);
+            float e[4];
+            uint32_t leaf_mask = 0, inner_mask = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float a0 = __builtin_fmaf(pick(n.lx, c), w.ix, w.sx), a1 = __builtin_fmaf(pick(n.hx, c), w.ix, w.sx);
+                const float b0 = __builtin_fmaf(pick(n.ly, c), w.iy, w.sy), b1 = __builtin_fmaf(pick(n.hy, c), w.iy, w.sy);
+                const float c0 = __builtin_fmaf(pick(n.lz, c), w.iz, w.sz), c1 = __builtin_fmaf(pick(n.hz, c), w.iz, w.sz);
+                e[c] = fmaxf(fminf(a0, a1), fmaxf(fminf(b0, b1), fmaxf(fminf(c0, c1), tmin)));
+                const float x = fminf(fmaxf(a0, a1), fminf(fmaxf(b0, b1), fminf(fmaxf(c0, c1), tmax)));
+                const uint32_t cn = pick(n.cnt, c);
+                const bool hit = e[c] <= x && cn != kNode4Empty;
+                leaf_mask |= (hit && cn != 0) ? (1u << c) : 0u;
+                inner_mask |= (hit && cn == 0) ? (1u << c) : 0u;
+            }
+            bool found = false;
+            uint32_t k = 0, k_end = 0;
+            while (true) {
+                if (k >= k_end) {
+                    if (!leaf_mask) break;
+                    const uint32_t c = __builtin_ctz(leaf_mask);
+                    leaf_mask &= leaf_mask - 1;
+                    k = pick(n.fst, c);
+                    k_end = k + pick(n.cnt, c);
+                    if (kStats) n_tests += k_end - k;
+                }
+                float t, u, v;
+                if (tri_test(load_tri(P.tris + k), w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
+                ++k;
+            }
+            if (found) {
+                L.blocked[owner] = 1u;
+                active = false;
+            } else if (inner_mask) {
+                uint32_t best = __builtin_ctz(inner_mask);
+                float be = best == 0 ? e[0] : best == 1 ? e[1] : best == 2 ? e[2] : e[3];
+#pragma unroll
+                for (int c = 1; c < 4; ++c)
+                    if ((inner_mask >> c & 1u) && e[c] < be) { be = e[c]; best = c; }
+                uint32_t rest = inner_mask & ~(1u << best);
+                if (cnt + __builtin_popcount(rest) > cap) { overflow = true; rest = 0; }
+                while (rest) {
+                    const uint32_t c = __builtin_ctz(rest);
+                    rest &= rest - 1;
+                    stk[top * kBlock] = pick(n.fst, c);
+                    top = top + 1 == cap ? 0 : top + 1;
+                    ++cnt;
+                }
+                cur = pick(n.fst, best);
+            } else if (cnt) {
+                top = (top == 0 ? cap : top) - 1;
+                cur = stk[top * kBlock];
+                --cnt;
+            } else {
+                active = false;                                       // this piece is done, no hit
+            }
+        }
+        // idle lanes take the bottom stack entry of lanes with pending subtrees
+        const unsigned long long idle = __ballot(!active);
+        const unsigned long long donors = __ballot(active && cnt > 0);
+        if (idle && donors) {
+            const uint32_t n_idle = __popcll(idle), n_don = __popcll(donors);
+            if (active && cnt > 0) {
+                const uint32_t r = __popcll(donors & lt_mask);
+                if (r < n_idle) {
+                    L.mail[wbase + r] = stk[bot * kBlock];
+                    L.from[wbase + r] = lane;
+                    bot = bot + 1 == cap ? 0 : bot + 1;
+                    --cnt;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            uint32_t mail = 0, donor = 0;
+            const uint32_t r = __popcll(idle & lt_mask);
+            const bool thief = !active && r < n_don;
+            if (thief) { mail = L.mail[wbase + r]; donor = L.from[wbase + r]; }
+            // every lane runs the shuffles; only thieves keep the values
+            const float ox = __shfl(w.o.x, donor, 64), oy = __shfl(w.o.y, donor, 64), oz = __shfl(w.o.z, donor, 64);
+            const float dx = __shfl(w.d.x, donor, 64), dy = __shfl(w.d.y, donor, 64), dz = __shfl(w.d.z, donor, 64);
+            const float jx = __shfl(w.ix, donor, 64), jy = __shfl(w.iy, donor, 64), jz = __shfl(w.iz, donor, 64);
+            const float tx = __shfl(w.sx, donor, 64), ty = __shfl(w.sy, donor, 64), tz = __shfl(w.sz, donor, 64);
+            const uint32_t down = __shfl(owner, donor, 64);
+            if (thief) {
+                w.o = F3{ox, oy, oz}; w.d = F3{dx, dy, dz};
+                w.ix = jx; w.iy = jy; w.iz = jz; w.sx = tx; w.sy = ty; w.sz = tz;
+                owner = down;
+                cur = mail;
+                top = bot = cnt = 0;
+                active = true;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ RayWork make_shadow_ray(F3 o, F3 sun) {
+    RayWork w;
+    w.o = o;
+    w.d = normalize(sun - o);                                          // render.hpp:135
+    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
+    w.ix = safe_inv(w.d.x); w.iy = safe_inv(w.d.y); w.iz = safe_inv(w.d.z);
+    w.sx = (-w.o.x) * w.ix; w.sy = (-w.o.y) * w.iy; w.sz = (-w.o.z) * w.iz;
+    return w;
+}
+
+// Shading / store of a lit or occluded pixel (render.hpp:139-150).
+__device__ __forceinline__ void finish_pixel(const KParams& P, uint32_t f, uint32_t lr, uint32_t i, uint32_t pix,
+                                             bool blocked, F3 sun_line, uint32_t slot, float hu, float hv,
+                                             uint32_t& occluded) {
+    if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
+    if (blocked) {
+        ++occluded;
+        store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);
+    } else {
+        const F3 view = primary_dir(P, f, i, global_row(P, lr));
+        float c[3];
+        shade(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
+        store_pixel(P, f, lr, i, c[0], c[1], c[2]);
+    }
+}
+
 template <bool kStats>
 __global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t pre[kShards + 1];
-    __shared__ uint32_t s_blocked[kBlock];
-    __shared__ uint32_t s_mail[kBlock];                          // stolen node, by thief rank
-    __shared__ uint32_t s_from[kBlock];                          // donor lane, by thief rank
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wbase = wave * 64;
+    __shared__ StealLds L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* stk = lds + tid;
-    const uint32_t cap = P.shadow_stack_entries;
     if (wave == 0) {
         uint32_t x = lane < kShards ? P.shards[lane].queued : 0u;
 #pragma unroll
@@ -542,10 +714,8 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
     __syncthreads();
     const uint32_t total = pre[kShards];
     const uint32_t frame_pixels = P.local_rows * P.W;
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
     uint32_t occluded = 0, n_pairs = 0, n_tests = 0;
     bool overflow = false;
-    const float tmin = 0.0f, tmax = FLT_MAX;
     for (uint32_t g0 = blockIdx.x * kBlock; g0 < total; g0 += gridDim.x * kBlock) {
         const uint32_t g = g0 + tid;
         const bool has_job = g < total;
@@ -561,142 +731,85 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
             const float4 J0 = q[0], J1 = q[1];
             pix = __float_as_uint(J0.x); slot = __float_as_uint(J0.y); hu = J0.z; hv = J0.w;
             f = P.frames > 1 ? pix / frame_pixels : 0;
-            w.o = F3{J1.x, J1.y, J1.z};
-            w.d = normalize(f3(P.cam[f].sun) - w.o);                 // render.hpp:135
-            auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
-            w.ix = safe_inv(w.d.x); w.iy = safe_inv(w.d.y); w.iz = safe_inv(w.d.z);
-            w.sx = (-w.o.x) * w.ix; w.sy = (-w.o.y) * w.iy; w.sz = (-w.o.z) * w.iz;
+            w = make_shadow_ray(F3{J1.x, J1.y, J1.z}, f3(P.cam[f].sun));
         }
-        const F3 sun_line = w.d;
-        s_blocked[tid] = 0;
-        bool active = has_job;
-        uint32_t owner = tid, cur = 0, top = 0, bot = 0, cnt = 0;
-        if (P.root_leaf_count) {                                       // single-leaf scene
-            if (has_job) {
-                Hit h;
-                s_blocked[tid] = trace<true, kStats>(P, w.o, w.d, stk, h, n_pairs, n_tests, overflow) ? 1u : 0u;
-            }
-            active = false;
-        }
-        __builtin_amdgcn_wave_barrier();
-        while (__ballot(active)) {
-            if (active && s_blocked[owner]) active = false;             // another piece found an occluder
-            if (active) {
-                if (kStats) ++n_pairs;
-                const N4 n = load_n4(P.nodes4 + cur);
-                float e[4];
-                uint32_t leaf_mask = 0, inner_mask = 0;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float a0 = __builtin_fmaf(pick(n.lx, c), w.ix, w.sx), a1 = __builtin_fmaf(pick(n.hx, c), w.ix, w.sx);
-                    const float b0 = __builtin_fmaf(pick(n.ly, c), w.iy, w.sy), b1 = __builtin_fmaf(pick(n.hy, c), w.iy, w.sy);
-                    const float c0 = __builtin_fmaf(pick(n.lz, c), w.iz, w.sz), c1 = __builtin_fmaf(pick(n.hz, c), w.iz, w.sz);
-                    e[c] = fmaxf(fminf(a0, a1), fmaxf(fminf(b0, b1), fmaxf(fminf(c0, c1), tmin)));
-                    const float x = fminf(fmaxf(a0, a1), fminf(fmaxf(b0, b1), fminf(fmaxf(c0, c1), tmax)));
-                    const uint32_t cn = pick(n.cnt, c);
-                    const bool hit = e[c] <= x && cn != kNode4Empty;
-                    leaf_mask |= (hit && cn != 0) ? (1u << c) : 0u;
-                    inner_mask |= (hit && cn == 0) ? (1u << c) : 0u;
-                }
-                bool found = false;
-                uint32_t k = 0, k_end = 0;
-                while (true) {
-                    if (k >= k_end) {
-                        if (!leaf_mask) break;
-                        const uint32_t c = __builtin_ctz(leaf_mask);
-                        leaf_mask &= leaf_mask - 1;
-                        k = pick(n.fst, c);
-                        k_end = k + pick(n.cnt, c);
-                        if (kStats) n_tests += k_end - k;
-                    }
-                    float t, u, v;
-                    if (tri_test(load_tri(P.tris + k), w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
-                    ++k;
-                }
-                if (found) {
-                    s_blocked[owner] = 1u;
-                    active = false;
-                } else if (inner_mask) {
-                    uint32_t best = __builtin_ctz(inner_mask);
-                    float be = best == 0 ? e[0] : best == 1 ? e[1] : best == 2 ? e[2] : e[3];
-#pragma unroll
-                    for (int c = 1; c < 4; ++c)
-                        if ((inner_mask >> c & 1u) && e[c] < be) { be = e[c]; best = c; }
-                    uint32_t rest = inner_mask & ~(1u << best);
-                    if (cnt + __builtin_popcount(rest) > cap) { overflow = true; rest = 0; }
-                    while (rest) {
-                        const uint32_t c = __builtin_ctz(rest);
-                        rest &= rest - 1;
-                        stk[top * kBlock] = pick(n.fst, c);
-                        top = top + 1 == cap ? 0 : top + 1;
-                        ++cnt;
-                    }
-                    cur = pick(n.fst, best);
-                } else if (cnt) {
-                    top = (top == 0 ? cap : top) - 1;
-                    cur = stk[top * kBlock];
-                    --cnt;
-                } else {
-                    active = false;                                   // this piece is done, no hit
-                }
-            }
-            // idle lanes take the bottom stack entry of lanes with pending subtrees
-            const unsigned long long idle = __ballot(!active);
-            const unsigned long long donors = __ballot(active && cnt > 0);
-            if (idle && donors) {
-                const uint32_t n_idle = __popcll(idle), n_don = __popcll(donors);
-                if (active && cnt > 0) {
-                    const uint32_t r = __popcll(donors & lt_mask);
-                    if (r < n_idle) {
-                        s_mail[wbase + r] = stk[bot * kBlock];
-                        s_from[wbase + r] = lane;
-                        bot = bot + 1 == cap ? 0 : bot + 1;
-                        --cnt;
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                uint32_t mail = 0, donor = 0;
-                const uint32_t r = __popcll(idle & lt_mask);
-                const bool thief = !active && r < n_don;
-                if (thief) { mail = s_mail[wbase + r]; donor = s_from[wbase + r]; }
-                // every lane runs the shuffles; only thieves keep the values
-                const float ox = __shfl(w.o.x, donor, 64), oy = __shfl(w.o.y, donor, 64), oz = __shfl(w.o.z, donor, 64);
-                const float dx = __shfl(w.d.x, donor, 64), dy = __shfl(w.d.y, donor, 64), dz = __shfl(w.d.z, donor, 64);
-                const float jx = __shfl(w.ix, donor, 64), jy = __shfl(w.iy, donor, 64), jz = __shfl(w.iz, donor, 64);
-                const float tx = __shfl(w.sx, donor, 64), ty = __shfl(w.sy, donor, 64), tz = __shfl(w.sz, donor, 64);
-                const uint32_t down = __shfl(owner, donor, 64);
-                if (thief) {
-                    w.o = F3{ox, oy, oz}; w.d = F3{dx, dy, dz};
-                    w.ix = jx; w.iy = jy; w.iz = jz; w.sx = tx; w.sy = ty; w.sz = tz;
-                    owner = down;
-                    cur = mail;
-                    top = bot = cnt = 0;
-                    active = true;
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
+        steal_traverse<kStats>(P, has_job, w, stk, L, tid, lane, n_pairs, n_tests, overflow);
         if (has_job) {                                                   // shade every pixel together
-            const bool blocked = s_blocked[tid] != 0;
             const uint32_t rem = pix - f * frame_pixels;
             const uint32_t lr = rem / P.W, i = rem - lr * P.W;
-            if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
-            if (blocked) {                                               // render.hpp:147-150
-                ++occluded;
-                store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);
-            } else {                                                     // render.hpp:139-146
-                const F3 view = primary_dir(P, f, i, global_row(P, lr));
-                float c[3];
-                shade(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
-                store_pixel(P, f, lr, i, c[0], c[1], c[2]);
-            }
+            finish_pixel(P, f, lr, i, pix, L.blocked[tid] != 0, w.d, slot, hu, hv, occluded);
         }
-        __syncthreads();                                                 // s_blocked reuse next round
+        __syncthreads();                                                 // L reuse next round
     }
     const uint32_t wo = wave_sum(occluded);
     const uint32_t shard = (blockIdx.x * (kBlock / 64) + wave) % kShards;
     if (lane == 0 && wo) atomicAdd(&P.shards[shard].hits, (unsigned long long)wo);
+    if (kStats) {
+        const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
+        if (lane == 0) {
+            atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
+            atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
+        }
+    }
+    if (overflow) atomicOr(&P.shards[shard].error, 1u);
+}
+
+// ---------------------------------------------------------------- fused frame kernel
+// Primary + shadow + shading of an 8x8 pixel tile per wavefront in ONE kernel: each wavefront
+// traces its tile's primary rays (BVH2, exact reference order), then the shadow rays of its
+// own hits with intra-wavefront work stealing (lanes whose pixel missed help the others), then
+// shades.  No shadow-ray queue in HBM, no second launch: the shadow work of early tiles
+// overlaps the primary work of later ones.  Same results as ceres_primary + ceres_shadow.
+template <bool kStats>
+__global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ StealLds L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t* stk = lds + tid;
+    const uint32_t f = blockIdx.y / P.row_blocks_per_frame;
+    const uint32_t by = blockIdx.y - f * P.row_blocks_per_frame;
+    const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const uint32_t lr = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool active = i < P.W && lr < P.local_rows;
+    const uint32_t px = (f * P.local_rows + lr) * P.W + i;
+    bool hit = false;
+    Hit h{0, 0.f, 0.f, 0.f};
+    uint32_t n_pairs = 0, n_tests = 0;
+    bool overflow = false;
+    RayWork w{};
+    if (active) {
+        const F3 view = primary_dir(P, f, i, global_row(P, lr));
+        hit = trace<false, kStats>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
+        if (P.rec_prim) {
+            P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
+            P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
+            P.rec_tuv[3 * size_t(px) + 1] = hit ? h.u : 0.f;
+            P.rec_tuv[3 * size_t(px) + 2] = hit ? h.v : 0.f;
+            P.rec_shadow[px] = -1;
+        }
+        if (!hit) {
+            store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);                 // render.hpp:116-117
+        } else {                                                     // render.hpp:127-135
+            const TriV tr = load_tri(P.tris + h.slot);
+            const F3 normal = normalize(tr.n);
+            const F3 p1 = tr.p0 - tr.e1, p2 = tr.p0 + tr.e2;
+            F3 p = tr.p0 * h.u + p1 * h.v + p2 * (1 - h.u - h.v);
+            const float scale = -0.00001;
+            p = p + normal * scale;
+            w = make_shadow_ray(p, f3(P.cam[f].sun));
+        }
+    }
+    const uint32_t n_shadow = __popcll(__ballot(hit));
+    steal_traverse<kStats>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow);
+    uint32_t occluded = 0;
+    if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
+    const uint32_t wo = wave_sum(occluded);
+    const uint32_t wave_id = (blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave;
+    const uint32_t shard = wave_id % kShards;
+    if (lane == 0 && n_shadow) {
+        atomicAdd(&P.shards[shard].queued, n_shadow);                  // shadow rays traced
+        atomicAdd(&P.shards[shard].hits, (unsigned long long)(n_shadow + wo));
+    }
     if (kStats) {
         const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
         if (lane == 0) {
@@ -888,6 +1001,15 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         if (e0) HIP_TRY(hipEventRecord(e0, stream));
         const size_t lds = size_t(s->stack_entries) * dev::kBlock * 4;
         const dim3 grid(bx, by * frames), block(dev::kBlock);
+        if (CERES_FUSED && mode == CERES_MODE_FULL) {
+            // one kernel: primary + work-stealing shadow + shading per 8x8 tile
+            const size_t flds = size_t(std::max(s->stack_entries, s->shadow_stack_entries)) * dev::kBlock * 4;
+            if (stats) hipLaunchKernelGGL((dev::ceres_fused<true>), grid, block, flds, stream, P);
+            else hipLaunchKernelGGL((dev::ceres_fused<false>), grid, block, flds, stream, P);
+            HIP_TRY(hipGetLastError());
+            if (e1) HIP_TRY(hipEventRecord(e1, stream));
+            if (e2) HIP_TRY(hipEventRecord(e2, stream));
+        } else {
         if (mode == CERES_MODE_PRIMARY) {
             if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, true>), grid, block, lds, stream, P);
             else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, false>), grid, block, lds, stream, P);
@@ -919,6 +1041,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             HIP_TRY(hipGetLastError());
         }
         if (e2) HIP_TRY(hipEventRecord(e2, stream));
+        }
     }
     if (d_counters) {
         hipLaunchKernelGGL(dev::ceres_finalize, dim3(1), dim3(64), 0, stream, s->d_shards,
@@ -940,7 +1063,10 @@ extern "C" {
 
 const char* ceres_last_error(void) { return error_buffer(); }
 const char* ceres_version(void) { return "ceres-mi355x 0.2 (gfx950)"; }
-const char* ceres_kernel_names(void) { return "ceres_primary,ceres_shadow,ceres_finalize,ceres_assemble"; }
+const char* ceres_kernel_names(void) {
+    return CERES_FUSED ? "ceres_fused,ceres_primary,ceres_finalize,ceres_assemble"
+                       : "ceres_primary,ceres_shadow,ceres_finalize,ceres_assemble";
+}
 
 size_t ceres_tiling_local_rows(size_t height, const ceres_tiling* t) {
     if (!t) return height;

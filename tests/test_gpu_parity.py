@@ -274,6 +274,15 @@ def test_cli_orbit_frames(gpu, tmp_path):
     assert "Total Rays:" in r.stdout
 
 
+def test_fast_reciprocal_is_exact(gpu):
+    """rcp_exact() (render_hip.hip) == IEEE 1/x for all normal |x| in [2^-126, 2^126): exhaustive
+    over every float bit pattern on this gfx950 (the kernels fall back to the division elsewhere)."""
+    exe = os.path.join(REPO, "tools", "probes", "rcp_exhaustive")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "exact for biased exponents [1, 252]" in r.stdout, r.stdout
+
+
 def test_repeat_renders_are_deterministic(gpu):
     pkg = gpu
     meta, _, _ = load_golden("dragon_1080")
