@@ -766,9 +766,14 @@ __global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
     __shared__ StealLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* stk = lds + tid;
-    const uint32_t f = blockIdx.y / P.row_blocks_per_frame;
-    const uint32_t by = blockIdx.y - f * P.row_blocks_per_frame;
-    const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    // 1-D grid over the batch's 16x16 tiles in tile_order (centre of the image first, so the
+    // expensive tiles start early and cheap background tiles fill the end of the launch)
+    const uint32_t t = __builtin_amdgcn_readfirstlane(P.tile_order[blockIdx.x]);
+    const uint32_t per_frame = P.tiles_x * P.row_blocks_per_frame;
+    const uint32_t f = t / per_frame;
+    const uint32_t rem = t - f * per_frame;
+    const uint32_t by = rem / P.tiles_x, bx = rem - by * P.tiles_x;
+    const uint32_t i = bx * 16 + (wave & 1) * 8 + (lane & 7);
     const uint32_t lr = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     const bool active = i < P.W && lr < P.local_rows;
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;
@@ -804,7 +809,7 @@ __global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
     uint32_t occluded = 0;
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
     const uint32_t wo = wave_sum(occluded);
-    const uint32_t wave_id = (blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave;
+    const uint32_t wave_id = blockIdx.x * (kBlock / 64) + wave;
     const uint32_t shard = wave_id % kShards;
     if (lane == 0 && n_shadow) {
         atomicAdd(&P.shards[shard].queued, n_shadow);                  // shadow rays traced
@@ -880,6 +885,9 @@ struct ceres_scene {
     size_t n_nodes4 = 0;
     SiblingPair* d_pairs = nullptr;
     Node4* d_nodes4 = nullptr;
+    uint32_t* d_order = nullptr;          // fused kernel tile order, for order_key
+    size_t order_cap = 0;
+    uint64_t order_key = ~0ull;
     Tri48* d_tris = nullptr;
     uint32_t* d_orig = nullptr;
     float* d_norms = nullptr;
@@ -914,7 +922,7 @@ void dfree(T*& p) { if (p) { (void)hipFree(p); p = nullptr; } }
 void scene_release(ceres_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
-    dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
+    dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_order); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
     for (auto e : s->ev_used) (void)hipEventDestroy(e);
@@ -942,6 +950,41 @@ int ensure_workspace(ceres_scene* s, size_t jobs, size_t px, bool want_px, bool 
         HIP_TRY(hipMalloc(&s->d_rgb8, px * 3));
         s->px_cap = px;
     }
+    return CERES_OK;
+}
+
+// Centre-first order of a batch's 16x16 tiles for the fused kernel: ascending distance of the
+// tile centre (global pixel coordinates) from the image centre, frames interleaved.  Cached
+// on the scene per (W, H, tiling, frames).
+int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, size_t rows, uint32_t frames,
+                      uint32_t bx, uint32_t by, hipStream_t stream) {
+    const uint64_t key = (uint64_t(W) << 44) ^ (uint64_t(H) << 24) ^ (uint64_t(t.row_block) << 12) ^
+                         (uint64_t(t.rank) << 36) ^ (uint64_t(t.world) << 52) ^ (uint64_t(frames) << 5) ^ rows;
+    const size_t n = size_t(bx) * by * frames;
+    if (key == s->order_key && s->d_order && n <= s->order_cap) return CERES_OK;
+    std::vector<std::pair<double, uint32_t>> k(n);
+    const double cx = 0.5 * double(W), cy = 0.5 * double(H);
+    for (uint32_t f = 0; f < frames; ++f)
+        for (uint32_t y = 0; y < by; ++y) {
+            const size_t lr = std::min<size_t>(size_t(y) * 16 + 8, rows - 1);
+            const size_t j = ((lr / t.row_block) * t.world + t.rank) * t.row_block + lr % t.row_block;
+            for (uint32_t x = 0; x < bx; ++x) {
+                const double dx = double(x) * 16 + 8 - cx, dy = double(j) - cy;
+                const uint32_t id = (f * by + y) * bx + x;
+                k[id] = {dx * dx + dy * dy, id};
+            }
+        }
+    std::stable_sort(k.begin(), k.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    std::vector<uint32_t> order(n);
+    for (size_t q = 0; q < n; ++q) order[q] = k[q].second;
+    if (n > s->order_cap) {
+        dfree(s->d_order);
+        HIP_TRY(hipMalloc(&s->d_order, n * sizeof(uint32_t)));
+        s->order_cap = n;
+    }
+    HIP_TRY(hipMemcpyAsync(s->d_order, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    s->order_key = key;
     return CERES_OK;
 }
 
@@ -996,6 +1039,8 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         e2 = s->ev_pool.back(); s->ev_pool.pop_back();
         s->ev_used.push_back(e0); s->ev_used.push_back(e1); s->ev_used.push_back(e2);
     }
+    if (CERES_FUSED && mode == CERES_MODE_FULL && rows)
+        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, bx, by, stream)) return rc;
     HIP_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, stream));
     if (rows) {                                                      // a rank may own no rows
         if (e0) HIP_TRY(hipEventRecord(e0, stream));
@@ -1004,8 +1049,11 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         if (CERES_FUSED && mode == CERES_MODE_FULL) {
             // one kernel: primary + work-stealing shadow + shading per 8x8 tile
             const size_t flds = size_t(std::max(s->stack_entries, s->shadow_stack_entries)) * dev::kBlock * 4;
-            if (stats) hipLaunchKernelGGL((dev::ceres_fused<true>), grid, block, flds, stream, P);
-            else hipLaunchKernelGGL((dev::ceres_fused<false>), grid, block, flds, stream, P);
+            P.tile_order = s->d_order;
+            P.tiles_x = bx;
+            const dim3 fgrid(bx * by * frames);
+            if (stats) hipLaunchKernelGGL((dev::ceres_fused<true>), fgrid, block, flds, stream, P);
+            else hipLaunchKernelGGL((dev::ceres_fused<false>), fgrid, block, flds, stream, P);
             HIP_TRY(hipGetLastError());
             if (e1) HIP_TRY(hipEventRecord(e1, stream));
             if (e2) HIP_TRY(hipEventRecord(e2, stream));
