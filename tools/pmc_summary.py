@@ -15,7 +15,7 @@ import os
 import sys
 from collections import defaultdict
 
-SHORT = {"ceres_primary": "ceres_primary", "ceres_shadow": "ceres_shadow", "ceres_finalize": "ceres_finalize"}
+SHORT = {k: k for k in ("ceres_fused", "ceres_primary", "ceres_shadow", "ceres_finalize", "ceres_assemble")}
 
 
 def short(name):
@@ -62,8 +62,11 @@ def main():
             e["l2_hit_rate"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
         if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_ACTIVE_INST_VALU", 0) > 0:
             e["valu_lane_utilisation"] = round(c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64), 4)
-        if "SQ_WAIT_INST_ANY" in c and c.get("SQ_WAVE_CYCLES", 0) > 0:
-            e["wait_inst_any_frac"] = round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+        if c.get("SQ_WAVE_CYCLES", 0) > 0:
+            for n, key in (("SQ_WAIT_INST_ANY", "issue_stall_frac"), ("SQ_WAIT_ANY", "waitcnt_parked_frac"),
+                           ("SQ_ACTIVE_INST_ANY", "active_inst_frac")):
+                if n in c:
+                    e[key] = round(c[n] / c["SQ_WAVE_CYCLES"], 4)
         entry[k] = e
     summ[cfg] = entry
     with open(dst, "w") as f:

@@ -11,6 +11,7 @@ step 120 list rocprofv3 -L
 step 400 trace rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $BENCH
 step 400 pmc_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
 step 400 pmc_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
-step 400 pmc_sq rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU --output-format csv -d $OUT/pmc_sq -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
+step 400 pmc_sq rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU --output-format csv -d $OUT/pmc_sq -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
+step 400 pmc_sq2 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_INSTS_VMEM_WR --output-format csv -d $OUT/pmc_sq2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
 step 400 pmc_l2 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_l2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline
-find $OUT -name "*.csv" | head -50
+python3 tools/pmc_summary.py dragon_1080 $OUT $OUT/pmc_summary.json > /dev/null && echo summary ok
