@@ -7,6 +7,7 @@ iracigt/ceres-raytracer) for Python callers, tests and bench.py:
     load_obj(path) -> Mesh                    obj_norms.hpp:120-127 (triangles + tri_norms)
     rotate_triangles(mesh, axis, degrees)     render.hpp:24-44
     build_bvh(mesh) -> Bvh                    binned_sah_builder.hpp:39-234 (static.cpp:100-107)
+    build_bvh_gpu(mesh) -> Bvh                the same BVH, built by gfx950 kernels
     Scene(mesh, bvh, device)                  the (bvh, triangles, tri_norms) arguments, on the GPU
     render(camera, sun, scene, W, H) -> (pixels, rays, hits)   render.hpp:86-156
 
@@ -32,7 +33,8 @@ MODE_FULL, MODE_PRIMARY = 0, 1
 SCENE_STATS = 1
 
 EXPORTED_SYMBOLS = (
-    "ceres_obj_load", "ceres_proc_mesh", "ceres_rotate_triangles", "ceres_bvh_build", "ceres_camera_basis",
+    "ceres_obj_load", "ceres_proc_mesh", "ceres_rotate_triangles", "ceres_bvh_build", "ceres_bvh_build_gpu",
+    "ceres_bvh_build_device", "ceres_camera_basis",
     "ceres_free", "ceres_scene_create", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
@@ -93,6 +95,9 @@ def lib():
     L.ceres_proc_mesh.argtypes = [ctypes.c_int, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz)]
     L.ceres_rotate_triangles.argtypes = [_fp, _sz, ctypes.c_int, ctypes.c_float]
     L.ceres_bvh_build.argtypes = [_fp, _sz, ctypes.POINTER(_u32p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p)]
+    L.ceres_bvh_build_gpu.argtypes = [_fp, _sz, ctypes.POINTER(_u32p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p),
+                                      ctypes.c_int]
+    L.ceres_bvh_build_device.argtypes = [_vp, _sz, _vp, _vp, ctypes.POINTER(_sz), _vp]
     L.ceres_camera_basis.argtypes = [_fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp]
     L.ceres_orbit_cameras.argtypes = [_fp, _fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp, ctypes.c_float,
                                       ctypes.c_uint32, ctypes.c_int, _fp, _fp, _fp]
@@ -200,6 +205,21 @@ def build_bvh(mesh):
     _check(lib().ceres_bvh_build(_p(mesh.tri, ctypes.c_float), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
                                  ctypes.byref(prim)))
     return Bvh(_take(nodes, m.value * 8, np.uint32).reshape(-1, 8), _take(prim, len(mesh), np.uint64))
+
+
+def build_bvh_gpu(mesh, device=0):
+    """The same binned-SAH BVH as build_bvh, built on the GPU (ceres_bvh_build_gpu)."""
+    nodes, prim, m = _u32p(), _u64p(), _sz()
+    _check(lib().ceres_bvh_build_gpu(_p(mesh.tri, ctypes.c_float), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
+                                     ctypes.byref(prim), int(device)))
+    return Bvh(_take(nodes, m.value * 8, np.uint32).reshape(-1, 8), _take(prim, len(mesh), np.uint64))
+
+
+def build_bvh_device(d_tri48, n_tri, d_nodes32, d_prim32, stream=0):
+    """ceres_bvh_build_device on device pointers (ints); returns the node count."""
+    m = _sz()
+    _check(lib().ceres_bvh_build_device(d_tri48, n_tri, d_nodes32, d_prim32, ctypes.byref(m), stream or None))
+    return m.value
 
 
 class Scene:

@@ -826,11 +826,14 @@ __global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
 }
 
 // ---------------------------------------------------------------- counters
-__global__ void ceres_finalize(const Shard* shards, uint64_t primary_rays, uint64_t* out) {
+// Sums the counter shards and zeroes them for the next render (so a render that follows a
+// counted one needs no memset).
+__global__ void ceres_finalize(Shard* shards, uint64_t primary_rays, uint64_t* out) {
     if (threadIdx.x != 0) return;
     unsigned long long q = 0, h = 0, p = 0, t = 0;
     uint32_t err = 0;
     for (int s = 0; s < kShards; ++s) { q += shards[s].queued; h += shards[s].hits; p += shards[s].pairs; t += shards[s].tests; err |= shards[s].error; }
+    for (int s = 0; s < kShards; ++s) { shards[s].queued = 0; shards[s].hits = 0; shards[s].pairs = 0; shards[s].tests = 0; shards[s].error = 0; }
     out[0] = primary_rays + q; out[1] = h; out[2] = primary_rays; out[3] = q;
     out[4] = p; out[5] = t; out[6] = err; out[7] = 0;
 }
@@ -892,6 +895,7 @@ struct ceres_scene {
     uint32_t* d_orig = nullptr;
     float* d_norms = nullptr;
     Shard* d_shards = nullptr;
+    bool shards_dirty = true;          // shards not known to be zero (see ceres_render_batch)
     uint64_t* d_counters = nullptr;
     ShadowJob* d_jobs = nullptr;
     size_t jobs_cap = 0;
@@ -906,6 +910,7 @@ struct ceres_scene {
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<hipEvent_t> ev_used;   // triples: start, after primary, after shadow
+    std::vector<char> ev_fused;        // per triple: one ceres_fused launch (no separate shadow kernel)
 };
 
 namespace {
@@ -926,7 +931,7 @@ void scene_release(ceres_scene* s) {
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
     for (auto e : s->ev_used) (void)hipEventDestroy(e);
-    s->ev_pool.clear(); s->ev_used.clear();
+    s->ev_pool.clear(); s->ev_used.clear(); s->ev_fused.clear();
     if (s->stream) (void)hipStreamDestroy(s->stream);
     s->stream = nullptr;
 }
@@ -1038,10 +1043,16 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         e1 = s->ev_pool.back(); s->ev_pool.pop_back();
         e2 = s->ev_pool.back(); s->ev_pool.pop_back();
         s->ev_used.push_back(e0); s->ev_used.push_back(e1); s->ev_used.push_back(e2);
+        s->ev_fused.push_back(char(CERES_FUSED && mode == CERES_MODE_FULL));
     }
     if (CERES_FUSED && mode == CERES_MODE_FULL && rows)
         if (int rc = ensure_tile_order(s, W, H, t, rows, frames, bx, by, stream)) return rc;
-    HIP_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, stream));
+    // The shards must start at zero when they are read back (counters) or hold the two-pass
+    // shadow queue; the fused kernel without counters only adds to them, so its steady-state
+    // frames skip the memset (ceres_finalize re-zeroes them after every counted render).
+    const bool need_clean = d_counters || !(CERES_FUSED && mode == CERES_MODE_FULL);
+    if (need_clean && s->shards_dirty) HIP_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, stream));
+    s->shards_dirty = true;
     if (rows) {                                                      // a rank may own no rows
         if (e0) HIP_TRY(hipEventRecord(e0, stream));
         const size_t lds = size_t(s->stack_entries) * dev::kBlock * 4;
@@ -1095,6 +1106,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         hipLaunchKernelGGL(dev::ceres_finalize, dim3(1), dim3(64), 0, stream, s->d_shards,
                            uint64_t(frames) * W * rows, d_counters);
         HIP_TRY(hipGetLastError());
+        s->shards_dirty = false;
     }
     return CERES_OK;
 }
@@ -1298,7 +1310,8 @@ int ceres_scene_wave_log(ceres_scene* s, uint64_t* out, size_t max_waves, size_t
 }
 
 // Per-kernel device timing for the roofline leg of bench.py: while enabled, every render
-// records HIP events around ceres_primary and ceres_shadow on the launch stream.
+// records HIP events around ceres_primary and ceres_shadow (or the one ceres_fused launch, reported
+// as primary_ms with shadow_ms = 0) on the launch stream.
 int ceres_scene_set_timing(ceres_scene* s, int enable) {
     if (!s) return set_error(CERES_EINVAL, "null scene");
     s->timing = enable != 0;
@@ -1317,10 +1330,12 @@ int ceres_scene_read_timing(ceres_scene* s, double* primary_ms, double* shadow_m
         float a = 0.f, b = 0.f;
         HIP_TRY(hipEventElapsedTime(&a, e0, e1));
         HIP_TRY(hipEventElapsedTime(&b, e1, e2));
-        p += a; q += b;
+        p += a;
+        if (!s->ev_fused[k]) q += b;   // fused: e1..e2 brackets no kernel
     }
     for (auto e : s->ev_used) s->ev_pool.push_back(e);
     s->ev_used.clear();
+    s->ev_fused.clear();
     if (primary_ms) *primary_ms = p;
     if (shadow_ms) *shadow_ms = q;
     if (renders) *renders = n;

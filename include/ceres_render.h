@@ -82,6 +82,16 @@ int ceres_rotate_triangles(float* tri48, size_t n_tri, int axis, float degrees);
 /* compute_bounding_boxes_and_centers + BinnedSahBuilder<Bvh,16>::build (utilities.hpp:142-171,
  * binned_sah_builder.hpp:39-234).  *nodes32 (n_nodes x 32 B) / *prim64 malloc'd. */
 int ceres_bvh_build(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64);
+/* The same BinnedSahBuilder<Bvh,16> build on the GPU: identical topology,
+ * boxes and primitive_indices as ceres_bvh_build (node numbering is breadth-first for the top,
+ * then subtree-contiguous, as the reference's own numbering is OpenMP-timing dependent).
+ * ceres_bvh_build_gpu: host buffers in/out, same outputs as ceres_bvh_build, on HIP `device`.
+ * ceres_bvh_build_device: d_tri48 in device memory; d_nodes32 holds 2*n_tri-1 nodes (8 u32 each),
+ * d_prim32 n_tri u32; stream-ordered on `stream` (a hipStream_t), returns once *n_nodes is known. */
+int ceres_bvh_build_gpu(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64,
+                        int device);
+int ceres_bvh_build_device(const float* d_tri48, size_t n_tri, uint32_t* d_nodes32, uint32_t* d_prim32,
+                           size_t* n_nodes, void* stream);
 /* Camera basis of render.hpp:91-97: out = {dir[3], image_u*w[3], image_v*w*ratio[3]}. */
 int ceres_camera_basis(const float eye[3], const float dir[3], const float up[3], float fov_deg,
                        size_t width, size_t height, float out9[9]);

@@ -337,6 +337,39 @@ extern "C" {
 const char* oracle_last_error(void) { return g_err.c_str(); }
 void oracle_free(void* p) { std::free(p); }
 
+// Numbering-independent serialisation of a bvh::Bvh<float> (bvh.hpp:25-79): pre-order DFS from
+// the root, per node its 6 bounds + primitive_count (7 x 4 B), leaves followed by their
+// primitive_indices (u64).  Same byte stream as tests/golden/make_golden.py canonical_bvh_sha,
+// in C so 10M-node trees take milliseconds.  *out is malloc'd.
+int oracle_bvh_canonical(const uint32_t* nodes32, size_t n_nodes, const uint64_t* prim, size_t n_prim,
+                         uint8_t** out, size_t* out_len) {
+    std::vector<uint8_t> buf;
+    buf.reserve(n_nodes * 28 + n_prim * 8);
+    std::vector<uint32_t> st{0};
+    size_t visited = 0;
+    while (!st.empty()) {
+        const uint32_t k = st.back(); st.pop_back();
+        if (k >= n_nodes || ++visited > n_nodes) { g_err = "bad BVH"; return -1; }
+        const uint32_t* n = nodes32 + 8 * size_t(k);
+        const uint8_t* b = reinterpret_cast<const uint8_t*>(n);
+        buf.insert(buf.end(), b, b + 28);
+        const uint32_t cnt = n[6], first = n[7];
+        if (cnt) {
+            if (size_t(first) + cnt > n_prim) { g_err = "bad leaf"; return -1; }
+            const uint8_t* q = reinterpret_cast<const uint8_t*>(prim + first);
+            buf.insert(buf.end(), q, q + 8 * size_t(cnt));
+        } else {
+            st.push_back(first + 1);
+            st.push_back(first);
+        }
+    }
+    *out = static_cast<uint8_t*>(std::malloc(std::max<size_t>(1, buf.size())));
+    if (!*out) { g_err = "out of memory"; return -3; }
+    std::memcpy(*out, buf.data(), buf.size());
+    *out_len = buf.size();
+    return 0;
+}
+
 int oracle_load_obj(const char* path, float** tri48, float** norm36, size_t* n_tri) {   // obj_norms.hpp:120-127
     std::ifstream is(path);
     Mesh m;

@@ -47,10 +47,28 @@ def lib():
         L.oracle_render.argtypes = [_fp, _fp, _sz, _u32p, _sz, _u64p, _fp, _fp, _fp, ctypes.c_int, _sz, _sz,
                                     _fp, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int32), _fp,
                                     ctypes.POINTER(ctypes.c_int8), _u64p, ctypes.c_int, _u32p]
+        L.oracle_bvh_canonical.argtypes = [_u32p, _sz, _u64p, _sz, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                           ctypes.POINTER(_sz)]
         L.oracle_free.argtypes = [ctypes.c_void_p]
         L.oracle_free.restype = None
         _lib = L
     return _lib
+
+
+def canonical_bvh_sha(nodes, prim):
+    """sha256 of the numbering-independent DFS serialisation of a BVH (nodes: m x 8 u32, prim: u64);
+    equal to tests/golden/make_golden.canonical_bvh_sha, computed in C."""
+    import hashlib
+    nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
+    prim = np.ascontiguousarray(prim, np.uint64)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = _sz()
+    _check(lib().oracle_bvh_canonical(_ptr(nodes, ctypes.c_uint32), nodes.shape[0], _ptr(prim, ctypes.c_uint64),
+                                      prim.size, ctypes.byref(out), ctypes.byref(n)))
+    try:
+        return hashlib.sha256(ctypes.string_at(out, n.value)).hexdigest()
+    finally:
+        lib().oracle_free(out)
 
 
 def _ptr(a, t):

@@ -162,7 +162,37 @@ def make(name):
     print(name, meta["exact"]["rays"], meta["exact"]["hits"], meta["ppm_bytes_differing_ref_vs_exact"], flush=True)
 
 
+def add_scene_hashes(name):
+    """Scene checksums for a config whose fixture was made without them (the 10M-triangle C5):
+    the reference's rotated triangles, normals and canonical BVH, dumped by the contraction-free
+    reference harness at a 1x1 frame (the dump does not depend on the frame size) and hashed
+    with the oracle's C serialiser (same byte stream as canonical_bvh_sha)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    cfg = configs.CONFIGS[name]
+    os.makedirs(SCRATCH, exist_ok=True)
+    p_dump = os.path.join(SCRATCH, name)
+    run(REF_EXACT, cfg, ["--size", "1", "1", "--out", os.devnull, "--dump", p_dump])
+    nodes = np.fromfile(p_dump + ".nodes32", dtype=np.uint32)
+    prim = np.fromfile(p_dump + ".prim64", dtype=np.uint64)
+    path = os.path.join(HERE, name + ".json")
+    meta = json.load(open(path))
+    meta["tri48_sha256"] = sha(p_dump + ".tri48")
+    meta["norm36_sha256"] = sha(p_dump + ".norm36")
+    meta["bvh_canonical_sha256"] = oracle.canonical_bvh_sha(nodes, prim)
+    with open(path, "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+        f.write("\n")
+    for suf in (".tri48", ".norm36", ".nodes32", ".prim64"):
+        os.remove(p_dump + suf)
+    print(name, "scene hashes added", flush=True)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["--scene-hashes"]:
+        for n in sys.argv[2:]:
+            add_scene_hashes(n)
+        sys.exit(0)
     names = sys.argv[1:] or list(configs.CONFIGS)
     for n in names:
         make(n)

@@ -72,6 +72,24 @@ def test_product_matches_oracle_on_c5_mesh(pkg, oracle_mod):
         make_golden.canonical_bvh_sha(nodes.tobytes(), prim.tobytes())
 
 
+def test_product_c5_scene_matches_reference(pkg, oracle_mod):
+    """Full C5 (9,999,392 triangles): rotated triangles, normals and the binned-SAH BVH of the
+    product's host path equal the reference's dump (tests/golden/proc_c5.json scene hashes)."""
+    meta, _, _ = load_golden("proc_c5")
+    mesh, bvh, _ = pkg.prepare(configs.CONFIGS["proc_c5"])
+    assert len(mesh) == meta["n_tri"] and bvh.nodes.shape[0] == meta["n_nodes"]
+    assert hashlib.sha256(mesh.tri.tobytes()).hexdigest() == meta["tri48_sha256"]
+    assert hashlib.sha256(mesh.norm.tobytes()).hexdigest() == meta["norm36_sha256"]
+    assert oracle_mod.canonical_bvh_sha(bvh.nodes, bvh.prim) == meta["bvh_canonical_sha256"]
+
+
+def test_oracle_canonical_hash_equals_python_definition(pkg, oracle_mod):
+    import make_golden
+    mesh, bvh, _ = pkg.prepare(configs.CONFIGS["dragon_1080"])
+    assert oracle_mod.canonical_bvh_sha(bvh.nodes, bvh.prim) == \
+        make_golden.canonical_bvh_sha(bvh.nodes.tobytes(), bvh.prim.tobytes())
+
+
 def test_obj_edge_cases(pkg, tmp_path):
     # unreadable file -> empty scene, like obj_norms.hpp:123-126
     m = pkg.load_obj(str(tmp_path / "missing.obj"))
