@@ -40,8 +40,11 @@ namespace bvhdev {
 constexpr int kBins = 16;
 constexpr uint32_t kMaxDepth = 64;       // top_down_builder.hpp:36
 constexpr uint32_t kMaxLeaf = 16;        // top_down_builder.hpp:41
-constexpr uint32_t kSmall = 512;         // subtree-per-wavefront threshold (primitives)
-constexpr int kChunk = 1024;             // positions per binning workgroup (256 threads x 4)
+#ifndef CERES_BVH_SMALL
+#define CERES_BVH_SMALL 256
+#endif
+constexpr uint32_t kSmall = CERES_BVH_SMALL;  // subtree-per-wavefront threshold (primitives)
+constexpr int kChunk = 4096;             // positions per binning workgroup (256 threads x 16)
 constexpr int kStack = 72;               // small-subtree work stack (depth <= 64 -> <= 66 entries)
 
 // One primitive in position order: centre (the bin key), box, original index.  48 B, moved
@@ -187,16 +190,19 @@ __device__ void child_boxes(const BinF* bins, uint32_t axis, uint32_t split, uin
 }
 
 __device__ __forceinline__ float comp3(float x, float y, float z, uint32_t a) { return a == 0 ? x : (a == 1 ? y : z); }
+__device__ __forceinline__ uint32_t sel3(uint32_t x, uint32_t y, uint32_t z, uint32_t a) { return a == 0 ? x : (a == 1 ? y : z); }
 
 // ---- init: per-primitive box + centre (triangle.hpp:39-48), root box ---------------------
 // Box: p0 extended by p1() = p0 - e1 then p2() = p0 + e2; centre (p0 + p1 + p2) * (1/3).
+constexpr int kInitPer = 8;              // primitives per thread in k_init
 __global__ void __launch_bounds__(256) k_init(const Tri48* __restrict__ tris, uint32_t n, PrimRec* __restrict__ rec,
                                               int32_t* __restrict__ seg, int32_t seg0,
                                               unsigned long long* __restrict__ root_keys) {
     __shared__ unsigned long long red[6][256];
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     unsigned long long k[6] = {kKeyMinEmpty, kKeyMinEmpty, kKeyMinEmpty, kKeyMaxEmpty, kKeyMaxEmpty, kKeyMaxEmpty};
-    if (i < n) {
+    for (int r = 0; r < kInitPer; ++r) {
+        const uint32_t i = (blockIdx.x * kInitPer + uint32_t(r)) * 256u + threadIdx.x;
+        if (i >= n) break;
         const Tri48 t = tris[i];
         const float p0[3] = {t.p0[0], t.p0[1], t.p0[2]};
         float p1[3], p2[3], lo[3], hi[3], c[3];
@@ -207,13 +213,13 @@ __global__ void __launch_bounds__(256) k_init(const Tri48* __restrict__ tris, ui
             hi[a] = greater(greater(p0[a], p1[a]), p2[a]);
             c[a] = (p0[a] + p1[a] + p2[a]) * (1.0f / 3.0f);
         }
-        PrimRec r;
-        r.cx = c[0]; r.cy = c[1]; r.cz = c[2]; r.idx = i;
-        r.lx = lo[0]; r.ly = lo[1]; r.lz = lo[2]; r.pad0 = 0.f;
-        r.hx = hi[0]; r.hy = hi[1]; r.hz = hi[2]; r.pad1 = 0.f;
-        rec[i] = r;
+        PrimRec pr;
+        pr.cx = c[0]; pr.cy = c[1]; pr.cz = c[2]; pr.idx = i;
+        pr.lx = lo[0]; pr.ly = lo[1]; pr.lz = lo[2]; pr.pad0 = 0.f;
+        pr.hx = hi[0]; pr.hy = hi[1]; pr.hz = hi[2]; pr.pad1 = 0.f;
+        rec[i] = pr;
         seg[i] = seg0;
-        for (int a = 0; a < 3; ++a) { k[a] = key_min(lo[a], i); k[3 + a] = key_max(hi[a], i); }
+        for (int a = 0; a < 3; ++a) { k[a] = min(k[a], key_min(lo[a], i)); k[3 + a] = max(k[3 + a], key_max(hi[a], i)); }
     }
     for (int v = 0; v < 6; ++v) red[v][threadIdx.x] = k[v];
     __syncthreads();
@@ -271,43 +277,125 @@ __global__ void k_item_prep(Item* items, uint32_t n_items, const RefNode* nodes,
     }
 }
 
-// Fill the bins of every large item (binned_sah_builder.hpp:157-164).  Positions of the
-// workgroup's first item reduce in LDS first; others go straight to L2.
+// Fill the bins of every large item (binned_sah_builder.hpp:157-164).  A wavefront whose active
+// positions all belong to one item reduces each (axis, bin) group of lanes with butterfly
+// reductions of the keys (one LDS / L2 atomic per group instead of one per lane); the
+// workgroup's first item reduces in LDS, others go straight to L2.  Mixed wavefronts (item
+// boundaries) fall back to per-lane atomics.  Keys make every order give the same bins.
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+    const uint32_t lo = uint32_t(__shfl_xor(int(uint32_t(v)), m));
+    const uint32_t hi = uint32_t(__shfl_xor(int(uint32_t(v >> 32)), m));
+    return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+
+// Lane (axis, bin) of each wavefront walks the wavefront's positions in order and keeps its
+// bin's running box exactly like the reference's sequential loop (ties keep the earlier value),
+// remembering which position supplied each bound; the partial bin is flushed as keys when the
+// item changes (LDS for the workgroup's first item, else L2).  Reads are LDS broadcasts of
+// staged 64-record runs; no atomics conflict inside a wavefront.
 __global__ void __launch_bounds__(256) k_bin(const PrimRec* __restrict__ rec, const int32_t* __restrict__ seg, uint32_t n,
                                              const Item* __restrict__ items, BinKeys* __restrict__ bins) {
     __shared__ unsigned long long slo[3 * kBins][3], shi[3 * kBins][3];
     __shared__ uint32_t scount[3 * kBins];
+    __shared__ PrimRec stage[4][64];
+    __shared__ int32_t sseg[4][64];
     __shared__ int32_t s0_sh;
-    const uint32_t base = blockIdx.x * uint32_t(kChunk);
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t blk = blockIdx.x * uint32_t(kChunk);
+    const uint32_t base = blk + wave * uint32_t(kChunk / 4);
+    const uint32_t my_axis = lane >> 4, my_bin = lane & 15u;
+    const bool binlane = lane < 3u * kBins;
     if (threadIdx.x < 3u * kBins) {
         for (int k = 0; k < 3; ++k) { slo[threadIdx.x][k] = kKeyMinEmpty; shi[threadIdx.x][k] = kKeyMaxEmpty; }
         scount[threadIdx.x] = 0;
     }
-    if (threadIdx.x == 0) s0_sh = seg[base];
+    if (threadIdx.x == 0) s0_sh = blk < n ? seg[blk] : -1;
     __syncthreads();
     const int32_t s0 = s0_sh;
-    for (int r = 0; r < kChunk / 256; ++r) {
-        const uint32_t p = base + uint32_t(r) * 256u + threadIdx.x;
-        if (p >= n) break;
-        const int32_t s = seg[p];
-        if (s < 0) continue;
-        const Item& it = items[s];
-        const PrimRec pr = rec[p];
-        const float c[3] = {pr.cx, pr.cy, pr.cz}, lo[3] = {pr.lx, pr.ly, pr.lz}, hi[3] = {pr.hx, pr.hy, pr.hz};
-        unsigned long long klo[3], khi[3];
-        for (int k = 0; k < 3; ++k) { klo[k] = key_min(lo[k], p); khi[k] = key_max(hi[k], p); }
-        for (int a = 0; a < 3; ++a) {
-            const uint32_t b = uint32_t(a) * kBins + bin_of(c[a], it.c2b[a], it.off[a]);
-            if (s == s0) {
-                atomicAdd(&scount[b], 1u);
-                for (int k = 0; k < 3; ++k) { atomicMin(&slo[b][k], klo[k]); atomicMax(&shi[b][k], khi[k]); }
-            } else {
-                BinKeys& g = bins[size_t(s) * 3 * kBins + b];
-                atomicAdd(&g.count, 1u);
-                for (int k = 0; k < 3; ++k) { atomicMin(&g.lo[k], klo[k]); atomicMax(&g.hi[k], khi[k]); }
+    int32_t cur = -1;
+    float mc2b = 0.f, moff = 0.f;
+    float lo[3], hi[3];
+    uint32_t plo[3], phi[3], cnt = 0;
+    auto reset = [&]() {
+        for (int k = 0; k < 3; ++k) { lo[k] = FLT_MAX; hi[k] = -FLT_MAX; plo[k] = 0x7fffffffu; phi[k] = 0x7fffffffu; }
+        cnt = 0;
+    };
+    auto flush = [&]() {
+        if (cur < 0 || !binlane || cnt == 0) return;
+        const uint32_t idx = lane;
+        if (cur == s0) {
+            atomicAdd(&scount[idx], cnt);
+            for (int k = 0; k < 3; ++k) { atomicMin(&slo[idx][k], key_min(lo[k], plo[k])); atomicMax(&shi[idx][k], key_max(hi[k], phi[k])); }
+        } else {
+            BinKeys& g = bins[size_t(cur) * 3 * kBins + idx];
+            atomicAdd(&g.count, cnt);
+            for (int k = 0; k < 3; ++k) { atomicMin(&g.lo[k], key_min(lo[k], plo[k])); atomicMax(&g.hi[k], key_max(hi[k], phi[k])); }
+        }
+    };
+    reset();
+    for (int r = 0; r < kChunk / 4 / 64; ++r) {
+        const uint32_t p0 = base + uint32_t(r) * 64u;
+        if (p0 + lane < n) { stage[wave][lane] = rec[p0 + lane]; sseg[wave][lane] = seg[p0 + lane]; }
+        else sseg[wave][lane] = -1;
+        __syncthreads();
+        const int32_t s_run = sseg[wave][0];
+        if (__ballot(sseg[wave][lane] == s_run) == ~0ull) {            // one item (or none) in this run
+            if (s_run != cur) {
+                flush();
+                reset();
+                cur = s_run;
+                if (s_run >= 0) {
+                    const Item& it = items[s_run];
+                    mc2b = comp3(it.c2b[0], it.c2b[1], it.c2b[2], my_axis);
+                    moff = comp3(it.off[0], it.off[1], it.off[2], my_axis);
+                }
+            }
+            if (s_run >= 0 && binlane) {
+#pragma unroll 4
+                for (uint32_t j = 0; j < 64; ++j) {
+                    const PrimRec& pr = stage[wave][j];
+                    if (bin_of(comp3(pr.cx, pr.cy, pr.cz, my_axis), mc2b, moff) == my_bin) {
+                        const uint32_t p = p0 + j;
+                        ++cnt;
+                        const float vl[3] = {pr.lx, pr.ly, pr.lz}, vh[3] = {pr.hx, pr.hy, pr.hz};
+                        for (int k = 0; k < 3; ++k) {
+                            if (vl[k] < lo[k]) { lo[k] = vl[k]; plo[k] = p; }
+                            if (hi[k] < vh[k]) { hi[k] = vh[k]; phi[k] = p; }
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            continue;
+        }
+        for (uint32_t j = 0; j < 64; ++j) {
+            const int32_t sj = sseg[wave][j];
+            if (sj != cur) {
+                flush();
+                reset();
+                cur = sj;
+                if (sj >= 0) {
+                    const Item& it = items[sj];
+                    mc2b = comp3(it.c2b[0], it.c2b[1], it.c2b[2], my_axis);
+                    moff = comp3(it.off[0], it.off[1], it.off[2], my_axis);
+                }
+            }
+            if (sj < 0) continue;
+            const PrimRec& pr = stage[wave][j];
+            const float c = comp3(pr.cx, pr.cy, pr.cz, my_axis);
+            if (binlane && bin_of(c, mc2b, moff) == my_bin) {
+                const uint32_t p = p0 + j;
+                ++cnt;
+                const float vl[3] = {pr.lx, pr.ly, pr.lz}, vh[3] = {pr.hx, pr.hy, pr.hz};
+                for (int k = 0; k < 3; ++k) {
+                    if (vl[k] < lo[k]) { lo[k] = vl[k]; plo[k] = p; }
+                    if (hi[k] < vh[k]) { hi[k] = vh[k]; phi[k] = p; }
+                }
             }
         }
+        __syncthreads();
     }
+    flush();
     __syncthreads();
     if (s0 >= 0 && threadIdx.x < 3u * kBins && scount[threadIdx.x]) {
         BinKeys& g = bins[size_t(s0) * 3 * kBins + threadIdx.x];
@@ -552,14 +640,48 @@ __global__ void __launch_bounds__(256) k_swap_seg(PrimRec* __restrict__ rec, int
 // inner nodes' first_child is local until k_place rebases them.
 struct StackEntry { uint32_t begin, end, depth; int32_t local; float box[6]; };
 
+// 16-lane segmented scans over the bins of one axis (lane = axis * 16 + bin).  The combine keeps
+// the EARLIER bin on ties, as the reference's ascending extend loops do (sign of zero exact).
+struct LaneBox { float lo[3], hi[3]; uint32_t cnt; };
+
+__device__ __forceinline__ LaneBox prefix16(LaneBox v, uint32_t i) {           // bins 0..i
+    for (int d = 1; d < 16; d <<= 1) {
+        LaneBox u;
+        for (int k = 0; k < 3; ++k) { u.lo[k] = __shfl_up(v.lo[k], d, 16); u.hi[k] = __shfl_up(v.hi[k], d, 16); }
+        u.cnt = __shfl_up(v.cnt, d, 16);
+        if (i >= uint32_t(d)) {
+            for (int k = 0; k < 3; ++k) { v.lo[k] = lesser(u.lo[k], v.lo[k]); v.hi[k] = greater(u.hi[k], v.hi[k]); }
+            v.cnt += u.cnt;
+        }
+    }
+    return v;
+}
+__device__ __forceinline__ LaneBox suffix16(LaneBox v, uint32_t i) {           // bins i..15
+    for (int d = 1; d < 16; d <<= 1) {
+        LaneBox u;
+        for (int k = 0; k < 3; ++k) { u.lo[k] = __shfl_down(v.lo[k], d, 16); u.hi[k] = __shfl_down(v.hi[k], d, 16); }
+        u.cnt = __shfl_down(v.cnt, d, 16);
+        if (i + uint32_t(d) < 16u) {
+            for (int k = 0; k < 3; ++k) { v.lo[k] = lesser(v.lo[k], u.lo[k]); v.hi[k] = greater(v.hi[k], u.hi[k]); }
+            v.cnt += u.cnt;
+        }
+    }
+    return v;
+}
+__device__ __forceinline__ float lane_half_area(const LaneBox& b) { return half_area(b.lo, b.hi); }
+
+// One wavefront builds the whole subtree of a small item.  Bins: keyed LDS atomics (position =
+// order of the reference's sequential loop); SAH sweeps: segmented scans, 16 lanes per axis
+// (the costs depend only on box values and counts, so they are bit-identical to the sequential
+// sweeps of binned_sah_builder.hpp:89-114); the first minimal cost wins (strict <).
 __global__ void __launch_bounds__(64) k_small(PrimRec* __restrict__ rec, const SmallItem* __restrict__ small, uint32_t n_small,
                                               RefNode* __restrict__ nodes, RefNode* __restrict__ tnodes,
                                               uint32_t* __restrict__ small_count, uint32_t* __restrict__ prim_out) {
     __shared__ PrimRec R[kSmall];
     __shared__ StackEntry st[kStack];
-    __shared__ BinF bins[3 * kBins];
+    __shared__ unsigned long long klo[3 * kBins][3], khi[3 * kBins][3];
+    __shared__ uint32_t kcnt[3 * kBins];
     __shared__ uint16_t posF[kSmall / 2], posT[kSmall / 2];
-    __shared__ uint32_t dec[4];
     const uint32_t s = blockIdx.x;
     if (s >= n_small) return;
     const uint32_t lane = threadIdx.x;
@@ -576,50 +698,87 @@ __global__ void __launch_bounds__(64) k_small(PrimRec* __restrict__ rec, const S
     int sp = 1;
     uint32_t nc = 0;                                         // local nodes allocated
     RefNode* const tbase = tnodes + 2 * size_t(b0);
-    const uint32_t my_axis = lane / kBins, my_bin = lane % kBins;
+    const uint32_t my_axis = lane >> 4, bi = lane & 15u;     // lanes 48..63: padding group
     while (sp > 0) {
         const StackEntry e = st[--sp];
         __syncthreads();
         RefNode* const nd = e.local < 0 ? nodes + si.node : tbase + e.local;
         const uint32_t m = e.end - e.begin;
-        auto leaf = [&]() {
+        if (m <= 1 || e.depth >= kMaxDepth) {
             if (lane == 0) { nd->primitive_count = m; nd->first_child_or_primitive = b0 + e.begin; }
-        };
-        if (m <= 1 || e.depth >= kMaxDepth) { leaf(); continue; }
+            continue;
+        }
         float c2b[3], off[3];
         for (int a = 0; a < 3; ++a) {
             const float lo = e.box[2 * a], hi = e.box[2 * a + 1];
             c2b[a] = (1.0f / (hi - lo)) * float(kBins);
             off[a] = (-lo) * c2b[a];
         }
-        // bins in the reference's sequential order: lane (axis, bin) scans all primitives
-        if (lane < 3u * kBins) {
-            float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-            uint32_t cnt = 0;
-            const float mc2b = comp3(c2b[0], c2b[1], c2b[2], my_axis), moff = comp3(off[0], off[1], off[2], my_axis);
-            for (uint32_t k = e.begin; k < e.end; ++k) {
-                const PrimRec& pr = R[k];
-                const float c = comp3(pr.cx, pr.cy, pr.cz, my_axis);
-                if (bin_of(c, mc2b, moff) == my_bin) {
-                    ++cnt;
-                    lo[0] = lesser(lo[0], pr.lx); lo[1] = lesser(lo[1], pr.ly); lo[2] = lesser(lo[2], pr.lz);
-                    hi[0] = greater(hi[0], pr.hx); hi[1] = greater(hi[1], pr.hy); hi[2] = greater(hi[2], pr.hz);
+        LaneBox v;
+        for (int k = 0; k < 3; ++k) { v.lo[k] = FLT_MAX; v.hi[k] = -FLT_MAX; }
+        v.cnt = 0;
+        {
+            if (lane < 3u * kBins) {
+                for (int k = 0; k < 3; ++k) { klo[lane][k] = kKeyMinEmpty; khi[lane][k] = kKeyMaxEmpty; }
+                kcnt[lane] = 0;
+            }
+            __syncthreads();
+            for (uint32_t p = e.begin + lane; p < e.end; p += 64) {
+                const PrimRec& pr = R[p];
+                const float c[3] = {pr.cx, pr.cy, pr.cz}, lo[3] = {pr.lx, pr.ly, pr.lz}, hi[3] = {pr.hx, pr.hy, pr.hz};
+                for (int a = 0; a < 3; ++a) {
+                    const uint32_t b = uint32_t(a) * kBins + bin_of(c[a], c2b[a], off[a]);
+                    atomicAdd(&kcnt[b], 1u);
+                    for (int k = 0; k < 3; ++k) { atomicMin(&klo[b][k], key_min(lo[k], p)); atomicMax(&khi[b][k], key_max(hi[k], p)); }
                 }
             }
-            BinF& bf = bins[lane];
-            for (int k = 0; k < 3; ++k) { bf.lo[k] = lo[k]; bf.hi[k] = hi[k]; }
-            bf.count = cnt;
+            __syncthreads();
+            if (lane < 3u * kBins) {
+                for (int k = 0; k < 3; ++k) { v.lo[k] = key_value(klo[lane][k]); v.hi[k] = key_value(khi[lane][k]); }
+                v.cnt = kcnt[lane];
+            }
         }
-        __syncthreads();
-        if (lane == 0) {
-            uint32_t axis = 0, split = 0, sah = 0;
-            const bool ok = sah_decide(bins, m, e.box, axis, split, sah);
-            dec[0] = ok; dec[1] = axis; dec[2] = split; dec[3] = sah;
+        const LaneBox L = prefix16(v, bi), Rs = suffix16(v, bi);
+        const float rcost = lane_half_area(Rs) * float(Rs.cnt);
+        const float rnext = __shfl_down(rcost, 1, 16);
+        const float cost = lane_half_area(L) * float(L.cnt) + rnext;
+        // first minimal valid cost of this axis (sequential "if (cost < best)" from FLT_MAX)
+        const bool valid = bi < 15u && cost < FLT_MAX;
+        float bc = valid ? cost : INFINITY;
+        uint32_t bs = valid ? bi + 1u : uint32_t(kBins);
+        for (int d = 8; d > 0; d >>= 1) {
+            const float oc = __shfl_xor(bc, d, 16);
+            const uint32_t os = __shfl_xor(bs, d, 16);
+            if (oc < bc || (oc == bc && os < bs)) { bc = oc; bs = os; }
         }
-        __syncthreads();
-        if (!dec[0]) { leaf(); continue; }
-        const uint32_t axis = dec[1], split = dec[2], sah = dec[3];
-        const float ac2b = c2b[axis], aoff = off[axis];
+        if (bs == uint32_t(kBins)) bc = FLT_MAX;
+        const float bcost[3] = {__shfl(bc, 0), __shfl(bc, 16), __shfl(bc, 32)};
+        const uint32_t bsplit[3] = {uint32_t(__shfl(int(bs), 0)), uint32_t(__shfl(int(bs), 16)), uint32_t(__shfl(int(bs), 32))};
+        uint32_t axis = 0;
+        if (bcost[0] > bcost[1]) axis = 1;
+        if (comp3(bcost[0], bcost[1], bcost[2], axis) > bcost[2]) axis = 2;
+        uint32_t split = sel3(bsplit[0], bsplit[1], bsplit[2], axis);
+        const float nlo[3] = {e.box[0], e.box[2], e.box[4]}, nhi[3] = {e.box[1], e.box[3], e.box[5]};
+        const float leaf_cost = half_area(nlo, nhi) * (float(m) - 1.0f);
+        bool make_leaf = false;
+        if (split == uint32_t(kBins) || comp3(bcost[0], bcost[1], bcost[2], axis) >= leaf_cost) {
+            if (m <= kMaxLeaf) {
+                make_leaf = true;
+            } else {
+                const float d0 = nhi[0] - nlo[0], d1 = nhi[1] - nlo[1], d2 = nhi[2] - nlo[2];   // largest_axis
+                axis = 0;
+                if (d0 < d1) axis = 1;
+                if (comp3(d0, d1, d2, axis) < d2) axis = 2;
+                const unsigned long long hit = __ballot(my_axis == axis && bi < 15u && L.cnt >= (m * 2u / 5u + 1u));
+                if (hit) split = uint32_t(__ffsll(hit) - 1) - axis * kBins + 1u;
+            }
+        }
+        if (make_leaf) {
+            if (lane == 0) { nd->primitive_count = m; nd->first_child_or_primitive = b0 + e.begin; }
+            continue;
+        }
+        const uint32_t sah = sel3(bsplit[0], bsplit[1], bsplit[2], axis);
+        const float ac2b = comp3(c2b[0], c2b[1], c2b[2], axis), aoff = comp3(off[0], off[1], off[2], axis);
         // partition: count, then misplaced positions, then swaps (libstdc++ std::partition)
         uint32_t T = 0;
         for (uint32_t base = e.begin; base < e.end; base += 64) {
@@ -627,21 +786,22 @@ __global__ void __launch_bounds__(64) k_small(PrimRec* __restrict__ rec, const S
             const bool f = p < e.end && bin_of(comp3(R[p].cx, R[p].cy, R[p].cz, axis), ac2b, aoff) < split;
             T += uint32_t(__popcll(__ballot(f)));
         }
-        if (T == 0 || T == m) { leaf(); continue; }
+        if (T == 0 || T == m) {
+            if (lane == 0) { nd->primitive_count = m; nd->first_child_or_primitive = b0 + e.begin; }
+            continue;
+        }
         const uint32_t mid = e.begin + T;
         uint32_t tr = 0, M = 0;
         for (uint32_t base = e.begin; base < e.end; base += 64) {
             const uint32_t p = base + lane;
             const bool f = p < e.end && bin_of(comp3(R[p].cx, R[p].cy, R[p].cz, axis), ac2b, aoff) < split;
             const unsigned long long mask = __ballot(f);
-            const uint32_t below = uint32_t(__popcll(mask & ((1ull << lane) - 1ull)));
-            const uint32_t trp = tr + below;                 // trues in [begin, p)
+            const uint32_t trp = tr + uint32_t(__popcll(mask & ((1ull << lane) - 1ull)));   // trues in [begin, p)
             if (p < e.end) {
                 if (p < mid && !f) posF[(p - e.begin) - trp] = uint16_t(p);
                 else if (p >= mid && f) posT[T - 1 - trp] = uint16_t(p);
             }
-            const unsigned long long lmask = __ballot(p < mid && p < e.end && !f);
-            M += uint32_t(__popcll(lmask));
+            M += uint32_t(__popcll(__ballot(p < mid && p < e.end && !f)));
             tr += uint32_t(__popcll(mask));
         }
         __syncthreads();
@@ -651,13 +811,17 @@ __global__ void __launch_bounds__(64) k_small(PrimRec* __restrict__ rec, const S
             R[a] = rb;
             R[b] = ra;
         }
-        __syncthreads();
-        // two child nodes, boxes from the bins; push right then left
+        // child boxes (binned_sah_builder.hpp:216-224): left = bins [0, sah), right = bins [split, 16)
+        float lb[6], rb[6];
+        const int lsrc = int(axis * kBins + sah - 1u), rsrc = int(axis * kBins + split);
+        for (int k = 0; k < 3; ++k) {
+            lb[2 * k] = __shfl(L.lo[k], lsrc); lb[2 * k + 1] = __shfl(L.hi[k], lsrc);
+            rb[2 * k] = __shfl(Rs.lo[k], rsrc); rb[2 * k + 1] = __shfl(Rs.hi[k], rsrc);
+        }
         const uint32_t child = nc;
         nc += 2;
+        __syncthreads();
         if (lane == 0) {
-            float lb[6], rb[6];
-            child_boxes(bins, axis, split, sah, lb, rb);
             RefNode l, r;
             for (int k = 0; k < 6; ++k) { l.bounds[k] = lb[k]; r.bounds[k] = rb[k]; }
             l.primitive_count = r.primitive_count = 0;
@@ -781,7 +945,7 @@ int ceres_bvh_build_device(const float* d_tri48, size_t n_tri, uint32_t* d_nodes
         const unsigned long long key_init[6] = {kKeyMinEmpty, kKeyMinEmpty, kKeyMinEmpty, kKeyMaxEmpty, kKeyMaxEmpty, kKeyMaxEmpty};
         BVH_TRY(hipMemcpyAsync(keys, key_init, sizeof key_init, hipMemcpyHostToDevice, stream));
         const uint32_t g256 = (n + 255) / 256;
-        hipLaunchKernelGGL(k_init, dim3(g256), dim3(256), 0, stream, reinterpret_cast<const Tri48*>(d_tri48), n, rec, seg,
+        hipLaunchKernelGGL(k_init, dim3((n + 256 * kInitPer - 1) / (256 * kInitPer)), dim3(256), 0, stream, reinterpret_cast<const Tri48*>(d_tri48), n, rec, seg,
                            n > kSmall ? 0 : -1, keys);
         BVH_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_root, dim3(1), dim3(64), 0, stream, nodes, keys, n, items[0], small, ctr);

@@ -8,7 +8,9 @@
 //   render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]
 //                [--rotate x|y|z deg] [--size W H] [-o|--out file.ppm] [--primary-only]
 //                [--proc N] [--device D] [--bench reps] [--json]
-//                [--orbit ax ay az step_deg count] [--frames N]
+//                [--orbit ax ay az step_deg count] [--frames N] [--gpu-bvh]
+//
+// --gpu-bvh builds the same BinnedSahBuilder BVH with the gfx950 builder (bvh_build.hip).
 //
 // --orbit / --frames are the anim.cpp:76-125 driver without Magick++: the camera eye, dir and
 // the sun are rotated by step_deg about the axis (transform.hpp:67-112) `count` times before
@@ -38,7 +40,7 @@ struct Opts {
     float rot_deg = 0.f;
     size_t W = 1920, H = 1080;
     int mode = CERES_MODE_FULL, proc = 0, device = 0, bench = 0;
-    bool json = false;
+    bool json = false, gpu_bvh = false;
     float orbit_axis[3] = {0.f, 1.f, 0.f}, orbit_step = 0.f;
     int orbit_count = 0, frames = 1;
 };
@@ -47,7 +49,8 @@ int usage() {
     std::fprintf(stderr,
                  "usage: render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]\n"
                  "              [--rotate x|y|z deg] [--size W H] [-o out.ppm] [--primary-only] [--proc N]\n"
-                 "              [--device D] [--bench reps] [--json] [--orbit ax ay az step_deg count] [--frames N]\n");
+                 "              [--device D] [--bench reps] [--json] [--orbit ax ay az step_deg count] [--frames N]\n"
+                 "              [--gpu-bvh]\n");
     return 2;
 }
 
@@ -78,6 +81,7 @@ bool parse(int argc, char** argv, Opts& o) {
         else if (a == "--device") { if (!have(1)) return false; o.device = std::atoi(argv[++i]); }
         else if (a == "--bench") { if (!have(1)) return false; o.bench = std::atoi(argv[++i]); }
         else if (a == "--json") o.json = true;
+        else if (a == "--gpu-bvh") o.gpu_bvh = true;
         else if (a == "--orbit") {
             if (!vec(o.orbit_axis) || !have(2) || !f(argv[i + 1], &o.orbit_step)) return false;
             o.orbit_count = std::atoi(argv[i + 2]); i += 2;
@@ -104,10 +108,12 @@ int main(int argc, char** argv) {
     if (n_tri == 0) { std::fprintf(stderr, "The given scene is empty or cannot be loaded\n"); return 1; }   // static.cpp:77-80
     if (o.rot_axis >= 0) ceres_rotate_triangles(tri, n_tri, o.rot_axis, o.rot_deg);
 
-    std::printf("Building BVH ( using BinnedSahBuilder )...\n");
+    std::printf("Building BVH ( using BinnedSahBuilder%s )...\n", o.gpu_bvh ? " on the GPU" : "");
     const double t0 = now_s();
     uint32_t* nodes = nullptr; uint64_t* prim = nullptr; size_t n_nodes = 0;
-    if (ceres_bvh_build(tri, n_tri, &nodes, &n_nodes, &prim) != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
+    const int rc_bvh = o.gpu_bvh ? ceres_bvh_build_gpu(tri, n_tri, &nodes, &n_nodes, &prim, o.device)
+                                 : ceres_bvh_build(tri, n_tri, &nodes, &n_nodes, &prim);
+    if (rc_bvh != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
     std::printf("%g\n", now_s() - t0);
     std::printf("BVH of %zu node(s) and %zu reference(s)\n", n_nodes, n_tri);
 

@@ -310,12 +310,13 @@ def test_c5_procedural_10m_triangles(gpu):
     scene.close()
 
 
-def test_cli_writes_reference_ppm(gpu, tmp_path):
+@pytest.mark.parametrize("gpu_bvh", [False, True])
+def test_cli_writes_reference_ppm(gpu, tmp_path, gpu_bvh):
     pkg = gpu
     name = "bunny_640"
     meta, _, ppm = load_golden(name)
     out = tmp_path / "bunny.ppm"
-    args = configs.cli_args(configs.CONFIGS[name])
+    args = configs.cli_args(configs.CONFIGS[name]) + (["--gpu-bvh"] if gpu_bvh else [])
     r = subprocess.run([pkg.CLI_PATH] + args + ["-o", str(out)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "Rays: %d\tHits: %d" % (meta["exact"]["rays"], meta["exact"]["hits"]) in r.stdout
