@@ -34,7 +34,8 @@ SCENE_STATS = 1
 
 EXPORTED_SYMBOLS = (
     "ceres_obj_load", "ceres_proc_mesh", "ceres_rotate_triangles", "ceres_bvh_build", "ceres_bvh_build_gpu",
-    "ceres_bvh_build_device", "ceres_camera_basis",
+    "ceres_bvh_build_device", "ceres_obj_load_gpu", "ceres_obj_parse_device", "ceres_rotate_triangles_device",
+    "ceres_device_free", "ceres_camera_basis",
     "ceres_free", "ceres_scene_create", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
@@ -98,6 +99,12 @@ def lib():
     L.ceres_bvh_build_gpu.argtypes = [_fp, _sz, ctypes.POINTER(_u32p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p),
                                       ctypes.c_int]
     L.ceres_bvh_build_device.argtypes = [_vp, _sz, _vp, _vp, ctypes.POINTER(_sz), _vp]
+    L.ceres_obj_load_gpu.argtypes = [ctypes.c_char_p, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz),
+                                     ctypes.c_int]
+    L.ceres_obj_parse_device.argtypes = [_vp, _sz, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_sz), _vp]
+    L.ceres_rotate_triangles_device.argtypes = [_vp, _sz, ctypes.c_int, ctypes.c_float, _vp]
+    L.ceres_device_free.argtypes = [_vp]
+    L.ceres_device_free.restype = None
     L.ceres_camera_basis.argtypes = [_fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp]
     L.ceres_orbit_cameras.argtypes = [_fp, _fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp, ctypes.c_float,
                                       ctypes.c_uint32, ctypes.c_int, _fp, _fp, _fp]
@@ -185,6 +192,32 @@ def load_obj(path):
     _check(lib().ceres_obj_load(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt)))
     c = cnt.value
     return Mesh(_take(t, c * 12, np.float32).reshape(c, 12), _take(n, c * 9, np.float32).reshape(c, 9))
+
+
+def load_obj_gpu(path, device=0):
+    """load_obj with the text parsed on the GPU (ceres_obj_load_gpu): the same bits."""
+    t, n, cnt = _fp(), _fp(), _sz()
+    _check(lib().ceres_obj_load_gpu(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt), int(device)))
+    c = cnt.value
+    return Mesh(_take(t, c * 12, np.float32).reshape(c, 12), _take(n, c * 9, np.float32).reshape(c, 9))
+
+
+def parse_obj_device(d_text, length, stream=0):
+    """ceres_obj_parse_device on a device text buffer (int pointer): returns (d_tri48, d_norm36, n_tri)
+    device pointers (free with device_free)."""
+    t, n, cnt = _vp(), _vp(), _sz()
+    _check(lib().ceres_obj_parse_device(d_text, length, ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt),
+                                        stream or None))
+    return t.value or 0, n.value or 0, cnt.value
+
+
+def rotate_triangles_device(d_tri48, n_tri, axis, degrees, stream=0):
+    ax = {"x": 0, "y": 1, "z": 2}[axis] if isinstance(axis, str) else int(axis)
+    _check(lib().ceres_rotate_triangles_device(d_tri48, n_tri, ax, float(degrees), stream or None))
+
+
+def device_free(d_ptr):
+    lib().ceres_device_free(d_ptr or None)
 
 
 def proc_mesh(n):

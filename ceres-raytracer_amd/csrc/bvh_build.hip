@@ -31,11 +31,14 @@
 #include "ceres_render.h"
 #include "ceres_types.hpp"
 #include "host_common.hpp"
+#include "dev_scan.hpp"
 
 #pragma clang fp contract(off)
 
 namespace ceres {
 namespace bvhdev {
+
+using namespace devscan;
 
 constexpr int kBins = 16;
 constexpr uint32_t kMaxDepth = 64;       // top_down_builder.hpp:36
@@ -453,63 +456,6 @@ __global__ void __launch_bounds__(256) k_flags(const PrimRec* __restrict__ rec, 
         }
     }
     flag[p] = f;
-}
-
-// ---- exclusive scan of u32 (n + 1 outputs: x[n] = total) --------------------------------
-constexpr int kScanBlock = 1024;           // elements per block (256 threads x 4)
-
-__device__ uint32_t block_exclusive_scan_256(uint32_t v, uint32_t* sh, uint32_t& total) {
-    // sh: 256 + 8 entries
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t x = v;
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, 64);
-        if (lane >= uint32_t(off)) x += y;
-    }
-    if (lane == 63) sh[256 + wave] = x;
-    __syncthreads();
-    uint32_t wbase = 0;
-    for (uint32_t w = 0; w < wave; ++w) wbase += sh[256 + w];
-    total = sh[256] + sh[257] + sh[258] + sh[259];
-    __syncthreads();
-    return wbase + x - v;
-}
-
-__global__ void __launch_bounds__(256) k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n, uint32_t* __restrict__ partial) {
-    __shared__ uint32_t sh[264];
-    const uint32_t base = blockIdx.x * uint32_t(kScanBlock) + threadIdx.x * 4u;
-    uint32_t v = 0;
-    for (int k = 0; k < 4; ++k) if (base + k < n) v += in[base + k];
-    uint32_t total;
-    (void)block_exclusive_scan_256(v, sh, total);
-    if (threadIdx.x == 0) partial[blockIdx.x] = total;
-}
-
-// single workgroup: exclusive scan of the block partials in place
-__global__ void __launch_bounds__(256) k_scan_partials(uint32_t* partial, uint32_t nb) {
-    __shared__ uint32_t sh[264];
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += 256) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < nb ? partial[i] : 0u;
-        uint32_t total;
-        const uint32_t ex = block_exclusive_scan_256(v, sh, total);
-        if (i < nb) partial[i] = carry + ex;
-        carry += total;
-    }
-    if (threadIdx.x == 0) partial[nb] = carry;
-}
-
-__global__ void __launch_bounds__(256) k_scan_down(const uint32_t* __restrict__ in, uint32_t n, const uint32_t* __restrict__ partial,
-                                                   uint32_t* __restrict__ out) {
-    __shared__ uint32_t sh[264];
-    const uint32_t base = blockIdx.x * uint32_t(kScanBlock) + threadIdx.x * 4u;
-    uint32_t v[4], sum = 0;
-    for (int k = 0; k < 4; ++k) { v[k] = base + k < n ? in[base + k] : 0u; sum += v[k]; }
-    uint32_t total;
-    uint32_t x = partial[blockIdx.x] + block_exclusive_scan_256(sum, sh, total);
-    for (int k = 0; k < 4; ++k) { if (base + k < n) out[base + k] = x; x += v[k]; }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = partial[gridDim.x];
 }
 
 // ---- per-level plan (one workgroup): finalize splits, allocate child nodes and items ------

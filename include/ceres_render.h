@@ -92,6 +92,18 @@ int ceres_bvh_build_gpu(const float* tri48, size_t n_tri, uint32_t** nodes32, si
                         int device);
 int ceres_bvh_build_device(const float* d_tri48, size_t n_tri, uint32_t* d_nodes32, uint32_t* d_prim32,
                            size_t* n_nodes, void* stream);
+/* obj::load_from_stream on the GPU: the reference loader's exact triangles
+ * and face-order normal sums (obj_norms.hpp:57-118), numbers via glibc-exact strtof/strtol.
+ * ceres_obj_load_gpu: same contract as ceres_obj_load (file read on the host, parsed on HIP
+ * `device`, malloc'd outputs).  ceres_obj_parse_device: device text in; *d_tri48 / *d_norm36
+ * are device arrays (free with ceres_device_free), NULL when the mesh is empty.  A face
+ * referencing a missing vertex (the reference's assert, obj_norms.hpp:90) returns CERES_EIO. */
+int ceres_obj_load_gpu(const char* path, float** tri48, float** norm36, size_t* n_tri, int device);
+int ceres_obj_parse_device(const char* d_text, size_t len, float** d_tri48, float** d_norm36, size_t* n_tri,
+                           void* stream);
+/* rotate_triangles<Axis> on device triangles (cos/sin of the angle taken on the host). */
+int ceres_rotate_triangles_device(float* d_tri48, size_t n_tri, int axis, float degrees, void* stream);
+void ceres_device_free(void* d_ptr);
 /* Camera basis of render.hpp:91-97: out = {dir[3], image_u*w[3], image_v*w*ratio[3]}. */
 int ceres_camera_basis(const float eye[3], const float dir[3], const float up[3], float fov_deg,
                        size_t width, size_t height, float out9[9]);
