@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "ceres_obj_load", "ceres_proc_mesh", "ceres_rotate_triangles", "ceres_bvh_build", "ceres_bvh_build_gpu",
     "ceres_bvh_build_device", "ceres_obj_load_gpu", "ceres_obj_parse_device", "ceres_rotate_triangles_device",
     "ceres_device_free", "ceres_camera_basis",
-    "ceres_free", "ceres_scene_create", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
+    "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
@@ -112,6 +112,8 @@ def lib():
     L.ceres_free.restype = None
     L.ceres_scene_create.argtypes = [_fp, _sz, _fp, _vp, _sz, _u64p, ctypes.c_int, ctypes.c_uint32]
     L.ceres_scene_create.restype = _vp
+    L.ceres_scene_create_device.argtypes = [_vp, _sz, _vp, _vp, _sz, _vp, ctypes.c_int, ctypes.c_uint32, _vp]
+    L.ceres_scene_create_device.restype = _vp
     L.ceres_scene_destroy.argtypes = [_vp]
     L.ceres_scene_destroy.restype = None
     L.ceres_scene_info.argtypes = [_vp, _u32p, _u32p, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]
@@ -258,8 +260,11 @@ def build_bvh_device(d_tri48, n_tri, d_nodes32, d_prim32, stream=0):
 class Scene:
     """A scene resident in HBM of one device (ceres_scene_create)."""
 
-    def __init__(self, mesh, bvh, device=0, stats=False):
+    def __init__(self, mesh, bvh, device=0, stats=False, _handle=None):
         L = lib()
+        if _handle is not None:                      # Scene.from_device
+            self._h, self.device, self.n_tri = _handle
+            return
         self._h = L.ceres_scene_create(_p(mesh.tri, ctypes.c_float), len(mesh), _p(mesh.norm, ctypes.c_float),
                                        bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0],
                                        _p(bvh.prim, ctypes.c_uint64), int(device), SCENE_STATS if stats else 0)
@@ -267,6 +272,16 @@ class Scene:
             raise CeresError("ceres_scene_create: " + L.ceres_last_error().decode())
         self.device = device
         self.n_tri = len(mesh)
+
+    @classmethod
+    def from_device(cls, d_tri48, n_tri, d_norm36, d_nodes32, n_nodes, d_prim32, device=0, stats=False, stream=0):
+        """ceres_scene_create_device: a scene from arrays already in HBM (int device pointers)."""
+        L = lib()
+        h = L.ceres_scene_create_device(d_tri48, n_tri, d_norm36, d_nodes32, n_nodes, d_prim32, int(device),
+                                        SCENE_STATS if stats else 0, stream or None)
+        if not h:
+            raise CeresError("ceres_scene_create_device: " + L.ceres_last_error().decode())
+        return cls(None, None, _handle=(h, device, n_tri))
 
     def info(self):
         d, s, n, b = ctypes.c_uint32(), ctypes.c_uint32(), _sz(), _sz()

@@ -110,6 +110,20 @@ struct KParams {
     unsigned long long* wave_log;
 };
 
+// device: reference BVH in HBM -> GPU layout (scene_device.hip); buffers hipMalloc'd
+struct DeviceLayout {
+    SiblingPair* pairs = nullptr;
+    Node4* nodes4 = nullptr;
+    Tri48* tris = nullptr;
+    uint32_t* orig = nullptr;
+    size_t n_pairs = 0, n_nodes4 = 0;
+    uint32_t depth = 0, stack4 = 0, root_leaf_count = 0, root_leaf_first = 0;
+};
+#ifdef __HIPCC__
+int relayout_device(const Tri48* d_tris, uint32_t n_tri, const RefNode* d_nodes, uint32_t n_nodes, const uint32_t* d_prim,
+                    hipStream_t stream, DeviceLayout& out);
+#endif
+
 // host: reference BVH -> GPU layout (scene_host.cpp)
 int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri48* tris,
                  std::vector<SiblingPair>& pairs, std::vector<Tri48>& leaf_tris, std::vector<uint32_t>& orig,

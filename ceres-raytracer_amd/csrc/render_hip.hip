@@ -1189,6 +1189,60 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     return s;
 }
 
+// Scene from arrays already in HBM (device `device`): the reference's Triangle[] / tri_norms
+// (e.g. from ceres_obj_parse_device + ceres_rotate_triangles_device) and a BVH with u32
+// primitive_indices (e.g. from ceres_bvh_build_device); relayout on the GPU (scene_device.hip).
+// The caller keeps its buffers.  Work is ordered on `stream` (NULL: the scene's own stream).
+ceres_scene* ceres_scene_create_device(const float* d_tri48, size_t n_tri, const float* d_norm36, const uint32_t* d_nodes32,
+                                       size_t n_nodes, const uint32_t* d_prim32, int device, uint32_t flags, void* stream) {
+    if (!d_tri48 || !d_norm36 || !d_nodes32 || !d_prim32 || n_tri == 0 || n_nodes == 0) {
+        set_error(CERES_EINVAL, "ceres_scene_create_device: empty scene or null argument");
+        return nullptr;
+    }
+    if (n_tri > 0xffffffffull || n_nodes > 0xffffffffull) { set_error(CERES_EUNSUPPORTED, "scene too large"); return nullptr; }
+    auto* s = new (std::nothrow) ceres_scene;
+    if (!s) { set_error(CERES_ENOMEM, "out of host memory"); return nullptr; }
+    DeviceLayout L;
+    auto fail = [&]() -> ceres_scene* {
+        if (L.pairs) (void)hipFree(L.pairs);
+        if (L.nodes4) (void)hipFree(L.nodes4);
+        if (L.tris) (void)hipFree(L.tris);
+        if (L.orig) (void)hipFree(L.orig);
+        scene_release(s); delete s; return nullptr;
+    };
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { set_error(CERES_EHIP, "no HIP device available"); return fail(); }
+    if (device < 0 || device >= ndev) { set_error(CERES_EINVAL, "device %d out of range (%d devices)", device, ndev); return fail(); }
+    s->device = device; s->flags = flags; s->n_tri = n_tri;
+    auto body = [&]() -> int {
+        HIP_TRY(hipSetDevice(device));
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return set_error(CERES_EHIP, "device %d is %s, this build targets gfx950 only", device, prop.gcnArchName);
+        s->num_cus = prop.multiProcessorCount;
+        HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
+        if (int rc = relayout_device(reinterpret_cast<const Tri48*>(d_tri48), uint32_t(n_tri),
+                                     reinterpret_cast<const RefNode*>(d_nodes32), uint32_t(n_nodes), d_prim32, st, L))
+            return rc;
+        s->d_pairs = L.pairs; s->d_nodes4 = L.nodes4; s->d_tris = L.tris; s->d_orig = L.orig;
+        s->n_pairs = L.n_pairs; s->n_nodes4 = L.n_nodes4;
+        s->depth = L.depth; s->root_leaf_count = L.root_leaf_count; s->root_leaf_first = L.root_leaf_first;
+        s->stack_entries = std::max<uint32_t>(1, L.depth);           // stack <= depth - 1 entries
+        s->shadow_stack_entries = std::max<uint32_t>(1, L.stack4);
+        L = DeviceLayout{};                                          // owned by the scene now
+        HIP_TRY(hipMalloc(&s->d_norms, n_tri * 36));
+        HIP_TRY(hipMemcpyAsync(s->d_norms, d_norm36, n_tri * 36, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMalloc(&s->d_shards, sizeof(Shard) * kShards));
+        HIP_TRY(hipMalloc(&s->d_counters, 8 * sizeof(uint64_t)));
+        HIP_TRY(hipStreamSynchronize(st));
+        return CERES_OK;
+    };
+    if (body()) return fail();
+    return s;
+}
+
 void ceres_scene_destroy(ceres_scene* s) {
     if (!s) return;
     scene_release(s);

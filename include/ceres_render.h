@@ -128,6 +128,14 @@ void ceres_free(void* p);
 ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* norm36,
                                 const void* nodes32, size_t n_nodes, const uint64_t* prim64,
                                 int device, uint32_t flags);
+/* The same scene from arrays already in HBM of `device`: d_tri48 / d_norm36 as
+ * above, the BVH as n_nodes x 32-B nodes with u32 primitive_indices (ceres_bvh_build_device's
+ * output).  The GPU layout is built on the GPU (records numbered differently from
+ * ceres_scene_create; the traversal and every image are identical).  Ordered on `stream`
+ * (a hipStream_t; NULL = the scene's own); the caller keeps its buffers. */
+ceres_scene* ceres_scene_create_device(const float* d_tri48, size_t n_tri, const float* d_norm36,
+                                       const uint32_t* d_nodes32, size_t n_nodes, const uint32_t* d_prim32,
+                                       int device, uint32_t flags, void* stream);
 void ceres_scene_destroy(ceres_scene* scene);
 /* depth of the BVH (levels below the root) and the traversal-stack entries the kernels use */
 int ceres_scene_info(const ceres_scene* scene, uint32_t* depth, uint32_t* stack_entries,
