@@ -437,28 +437,29 @@ int ceres_obj_load_gpu(const char* path, float** tri48, float** norm36, size_t* 
     if (!path || !tri48 || !norm36 || !n_tri) return set_error(CERES_EINVAL, "ceres_obj_load_gpu: null argument");
     *tri48 = *norm36 = nullptr;
     *n_tri = 0;
-    std::vector<char> buf;
-    if (FILE* f = std::fopen(path, "rb")) {
-        std::fseek(f, 0, SEEK_END);
-        const long sz = std::ftell(f);
-        std::fseek(f, 0, SEEK_SET);
-        if (sz > 0) {
-            buf.resize(size_t(sz));
-            buf.resize(std::fread(buf.data(), 1, buf.size(), f));
-        }
-        std::fclose(f);
-    }   // unreadable file: empty mesh, like obj_norms.hpp:123-126
-    if (buf.empty()) return CERES_OK;
     int rc = CERES_OK;
     hipStream_t stream = nullptr;
+    char* h_text = nullptr;                                   // pinned: the upload runs at PCIe speed
     char* d_text = nullptr;
     float *d_tri = nullptr, *d_norm = nullptr;
-    size_t n = 0;
+    size_t n = 0, len = 0;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return CERES_OK;                                  // unreadable file: empty mesh (obj_norms.hpp:123-126)
+    std::fseek(f, 0, SEEK_END);
+    const long sz = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
     OBJ_TRY(hipSetDevice(device));
+    if (sz > 0) {
+        OBJ_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_text), size_t(sz), hipHostMallocDefault));
+        len = std::fread(h_text, 1, size_t(sz), f);
+    }
+    std::fclose(f);
+    f = nullptr;
+    if (len == 0) goto done;
     OBJ_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    OBJ_TRY(hipMalloc(&d_text, buf.size()));
-    OBJ_TRY(hipMemcpyAsync(d_text, buf.data(), buf.size(), hipMemcpyHostToDevice, stream));
-    if ((rc = ceres_obj_parse_device(d_text, buf.size(), &d_tri, &d_norm, &n, stream)) != CERES_OK) goto done;
+    OBJ_TRY(hipMalloc(&d_text, len));
+    OBJ_TRY(hipMemcpyAsync(d_text, h_text, len, hipMemcpyHostToDevice, stream));
+    if ((rc = ceres_obj_parse_device(d_text, len, &d_tri, &d_norm, &n, stream)) != CERES_OK) goto done;
     if (n) {
         *tri48 = static_cast<float*>(std::malloc(n * 48));
         *norm36 = static_cast<float*>(std::malloc(n * 36));
@@ -469,10 +470,12 @@ int ceres_obj_load_gpu(const char* path, float** tri48, float** norm36, size_t* 
         *n_tri = n;
     }
 done:
+    if (f) std::fclose(f);
     if (rc != CERES_OK) { std::free(*tri48); std::free(*norm36); *tri48 = *norm36 = nullptr; *n_tri = 0; }
     if (d_tri) (void)hipFree(d_tri);
     if (d_norm) (void)hipFree(d_norm);
     if (d_text) (void)hipFree(d_text);
+    if (h_text) (void)hipHostFree(h_text);
     if (stream) (void)hipStreamDestroy(stream);
     return rc;
 }

@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Time-to-first-frame of the whole CERES pipeline (static.cpp:76-147) for a config whose mesh
+is OBJ text: load + normals, rotate, BVH, scene upload / relayout, first frame -- once on the
+host path (ceres_obj_load, ceres_rotate_triangles, ceres_bvh_build, ceres_scene_create) and once
+fully on the GPU (ceres_obj_parse_device, ceres_rotate_triangles_device, ceres_bvh_build_device,
+ceres_scene_create_device), both ending in the same GPU render, which must match the reference
+fixture.  Procedural configs are written as OBJ text first (tools/probes/proc_obj).
+Prints one JSON line per config.   python tools/pipeline_bench.py [configs...]
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+
+def main():
+    import torch
+    from conftest import import_package, load_golden
+    pkg = import_package()
+    names = sys.argv[1:] or ["dragon_1080", "proc_c5"]
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for name in names:
+        cfg = pkg.configs.CONFIGS[name]
+        meta, _, _ = load_golden(name)
+        bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
+        basis = np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
+        W, H = cfg["W"], cfg["H"]
+        with tempfile.TemporaryDirectory() as td:
+            if cfg.get("proc"):
+                path = os.path.join(td, "mesh.obj")
+                subprocess.run([os.path.join(REPO, "tools", "probes", "proc_obj"), str(cfg["proc"]), path], check=True)
+            else:
+                path = pkg.configs.obj_path(cfg)
+            text = open(path, "rb").read()
+            # warm both paths once on a tiny mesh (runtime init, kernel loads)
+            warm = pkg.load_obj(os.path.join(REPO, "tests", "golden", "quad.obj"))
+            pkg.Scene(warm, pkg.build_bvh_gpu(warm)).close()
+            # host path
+            t = {}
+            t0 = time.perf_counter()
+            mesh = pkg.load_obj(path)
+            t["load"] = time.perf_counter()
+            if cfg.get("rotate"):
+                pkg.rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1])
+            t["rotate"] = time.perf_counter()
+            bvh = pkg.build_bvh(mesh)
+            t["bvh"] = time.perf_counter()
+            scene = pkg.Scene(mesh, bvh)
+            t["scene"] = time.perf_counter()
+            _, rgb, _ = scene.render(basis, cfg["sun"], W, H, want_pixels=False)
+            t["frame"] = time.perf_counter()
+            scene.close()
+            host = {k: round((v - t0) * 1e3, 1) for k, v in t.items()}
+            host_ok = hashlib.sha256(pkg.ppm(W, H, rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
+            del mesh, bvh
+            # device path (text already in host memory; its upload is timed)
+            torch.cuda.synchronize(dev)
+            g = {}
+            t0 = time.perf_counter()
+            d_text = torch.frombuffer(bytearray(text), dtype=torch.uint8).pin_memory().to(dev, non_blocking=True)
+            torch.cuda.synchronize(dev)
+            g["upload_text"] = time.perf_counter()      # includes pinning the host buffer
+            d_tri, d_norm, n = pkg.parse_obj_device(d_text.data_ptr(), d_text.numel(), stream)
+            g["load"] = time.perf_counter()
+            if cfg.get("rotate"):
+                pkg.rotate_triangles_device(d_tri, n, cfg["rotate"][0], cfg["rotate"][1], stream)
+            torch.cuda.synchronize(dev)
+            g["rotate"] = time.perf_counter()
+            d_nodes = torch.empty((2 * n - 1) * 8, dtype=torch.int32, device=dev)
+            d_prim = torch.empty(n, dtype=torch.int32, device=dev)
+            m = pkg.build_bvh_device(d_tri, n, d_nodes.data_ptr(), d_prim.data_ptr(), stream)
+            g["bvh"] = time.perf_counter()
+            scene = pkg.Scene.from_device(d_tri, n, d_norm, d_nodes.data_ptr(), m, d_prim.data_ptr(), stream=stream)
+            g["scene"] = time.perf_counter()
+            _, rgb, _ = scene.render(basis, cfg["sun"], W, H, want_pixels=False)
+            g["frame"] = time.perf_counter()
+            scene.close()
+            pkg.device_free(d_tri)
+            pkg.device_free(d_norm)
+            gpu = {k: round((v - t0) * 1e3, 1) for k, v in g.items()}
+            gpu_ok = hashlib.sha256(pkg.ppm(W, H, rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
+        print(json.dumps({"config": name, "n_tri": int(n), "obj_bytes": len(text),
+                          "host_path_cumulative_ms": host, "gpu_path_cumulative_ms": gpu,
+                          "speedup_to_first_frame": round(host["frame"] / gpu["frame"], 1),
+                          "frames_match_reference": [host_ok, gpu_ok],
+                          "host_threads": int(os.environ.get("OMP_NUM_THREADS", "0") or os.cpu_count())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
