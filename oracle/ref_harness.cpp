@@ -23,6 +23,11 @@
 //   --dump p       write p.tri48 (rotated Triangle[]), p.norm36, p.nodes32, p.prim64
 //   --primary-only render.hpp:123-125 (commented-out normal visualisation) as the
 //                  primary-rays-only mode: pixel = |normalize(tri.n)|
+//
+// Built twice more with -DREF_SCALAR=double (_ref/ref_render_f64{,_exact}): the whole
+// sequence as render<double> (anim.cpp's -d mode, anim.cpp:146-155) -- load_from_file<double>,
+// rotate_triangles<double>, BinnedSahBuilder<Bvh<double>,16>, render<double>.  Command-line
+// numbers are then parsed with strtod (double literals, as anim.cpp writes its camera).
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -44,30 +49,37 @@
 #include "obj_norms.hpp"
 #include "transform.hpp"
 
-using Scalar   = float;
+#ifndef REF_SCALAR
+#define REF_SCALAR float
+#endif
+using Scalar   = REF_SCALAR;
 using Vector3  = bvh::Vector3<Scalar>;
 using Triangle = bvh::Triangle<Scalar>;
 using Bvh      = bvh::Bvh<Scalar>;
 
-static void hexf(char* buf, float f) {
+[[maybe_unused]] static void hexf(char* buf, float f) {
     uint32_t u; std::memcpy(&u, &f, 4); std::sprintf(buf, "\"0x%08x\"", u);
 }
+[[maybe_unused]] static void hexf(char* buf, double f) {
+    uint64_t u; std::memcpy(&u, &f, 8); std::sprintf(buf, "\"0x%016llx\"", (unsigned long long)u);
+}
+static Scalar num(const char* s) { return sizeof(Scalar) == 8 ? Scalar(std::strtod(s, nullptr)) : Scalar(std::strtof(s, nullptr)); }
 
 struct Args {
     std::string obj;
     Vector3 eye{0.f, -15.f, 2.f}, dir{0.f, 1.f, 0.f}, up{0.f, 0.f, 1.f}, sun{-50.f, -20.f, 0.f};
-    float fov = 60.f;
-    int rot_axis = -1; float rot_deg = 0.f;
+    Scalar fov = 60.f;
+    int rot_axis = -1; Scalar rot_deg = 0.f;
     size_t W = 1920, H = 1080;
     std::string out, fout, records, dump;
     int reps = 1;
     bool stats = false, primary_only = false;
     int proc = 0;  // >0: procedural heightfield with proc x proc vertices instead of an OBJ
     Vector3 orbit_axis{0.f, 1.f, 0.f};
-    float orbit_step = 0.f; int orbit_count = 0;   // --orbit: anim.cpp camera/sun rotations
+    Scalar orbit_step = 0.f; int orbit_count = 0;   // --orbit: anim.cpp camera/sun rotations
 };
 
-static Vector3 v3(char** a) { return Vector3(std::strtof(a[0], nullptr), std::strtof(a[1], nullptr), std::strtof(a[2], nullptr)); }
+static Vector3 v3(char** a) { return Vector3(num(a[0]), num(a[1]), num(a[2])); }
 
 static bool parse(int argc, char** argv, Args& a) {
     for (int i = 1; i < argc; ++i) {
@@ -77,8 +89,8 @@ static bool parse(int argc, char** argv, Args& a) {
         else if (s == "--dir") { need(3); a.dir = v3(argv + i + 1); i += 3; }
         else if (s == "--up")  { need(3); a.up  = v3(argv + i + 1); i += 3; }
         else if (s == "--sun") { need(3); a.sun = v3(argv + i + 1); i += 3; }
-        else if (s == "--fov") { need(1); a.fov = std::strtof(argv[++i], nullptr); }
-        else if (s == "--rotate") { need(2); char c = argv[i + 1][0]; a.rot_axis = c == 'x' ? 0 : c == 'y' ? 1 : 2; a.rot_deg = std::strtof(argv[i + 2], nullptr); i += 2; }
+        else if (s == "--fov") { need(1); a.fov = num(argv[++i]); }
+        else if (s == "--rotate") { need(2); char c = argv[i + 1][0]; a.rot_axis = c == 'x' ? 0 : c == 'y' ? 1 : 2; a.rot_deg = num(argv[i + 2]); i += 2; }
         else if (s == "--size") { need(2); a.W = std::strtoul(argv[i + 1], nullptr, 10); a.H = std::strtoul(argv[i + 2], nullptr, 10); i += 2; }
         else if (s == "--out") { need(1); a.out = argv[++i]; }
         else if (s == "--float") { need(1); a.fout = argv[++i]; }
@@ -88,7 +100,7 @@ static bool parse(int argc, char** argv, Args& a) {
         else if (s == "--stats") a.stats = true;
         else if (s == "--primary-only") a.primary_only = true;
         else if (s == "--proc") { need(1); a.proc = std::atoi(argv[++i]); }
-        else if (s == "--orbit") { need(5); a.orbit_axis = v3(argv + i + 1); a.orbit_step = std::strtof(argv[i + 4], nullptr); a.orbit_count = std::atoi(argv[i + 5]); i += 5; }
+        else if (s == "--orbit") { need(5); a.orbit_axis = v3(argv + i + 1); a.orbit_step = num(argv[i + 4]); a.orbit_count = std::atoi(argv[i + 5]); i += 5; }
         else if (s[0] == '-') { std::fprintf(stderr, "unknown flag %s\n", s.c_str()); return false; }
         else a.obj = s;
     }
@@ -118,12 +130,12 @@ static std::string proc_obj(int n) {
     return s;
 }
 
-struct PixelRecord {          // 40 bytes, little-endian, written for every pixel
+struct PixelRecord {          // little-endian, every pixel: 40 B (float); double: natural alignment, 72 B
     uint32_t i, j;
     int32_t  prim;            // -1 on primary miss
-    float    t, u, v;
+    Scalar   t, u, v;
     int32_t  shadow;          // 1 if the shadow ray hit something, 0 if lit, -1 if no shadow ray
-    float    r, g, b;
+    Scalar   r, g, b;
 };
 
 int main(int argc, char** argv) {
@@ -163,9 +175,10 @@ int main(int argc, char** argv) {
     if (!a.dump.empty()) {
         auto wr = [&](const std::string& suf, const void* p, size_t n) {
             std::ofstream f(a.dump + suf, std::ios::binary); f.write((const char*)p, n); };
-        wr(".tri48", triangles.data(), triangles.size() * sizeof(Triangle));
-        wr(".norm36", tri_norms.data(), tri_norms.size() * sizeof(std::array<Vector3, 3>));
-        wr(".nodes32", bvh.nodes.get(), bvh.node_count * sizeof(Bvh::Node));
+        const std::string w = sizeof(Scalar) == 8 ? "64" : "";      // .tri48 .norm36 .nodes32 | .tri96 .norm72 .nodes64
+        wr(w.empty() ? ".tri48" : ".tri96", triangles.data(), triangles.size() * sizeof(Triangle));
+        wr(w.empty() ? ".norm36" : ".norm72", tri_norms.data(), tri_norms.size() * sizeof(std::array<Vector3, 3>));
+        wr(w.empty() ? ".nodes32" : ".nodes64", bvh.nodes.get(), bvh.node_count * sizeof(Bvh::Node));
         std::vector<uint64_t> pi(bvh.primitive_indices.get(), bvh.primitive_indices.get() + triangles.size());
         wr(".prim64", pi.data(), pi.size() * 8);
     }
@@ -267,7 +280,7 @@ int main(int argc, char** argv) {
         }
         if (a.primary_only) { pixels = px2; rh = {int(loop_rays), int(loop_hits)}; }
         else mismatch = size_t(std::count_if(pixels.begin(), pixels.end(), [&, k = size_t(0)](Scalar x) mutable {
-            uint32_t p, q; Scalar y = px2[k++]; std::memcpy(&p, &x, 4); std::memcpy(&q, &y, 4); return p != q; }));
+            uint64_t p = 0, q = 0; Scalar y = px2[k++]; std::memcpy(&p, &x, sizeof x); std::memcpy(&q, &y, sizeof y); return p != q; }));
     }
 
     if (!a.records.empty()) {
@@ -297,7 +310,7 @@ int main(int argc, char** argv) {
     std::sort(times.begin(), times.end());
     double med = times.empty() ? 0.0 : times[times.size() / 2];
     double best = times.empty() ? 0.0 : times[0];
-    char h[15][16];
+    char h[15][24];
     hexf(h[9], camera.eye[0]); hexf(h[10], camera.eye[1]); hexf(h[11], camera.eye[2]);
     hexf(h[12], a.sun[0]); hexf(h[13], a.sun[1]); hexf(h[14], a.sun[2]);
     hexf(h[0], dir[0]); hexf(h[1], dir[1]); hexf(h[2], dir[2]);
