@@ -35,7 +35,9 @@ SCENE_STATS = 1
 EXPORTED_SYMBOLS = (
     "ceres_obj_load", "ceres_proc_mesh", "ceres_rotate_triangles", "ceres_bvh_build", "ceres_bvh_build_gpu",
     "ceres_bvh_build_device", "ceres_obj_load_gpu", "ceres_obj_parse_device", "ceres_rotate_triangles_device",
-    "ceres_device_free", "ceres_camera_basis",
+    "ceres_device_free", "ceres_camera_basis", "ceres_obj_load_f64", "ceres_proc_mesh_f64", "ceres_rotate_triangles_f64",
+    "ceres_bvh_build_f64", "ceres_camera_basis_f64", "ceres_orbit_cameras_f64", "ceres_scene_create_f64",
+    "ceres_render_f64", "ceres_render_records_f64",
     "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
@@ -59,6 +61,7 @@ class Tiling(ctypes.Structure):
 
 _lib = None
 _fp = ctypes.POINTER(ctypes.c_float)
+_dp = ctypes.POINTER(ctypes.c_double)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _sz = ctypes.c_size_t
@@ -106,6 +109,19 @@ def lib():
     L.ceres_device_free.argtypes = [_vp]
     L.ceres_device_free.restype = None
     L.ceres_camera_basis.argtypes = [_fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp]
+    L.ceres_obj_load_f64.argtypes = [ctypes.c_char_p, ctypes.POINTER(_dp), ctypes.POINTER(_dp), ctypes.POINTER(_sz)]
+    L.ceres_proc_mesh_f64.argtypes = [ctypes.c_int, ctypes.POINTER(_dp), ctypes.POINTER(_dp), ctypes.POINTER(_sz)]
+    L.ceres_rotate_triangles_f64.argtypes = [_dp, _sz, ctypes.c_int, ctypes.c_double]
+    L.ceres_bvh_build_f64.argtypes = [_dp, _sz, ctypes.POINTER(_u64p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p)]
+    L.ceres_camera_basis_f64.argtypes = [_dp, _dp, _dp, ctypes.c_double, _sz, _sz, _dp]
+    L.ceres_orbit_cameras_f64.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_double, _sz, _sz, _dp, ctypes.c_double,
+                                          ctypes.c_uint32, ctypes.c_int, _dp, _dp, _dp]
+    L.ceres_scene_create_f64.argtypes = [_dp, _sz, _dp, _vp, _sz, _u64p, ctypes.c_int, ctypes.c_uint32]
+    L.ceres_scene_create_f64.restype = _vp
+    L.ceres_render_f64.argtypes = [_vp, _dp, _dp, ctypes.c_int, _dp, ctypes.POINTER(ctypes.c_uint8), _sz, _sz,
+                                   ctypes.POINTER(_Stats)]
+    L.ceres_render_records_f64.argtypes = [_vp, _dp, _dp, ctypes.c_int, _sz, _sz, ctypes.POINTER(ctypes.c_int32), _dp,
+                                           ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(_Stats)]
     L.ceres_orbit_cameras.argtypes = [_fp, _fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp, ctypes.c_float,
                                       ctypes.c_uint32, ctypes.c_int, _fp, _fp, _fp]
     L.ceres_free.argtypes = [_vp]
@@ -154,16 +170,23 @@ def _take(ptr, count, dtype):
 
 
 class Camera:
-    """render.hpp:16-22 -- eye, dir, up, fov (degrees)."""
+    """render.hpp:16-22 -- eye, dir, up, fov (degrees); Camera<float> or, with dtype=np.float64,
+    Camera<double> (anim.cpp -d)."""
 
-    def __init__(self, eye, dir, up, fov):
-        self.eye = np.asarray(eye, np.float32)
-        self.dir = np.asarray(dir, np.float32)
-        self.up = np.asarray(up, np.float32)
+    def __init__(self, eye, dir, up, fov, dtype=np.float32):
+        self.dtype = np.dtype(dtype)
+        self.eye = np.asarray(eye, self.dtype)
+        self.dir = np.asarray(dir, self.dtype)
+        self.up = np.asarray(up, self.dtype)
         self.fov = float(fov)
 
     def basis(self, W, H):
         """render.hpp:91-97 on the host (libm stays on the host): {eye, dir, image_u, image_v}."""
+        if self.dtype == np.float64:
+            out = np.zeros(9, np.float64)
+            _check(lib().ceres_camera_basis_f64(_p(self.eye, ctypes.c_double), _p(self.dir, ctypes.c_double),
+                                                _p(self.up, ctypes.c_double), self.fov, W, H, _p(out, ctypes.c_double)))
+            return np.concatenate([self.eye, out])
         out = np.zeros(9, np.float32)
         _check(lib().ceres_camera_basis(_p(self.eye, ctypes.c_float), _p(self.dir, ctypes.c_float),
                                         _p(self.up, ctypes.c_float), self.fov, W, H, _p(out, ctypes.c_float)))
@@ -171,21 +194,29 @@ class Camera:
 
 
 class Mesh:
-    """Triangles (n x 12 f32 = bvh::Triangle<float>) and per-triangle vertex normals (n x 9)."""
+    """Triangles (n x 12 = bvh::Triangle<S>) and per-triangle vertex normals (n x 9); S = float
+    (f32 arrays) or double (f64 arrays, render<double>)."""
 
     def __init__(self, tri, norm):
-        self.tri = np.ascontiguousarray(tri, np.float32).reshape(-1, 12)
-        self.norm = np.ascontiguousarray(norm, np.float32).reshape(-1, 9)
+        dt = np.float64 if np.asarray(tri).dtype == np.float64 else np.float32
+        self.tri = np.ascontiguousarray(tri, dt).reshape(-1, 12)
+        self.norm = np.ascontiguousarray(norm, dt).reshape(-1, 9)
+
+    @property
+    def f64(self):
+        return self.tri.dtype == np.float64
 
     def __len__(self):
         return self.tri.shape[0]
 
 
 class Bvh:
-    """bvh::Bvh<float>: nodes (m x 8 u32 = Node) and primitive_indices (u64)."""
+    """bvh::Bvh<S>: nodes (m x 8 u32 = Node<float>, or m x 8 u64 = Node<double>: 6 doubles +
+    2 u64) and primitive_indices (u64)."""
 
     def __init__(self, nodes, prim):
-        self.nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
+        dt = np.uint64 if np.asarray(nodes).dtype == np.uint64 else np.uint32
+        self.nodes = np.ascontiguousarray(nodes, dt).reshape(-1, 8)
         self.prim = np.ascontiguousarray(prim, np.uint64)
 
 
@@ -194,6 +225,21 @@ def load_obj(path):
     _check(lib().ceres_obj_load(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt)))
     c = cnt.value
     return Mesh(_take(t, c * 12, np.float32).reshape(c, 12), _take(n, c * 9, np.float32).reshape(c, 9))
+
+
+def load_obj_f64(path):
+    """obj::load_from_file<double> (anim.cpp -d): strtof coordinates widened to double."""
+    t, n, cnt = _dp(), _dp(), _sz()
+    _check(lib().ceres_obj_load_f64(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt)))
+    c = cnt.value
+    return Mesh(_take(t, c * 12, np.float64).reshape(c, 12), _take(n, c * 9, np.float64).reshape(c, 9))
+
+
+def proc_mesh_f64(n):
+    t, nn, cnt = _dp(), _dp(), _sz()
+    _check(lib().ceres_proc_mesh_f64(int(n), ctypes.byref(t), ctypes.byref(nn), ctypes.byref(cnt)))
+    c = cnt.value
+    return Mesh(_take(t, c * 12, np.float64).reshape(c, 12), _take(nn, c * 9, np.float64).reshape(c, 9))
 
 
 def load_obj_gpu(path, device=0):
@@ -231,11 +277,19 @@ def proc_mesh(n):
 
 def rotate_triangles(mesh, axis, degrees):
     ax = {"x": 0, "y": 1, "z": 2}[axis] if isinstance(axis, str) else int(axis)
-    _check(lib().ceres_rotate_triangles(_p(mesh.tri, ctypes.c_float), len(mesh), ax, float(degrees)))
+    if mesh.f64:
+        _check(lib().ceres_rotate_triangles_f64(_p(mesh.tri, ctypes.c_double), len(mesh), ax, float(degrees)))
+    else:
+        _check(lib().ceres_rotate_triangles(_p(mesh.tri, ctypes.c_float), len(mesh), ax, float(degrees)))
     return mesh
 
 
 def build_bvh(mesh):
+    if mesh.f64:
+        nodes, prim, m = _u64p(), _u64p(), _sz()
+        _check(lib().ceres_bvh_build_f64(_p(mesh.tri, ctypes.c_double), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
+                                         ctypes.byref(prim)))
+        return Bvh(_take(nodes, m.value * 8, np.uint64).reshape(-1, 8), _take(prim, len(mesh), np.uint64))
     nodes, prim, m = _u32p(), _u64p(), _sz()
     _check(lib().ceres_bvh_build(_p(mesh.tri, ctypes.c_float), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
                                  ctypes.byref(prim)))
@@ -264,10 +318,17 @@ class Scene:
         L = lib()
         if _handle is not None:                      # Scene.from_device
             self._h, self.device, self.n_tri = _handle
+            self.f64 = False
             return
-        self._h = L.ceres_scene_create(_p(mesh.tri, ctypes.c_float), len(mesh), _p(mesh.norm, ctypes.c_float),
-                                       bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0],
-                                       _p(bvh.prim, ctypes.c_uint64), int(device), SCENE_STATS if stats else 0)
+        self.f64 = mesh.f64
+        if self.f64:
+            self._h = L.ceres_scene_create_f64(_p(mesh.tri, ctypes.c_double), len(mesh), _p(mesh.norm, ctypes.c_double),
+                                               bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0],
+                                               _p(bvh.prim, ctypes.c_uint64), int(device), SCENE_STATS if stats else 0)
+        else:
+            self._h = L.ceres_scene_create(_p(mesh.tri, ctypes.c_float), len(mesh), _p(mesh.norm, ctypes.c_float),
+                                           bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0],
+                                           _p(bvh.prim, ctypes.c_uint64), int(device), SCENE_STATS if stats else 0)
         if not self._h:
             raise CeresError("ceres_scene_create: " + L.ceres_last_error().decode())
         self.device = device
@@ -300,28 +361,31 @@ class Scene:
             pass
 
     def render(self, basis12, sun, W, H, mode=MODE_FULL, want_pixels=True, want_rgb8=True):
-        """ceres_render_f32: host buffers out; returns (pixels [H*W*3] f32 | None, rgb8 | None, stats dict)."""
-        b = np.ascontiguousarray(basis12, np.float32)
-        s = np.ascontiguousarray(sun, np.float32)
-        px = np.empty(3 * W * H, np.float32) if want_pixels else None
+        """ceres_render_f32 / ceres_render_f64 (double scenes): host buffers out; returns
+        (pixels [H*W*3] f32|f64 | None, rgb8 | None, stats dict)."""
+        dt, ct = (np.float64, ctypes.c_double) if self.f64 else (np.float32, ctypes.c_float)
+        b = np.ascontiguousarray(basis12, dt)
+        s = np.ascontiguousarray(sun, dt)
+        px = np.empty(3 * W * H, dt) if want_pixels else None
         rgb = np.empty(3 * W * H, np.uint8) if want_rgb8 else None
         st = _Stats()
-        _check(lib().ceres_render_f32(self._h, _p(b, ctypes.c_float), _p(s, ctypes.c_float), int(mode),
-                                      _p(px, ctypes.c_float), _p(rgb, ctypes.c_uint8), W, H, ctypes.byref(st)))
+        fn = lib().ceres_render_f64 if self.f64 else lib().ceres_render_f32
+        _check(fn(self._h, _p(b, ct), _p(s, ct), int(mode), _p(px, ct), _p(rgb, ctypes.c_uint8), W, H, ctypes.byref(st)))
         return px, rgb, dict(rays=st.rays, hits=st.hits, primary_rays=st.primary_rays, shadow_rays=st.shadow_rays,
                              node_pairs=st.node_pairs, tri_tests=st.tri_tests, ms=st.ms)
 
     def records(self, basis12, sun, W, H, mode=MODE_FULL):
-        """ceres_render_records: per-pixel (prim [W*H] i32, tuv [W*H,3] f32, shadow [W*H] i8, stats)."""
-        b = np.ascontiguousarray(basis12, np.float32)
-        s = np.ascontiguousarray(sun, np.float32)
+        """ceres_render_records(_f64): per-pixel (prim [W*H] i32, tuv [W*H,3] f32|f64, shadow [W*H] i8, stats)."""
+        dt, ct = (np.float64, ctypes.c_double) if self.f64 else (np.float32, ctypes.c_float)
+        b = np.ascontiguousarray(basis12, dt)
+        s = np.ascontiguousarray(sun, dt)
         prim = np.empty(W * H, np.int32)
-        tuv = np.empty(3 * W * H, np.float32)
+        tuv = np.empty(3 * W * H, dt)
         sh = np.empty(W * H, np.int8)
         st = _Stats()
-        _check(lib().ceres_render_records(self._h, _p(b, ctypes.c_float), _p(s, ctypes.c_float), int(mode), W, H,
-                                          _p(prim, ctypes.c_int32), _p(tuv, ctypes.c_float), _p(sh, ctypes.c_int8),
-                                          ctypes.byref(st)))
+        fn = lib().ceres_render_records_f64 if self.f64 else lib().ceres_render_records
+        _check(fn(self._h, _p(b, ct), _p(s, ct), int(mode), W, H, _p(prim, ctypes.c_int32), _p(tuv, ct),
+                  _p(sh, ctypes.c_int8), ctypes.byref(st)))
         return prim, tuv.reshape(-1, 3), sh, dict(rays=st.rays, hits=st.hits, node_pairs=st.node_pairs,
                                                   tri_tests=st.tri_tests)
 
@@ -396,6 +460,25 @@ def pose(cfg, frame=0):
     return Camera(b[n, :3], d3[n], cfg["up"], cfg["fov"]), s3[n].copy()
 
 
+def pose_f64(cfg):
+    """(Camera<double>, sun) of a config: its values as double literals (anim.cpp writes its
+    camera as double literals), orbited with Transform<double> when the config has "orbit"."""
+    cam = Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"], dtype=np.float64)
+    sun = np.asarray(cfg["sun"], np.float64)
+    if not cfg.get("orbit"):
+        return cam, sun
+    (axis, step, n) = cfg["orbit"]
+    b = np.zeros((n + 1, 12), np.float64)
+    s3 = np.zeros((n + 1, 3), np.float64)
+    d3 = np.zeros((n + 1, 3), np.float64)
+    ax = np.asarray(axis, np.float64)
+    _check(lib().ceres_orbit_cameras_f64(_p(cam.eye, ctypes.c_double), _p(cam.dir, ctypes.c_double),
+                                         _p(cam.up, ctypes.c_double), _p(sun, ctypes.c_double), cam.fov, cfg["W"],
+                                         cfg["H"], _p(ax, ctypes.c_double), float(step), n + 1, 0,
+                                         _p(b, ctypes.c_double), _p(s3, ctypes.c_double), _p(d3, ctypes.c_double)))
+    return Camera(b[n, :3], d3[n], cfg["up"], cfg["fov"], dtype=np.float64), s3[n].copy()
+
+
 def assemble_rgb8(d_gathered, rank_stride, d_out, frames, W, H, row_block, world, stream=0):
     """ceres_assemble_rgb8 (device pointers): rank-major gathered batch rows -> F PPM bodies."""
     _check(lib().ceres_assemble_rgb8(d_gathered, rank_stride, d_out, int(frames), W, H, int(row_block), int(world),
@@ -418,9 +501,17 @@ def row_map(H, row_block, world):
     return out
 
 
-def prepare(cfg):
+def prepare(cfg, f64=False):
     """Scene prep of the reference app for a config (configs.CONFIGS entry): mesh, bvh, camera
-    (at the config's orbit pose; pose(cfg) also gives the sun)."""
+    (at the config's orbit pose; pose(cfg) also gives the sun).  f64: the render<double>
+    pipeline (anim.cpp -d) -- double mesh / BVH, camera at the config's pose in double."""
+    if f64:
+        mesh = proc_mesh_f64(cfg["proc"]) if cfg.get("proc") else load_obj_f64(configs.obj_path(cfg))
+        if len(mesh) == 0:
+            raise CeresError("The given scene is empty or cannot be loaded")
+        if cfg.get("rotate"):
+            rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1])
+        return mesh, build_bvh(mesh), pose_f64(cfg)[0]
     mesh = proc_mesh(cfg["proc"]) if cfg.get("proc") else load_obj(configs.obj_path(cfg))
     if len(mesh) == 0:
         raise CeresError("The given scene is empty or cannot be loaded")

@@ -42,6 +42,22 @@ struct alignas(16) SiblingPair {
 };
 static_assert(sizeof(SiblingPair) == 64, "SiblingPair");
 
+// Double precision (render<double>, anim.cpp -d): the reference's Bvh<double>::Node (64 B),
+// Triangle<double> (96 B) and the sibling-pair record with double bounds (112 B = 7 x 16 B).
+struct RefNode64 {
+    double bounds[6];
+    uint64_t primitive_count;
+    uint64_t first_child_or_primitive;
+};
+static_assert(sizeof(RefNode64) == 64, "RefNode64");
+struct Tri96 { double p0[3], e1[3], e2[3], n[3]; };
+static_assert(sizeof(Tri96) == 96, "Tri96");
+struct alignas(16) SiblingPair64 {
+    double lb[6], rb[6];
+    uint32_t lcount, lfirst, rcount, rfirst;
+};
+static_assert(sizeof(SiblingPair64) == 112, "SiblingPair64");
+
 // Shadow-ray BVH4 record (build_shadow_bvh4, scene_host.cpp): 4 child boxes as SoA float4
 // rows, then per-child count (0 inner -> first = Node4 index; kNode4Empty unused slot;
 // else leaf of `count` triangles from leaf slot `first`).  128 B = one L2 line.
@@ -130,5 +146,8 @@ int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, siz
                  uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first);
 int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>& out, uint32_t& stack_bound,
                       uint32_t& not_collapsed);
+int relayout_bvh64(const RefNode64* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri96* tris,
+                   std::vector<SiblingPair64>& pairs, std::vector<Tri96>& leaf_tris, std::vector<uint32_t>& orig,
+                   uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first);
 
 }  // namespace ceres

@@ -879,39 +879,7 @@ __global__ __launch_bounds__(256) void ceres_assemble(const uint8_t* __restrict_
 // =====================================================================================
 using namespace ceres;
 
-struct ceres_scene {
-    int device = 0;
-    uint32_t flags = 0;
-    size_t n_tri = 0, n_pairs = 0;
-    uint32_t depth = 0, stack_entries = 1, root_leaf_count = 0, root_leaf_first = 0;
-    uint32_t shadow_stack_entries = 1;
-    size_t n_nodes4 = 0;
-    SiblingPair* d_pairs = nullptr;
-    Node4* d_nodes4 = nullptr;
-    uint32_t* d_order = nullptr;          // fused kernel tile order, for order_key
-    size_t order_cap = 0;
-    uint64_t order_key = ~0ull;
-    Tri48* d_tris = nullptr;
-    uint32_t* d_orig = nullptr;
-    float* d_norms = nullptr;
-    Shard* d_shards = nullptr;
-    bool shards_dirty = true;          // shards not known to be zero (see ceres_render_batch)
-    uint64_t* d_counters = nullptr;
-    ShadowJob* d_jobs = nullptr;
-    size_t jobs_cap = 0;
-    float* d_pixels = nullptr;
-    uint8_t* d_rgb8 = nullptr;
-    size_t px_cap = 0;
-    hipStream_t stream = nullptr;
-    int num_cus = 256;
-    unsigned long long* d_wave_log = nullptr;   // stats scenes: per-wave diagnostic records
-    size_t wave_log_waves = 0, last_grid_waves = 0;
-    // optional per-kernel device timing (bench.py roofline leg)
-    bool timing = false;
-    std::vector<hipEvent_t> ev_pool;
-    std::vector<hipEvent_t> ev_used;   // triples: start, after primary, after shadow
-    std::vector<char> ev_fused;        // per triple: one ceres_fused launch (no separate shadow kernel)
-};
+#include "scene_internal.hpp"
 
 namespace {
 
@@ -924,9 +892,12 @@ namespace {
 template <typename T>
 void dfree(T*& p) { if (p) { (void)hipFree(p); p = nullptr; } }
 
-void scene_release(ceres_scene* s) {
+}  // namespace
+
+void ceres::scene_release(ceres_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
+    dfree(s->d_pairs64); dfree(s->d_tris64); dfree(s->d_norms64);
     dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_order); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
@@ -935,6 +906,8 @@ void scene_release(ceres_scene* s) {
     if (s->stream) (void)hipStreamDestroy(s->stream);
     s->stream = nullptr;
 }
+
+namespace {
 
 size_t local_rows_of(size_t H, uint32_t rb, uint32_t rank, uint32_t world) {
     const size_t nblocks = (H + rb - 1) / rb;
@@ -998,6 +971,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
            const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream,
            int32_t* d_rec_prim = nullptr, float* d_rec_tuv = nullptr, int8_t* d_rec_shadow = nullptr) {
     if (!s || !basis12 || !sun) return set_error(CERES_EINVAL, "render: null argument");
+    if (s->f64) return set_error(CERES_EINVAL, "scene is double precision: use ceres_render_f64");
     if (frames == 0 || frames > uint32_t(kMaxFrames))
         return set_error(CERES_EINVAL, "render: %u frames per batch (1..%d)", frames, kMaxFrames);
     if (mode != CERES_MODE_FULL && mode != CERES_MODE_PRIMARY) return set_error(CERES_EINVAL, "render: bad mode %d", mode);

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 #ifdef _OPENMP
@@ -28,51 +29,63 @@
 namespace ceres {
 namespace {
 
-struct Vec { float x, y, z; };
-inline float comp(const Vec& v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
-inline Vec operator+(Vec a, Vec b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
-inline Vec operator-(Vec a, Vec b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
-inline Vec scale(Vec a, float s) { return {a.x * s, a.y * s, a.z * s}; }
-inline float vdot(Vec a, Vec b) { float s = a.x * b.x; s += a.y * b.y; s += a.z * b.z; return s; }
-inline Vec vcross(Vec a, Vec b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
-inline Vec vnormalize(Vec v) { float inv = 1.0f / std::sqrt(vdot(v, v)); return scale(v, inv); }
+// Scalar-generic vector (S = float: render<float>, static.cpp; S = double: render<double>,
+// anim.cpp -d).  Every operation keeps the reference's order (vector.hpp:136-153).
+template <class S> struct V3 { S x, y, z; };
+template <class S> inline S comp(const V3<S>& v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+template <class S> inline V3<S> operator+(V3<S> a, V3<S> b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+template <class S> inline V3<S> operator-(V3<S> a, V3<S> b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+template <class S> inline V3<S> scale(V3<S> a, S s) { return {a.x * s, a.y * s, a.z * s}; }
+template <class S> inline S vdot(V3<S> a, V3<S> b) { S s = a.x * b.x; s += a.y * b.y; s += a.z * b.z; return s; }
+template <class S> inline V3<S> vcross(V3<S> a, V3<S> b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+template <class S> inline V3<S> vnormalize(V3<S> v) { S inv = S(1) / std::sqrt(vdot(v, v)); return scale(v, inv); }
+using Vec = V3<float>;
 
-inline Tri48 tri_from_points(Vec p0, Vec p1, Vec p2) {       // Triangle ctor, triangle.hpp:30-34
-    Vec e1 = p0 - p1, e2 = p2 - p0, n = vcross(e1, e2);
-    return Tri48{{p0.x, p0.y, p0.z}, {e1.x, e1.y, e1.z}, {e2.x, e2.y, e2.z}, {n.x, n.y, n.z}};
+template <class S> struct TriT { S p0[3], e1[3], e2[3], n[3]; };     // bvh::Triangle<S>
+static_assert(sizeof(TriT<float>) == sizeof(Tri48), "Tri48");
+template <class S> struct NodeT;                                     // bvh::Bvh<S>::Node (bvh.hpp:25-30)
+template <> struct NodeT<float> { float bounds[6]; uint32_t primitive_count, first_child_or_primitive; };
+template <> struct NodeT<double> { double bounds[6]; uint64_t primitive_count, first_child_or_primitive; };
+static_assert(sizeof(NodeT<float>) == 32 && sizeof(NodeT<double>) == 64, "Node");
+
+template <class S> inline TriT<S> tri_from_points(V3<S> p0, V3<S> p1, V3<S> p2) {   // Triangle ctor, triangle.hpp:30-34
+    V3<S> e1 = p0 - p1, e2 = p2 - p0, n = vcross(e1, e2);
+    return TriT<S>{{p0.x, p0.y, p0.z}, {e1.x, e1.y, e1.z}, {e2.x, e2.y, e2.z}, {n.x, n.y, n.z}};
 }
-inline Vec P0(const Tri48& t) { return {t.p0[0], t.p0[1], t.p0[2]}; }
-inline Vec E1(const Tri48& t) { return {t.e1[0], t.e1[1], t.e1[2]}; }
-inline Vec E2(const Tri48& t) { return {t.e2[0], t.e2[1], t.e2[2]}; }
-inline Vec N(const Tri48& t) { return {t.n[0], t.n[1], t.n[2]}; }
+template <class S> inline V3<S> P0(const TriT<S>& t) { return {t.p0[0], t.p0[1], t.p0[2]}; }
+template <class S> inline V3<S> E1(const TriT<S>& t) { return {t.e1[0], t.e1[1], t.e1[2]}; }
+template <class S> inline V3<S> E2(const TriT<S>& t) { return {t.e2[0], t.e2[1], t.e2[2]}; }
+template <class S> inline V3<S> N(const TriT<S>& t) { return {t.n[0], t.n[1], t.n[2]}; }
 
 // ------------------------------------------------------------------ mesh assembly
 // Accumulates fan-triangulated faces and area-weighted (un-normalised, left-handed) face
-// normals per vertex in face order, exactly like obj_norms.hpp:84-115.
+// normals per vertex in face order, exactly like obj_norms.hpp:84-115.  Vertex coordinates
+// are floats from strtof (obj_norms.hpp:78-80), widened for S = double.
+template <class S>
 struct MeshBuilder {
-    std::vector<Vec> verts, vn;
-    std::vector<Tri48> tris;
+    std::vector<V3<S>> verts, vn;
+    std::vector<TriT<S>> tris;
     std::vector<uint32_t> corner;     // 3 vertex ids per triangle
 
-    void add_vertex(Vec v) { verts.push_back(v); vn.push_back({0.f, 0.f, 0.f}); }
+    void add_vertex(V3<S> v) { verts.push_back(v); vn.push_back({S(0), S(0), S(0)}); }
     void add_triangle(size_t a, size_t b, size_t c) {
         tris.push_back(tri_from_points(verts[a], verts[b], verts[c]));
-        Vec n = N(tris.back());
+        V3<S> n = N(tris.back());
         vn[a] = vn[a] + n; vn[b] = vn[b] + n; vn[c] = vn[c] + n;
         corner.push_back(uint32_t(a)); corner.push_back(uint32_t(b)); corner.push_back(uint32_t(c));
     }
-    int finish(float** tri48, float** norm36, size_t* n_tri) {
+    int finish(S** tri, S** norm, size_t* n_tri) {
         for (auto& n : vn) n = vnormalize(n);                // obj_norms.hpp:109-111
         const size_t nt = tris.size();
         *n_tri = nt;
-        *tri48 = static_cast<float*>(std::malloc(std::max<size_t>(1, nt * 48)));
-        *norm36 = static_cast<float*>(std::malloc(std::max<size_t>(1, nt * 36)));
-        if (!*tri48 || !*norm36) { std::free(*tri48); std::free(*norm36); *tri48 = *norm36 = nullptr; return set_error(CERES_ENOMEM, "out of host memory"); }
-        std::memcpy(*tri48, tris.data(), nt * 48);
-        float* o = *norm36;
+        *tri = static_cast<S*>(std::malloc(std::max<size_t>(1, nt * sizeof(TriT<S>))));
+        *norm = static_cast<S*>(std::malloc(std::max<size_t>(1, nt * 9 * sizeof(S))));
+        if (!*tri || !*norm) { std::free(*tri); std::free(*norm); *tri = *norm = nullptr; return set_error(CERES_ENOMEM, "out of host memory"); }
+        std::memcpy(*tri, tris.data(), nt * sizeof(TriT<S>));
+        S* o = *norm;
         for (size_t t = 0; t < nt; ++t)
             for (int k = 0; k < 3; ++k) {
-                const Vec& v = vn[corner[3 * t + k]];
+                const V3<S>& v = vn[corner[3 * t + k]];
                 o[9 * t + 3 * k] = v.x; o[9 * t + 3 * k + 1] = v.y; o[9 * t + 3 * k + 2] = v.z;
             }
         return CERES_OK;
@@ -102,7 +115,8 @@ inline bool face_index(char** cursor, long* out) {
     return true;
 }
 
-int parse_obj(const char* data, size_t len, MeshBuilder& mb) {
+template <class S>
+int parse_obj(const char* data, size_t len, MeshBuilder<S>& mb) {
     constexpr size_t kMaxLine = 1024;                       // istream::getline(line, 1024)
     char line[kMaxLine];
     size_t pos = 0;
@@ -121,7 +135,7 @@ int parse_obj(const char* data, size_t len, MeshBuilder& mb) {
             float x = std::strtof(q, &q);
             float y = std::strtof(q, &q);
             float z = std::strtof(q, &q);
-            mb.add_vertex({x, y, z});
+            mb.add_vertex({S(x), S(y), S(z)});
         } else if (p[0] == 'f' && std::isspace(static_cast<unsigned char>(p[1]))) {
             char* q = p + 2;
             size_t first = 0, prev = 0;
@@ -140,37 +154,104 @@ int parse_obj(const char* data, size_t len, MeshBuilder& mb) {
     return CERES_OK;
 }
 
+template <class S>
+int obj_load(const char* path, S** tri, S** norm, size_t* n_tri) {
+    if (!path || !tri || !norm || !n_tri) return set_error(CERES_EINVAL, "ceres_obj_load: null argument");
+    *tri = *norm = nullptr; *n_tri = 0;
+    std::vector<char> buf;
+    if (FILE* f = std::fopen(path, "rb")) {
+        char chunk[1 << 16];
+        size_t got;
+        while ((got = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + got);
+        std::fclose(f);
+    }   // unreadable file: empty mesh, like obj_norms.hpp:123-126
+    MeshBuilder<S> mb;
+    int rc = parse_obj(buf.data(), buf.size(), mb);
+    if (rc) return rc;
+    return mb.finish(tri, norm, n_tri);
+}
+
+template <class S>
+int proc_mesh(int n, S** tri, S** norm, size_t* n_tri) {
+    if (n < 2 || !tri || !norm || !n_tri) return set_error(CERES_EINVAL, "ceres_proc_mesh: need n >= 2");
+    MeshBuilder<S> mb;
+    const size_t nv = size_t(n) * size_t(n);
+    mb.verts.reserve(nv); mb.vn.reserve(nv);
+    mb.tris.reserve(2 * size_t(n - 1) * size_t(n - 1));
+    mb.corner.reserve(6 * size_t(n - 1) * size_t(n - 1));
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) {
+            double x = double(i) / double(n - 1), y = double(j) / double(n - 1);
+            double z = 0.05 * (std::sin(40.0 * x) + std::cos(37.0 * y)) + 0.01 * std::sin(400.0 * x + 300.0 * y);
+            mb.add_vertex({S(float(x)), S(float(y)), S(float(z))});   // the OBJ-text values (%.9g floats)
+        }
+    for (int j = 0; j + 1 < n; ++j)
+        for (int i = 0; i + 1 < n; ++i) {
+            size_t a = size_t(j) * n + i, b = a + 1, c = a + n + 1, d = a + n;
+            mb.add_triangle(a, b, c);
+            mb.add_triangle(a, c, d);
+        }
+    return mb.finish(tri, norm, n_tri);
+}
+
+template <class S>
+int rotate_triangles(S* tri, size_t n_tri, int axis, S degrees) {         // render.hpp:24-44
+    if ((!tri && n_tri) || axis < 0 || axis > 2) return set_error(CERES_EINVAL, "ceres_rotate_triangles: bad argument");
+    const S pi = S(3.14159265359);
+    const S c = std::cos(degrees * pi / S(180));
+    const S s = std::sin(degrees * pi / S(180));
+    auto rot = [&](V3<S> p) -> V3<S> {
+        if (axis == 0) return {p.x, p.y * c - p.z * s, p.y * s + p.z * c};
+        if (axis == 1) return {p.x * c + p.z * s, p.y, -p.x * s + p.z * c};
+        return {p.x * c - p.y * s, p.x * s + p.y * c, p.z};
+    };
+    TriT<S>* t = reinterpret_cast<TriT<S>*>(tri);
+    #pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n_tri; ++i) {
+        const V3<S> p0 = P0(t[i]), p1 = P0(t[i]) - E1(t[i]), p2 = P0(t[i]) + E2(t[i]);   // p1(), p2()
+        t[i] = tri_from_points(rot(p0), rot(p1), rot(p2));
+    }
+    return CERES_OK;
+}
+
 // ------------------------------------------------------------------ binned SAH BVH
 // Same split rules as BinnedSahBuilder<Bvh,16> so the topology (and leaf order) is the
-// reference's: 16 bins per axis on centroids (bin index by fmaf, :144-147), SAH sweeps
+// reference's: 16 bins per axis on centroids (bin index by fma, :144-147), SAH sweeps
 // (:89-114), axis choice (:170-174), leaf test with traversal_cost 1 (:179), 0.4-quantile
 // fallback above 16 primitives (:180-196), std::partition (:199-201), child boxes from the
 // bins (:216-224, including its use of the pre-fallback split count for the left box).
 // Subtrees above 1024 primitives become OpenMP tasks (top_down_builder.hpp:63-66).
 constexpr size_t kBins = 16, kMaxDepth = 64, kMaxLeaf = 16, kTaskThreshold = 1024;
 
-struct Box { Vec lo, hi; };
-inline Box empty_box() { return {{FLT_MAX, FLT_MAX, FLT_MAX}, {-FLT_MAX, -FLT_MAX, -FLT_MAX}}; }
-inline float lesser(float a, float b) { return (b < a) ? b : a; }
-inline float greater(float a, float b) { return (a < b) ? b : a; }
-inline void grow(Box& a, const Box& b) {
+template <class S> struct BoxT { V3<S> lo, hi; };
+template <class S> inline BoxT<S> empty_box() {
+    const S m = std::numeric_limits<S>::max();
+    return {{m, m, m}, {-m, -m, -m}};
+}
+template <class S> inline S lesser(S a, S b) { return (b < a) ? b : a; }
+template <class S> inline S greater(S a, S b) { return (a < b) ? b : a; }
+template <class S> inline void grow(BoxT<S>& a, const BoxT<S>& b) {
     a.lo = {lesser(a.lo.x, b.lo.x), lesser(a.lo.y, b.lo.y), lesser(a.lo.z, b.lo.z)};
     a.hi = {greater(a.hi.x, b.hi.x), greater(a.hi.y, b.hi.y), greater(a.hi.z, b.hi.z)};
 }
-inline float box_half_area(const Box& b) { Vec d = b.hi - b.lo; return (d.x + d.y) * d.z + d.x * d.y; }
+template <class S> inline S box_half_area(const BoxT<S>& b) { V3<S> d = b.hi - b.lo; return (d.x + d.y) * d.z + d.x * d.y; }
 
+template <class S>
 struct SahBuild {
-    RefNode* nodes;
+    using Node = NodeT<S>;
+    using Box = BoxT<S>;
+    using Vs = V3<S>;
+    Node* nodes;
     size_t* prim;
     const Box* boxes;
-    const Vec* centers;
+    const Vs* centers;
     std::atomic<size_t> node_count{1};
 
-    static void store_box(RefNode& n, const Box& b) {
+    static void store_box(Node& n, const Box& b) {
         n.bounds[0] = b.lo.x; n.bounds[1] = b.hi.x; n.bounds[2] = b.lo.y;
         n.bounds[3] = b.hi.y; n.bounds[4] = b.lo.z; n.bounds[5] = b.hi.z;
     }
-    static Box load_box(const RefNode& n) {
+    static Box load_box(const Node& n) {
         return {{n.bounds[0], n.bounds[2], n.bounds[4]}, {n.bounds[1], n.bounds[3], n.bounds[5]}};
     }
 
@@ -178,35 +259,35 @@ struct SahBuild {
 
     // split one node; returns false for a leaf
     bool split(const Task& t, Task& a, Task& b) {
-        struct Bin { Box box; size_t count; float right; };
+        struct Bin { Box box; size_t count; S right; };
         Bin bins[3][kBins];
-        RefNode& node = nodes[t.node];
+        Node& node = nodes[t.node];
         const size_t n = t.end - t.begin;
-        auto make_leaf = [&] { node.first_child_or_primitive = uint32_t(t.begin); node.primitive_count = uint32_t(n); return false; };
+        auto make_leaf = [&] { node.first_child_or_primitive = t.begin; node.primitive_count = n; return false; };
         if (n <= 1 || t.depth >= kMaxDepth) return make_leaf();
         const Box bb = load_box(node);
-        const Vec diag = bb.hi - bb.lo;
-        const Vec c2b = scale(Vec{1.0f / diag.x, 1.0f / diag.y, 1.0f / diag.z}, float(kBins));
-        const Vec off = {(-bb.lo.x) * c2b.x, (-bb.lo.y) * c2b.y, (-bb.lo.z) * c2b.z};
-        auto bin_index = [&](const Vec& c, int axis) -> size_t {
-            float f = std::fmaf(comp(c, axis), comp(c2b, axis), comp(off, axis));
-            return std::min(kBins - 1, size_t(std::max(0.0f, f)));
+        const Vs diag = bb.hi - bb.lo;
+        const Vs c2b = scale(Vs{S(1) / diag.x, S(1) / diag.y, S(1) / diag.z}, S(kBins));
+        const Vs off = {(-bb.lo.x) * c2b.x, (-bb.lo.y) * c2b.y, (-bb.lo.z) * c2b.z};
+        auto bin_index = [&](const Vs& c, int axis) -> size_t {
+            S f = std::fma(comp(c, axis), comp(c2b, axis), comp(off, axis));
+            return std::min(kBins - 1, size_t(std::max(S(0), f)));
         };
-        for (auto& row : bins) for (auto& bin : row) { bin.box = empty_box(); bin.count = 0; bin.right = 0.f; }
+        for (auto& row : bins) for (auto& bin : row) { bin.box = empty_box<S>(); bin.count = 0; bin.right = S(0); }
         for (size_t i = t.begin; i < t.end; ++i) {
             const size_t p = prim[i];
             for (int axis = 0; axis < 3; ++axis) { Bin& bin = bins[axis][bin_index(centers[p], axis)]; bin.count++; grow(bin.box, boxes[p]); }
         }
-        float best_cost[3]; size_t best_split[3];
+        S best_cost[3]; size_t best_split[3];
         for (int axis = 0; axis < 3; ++axis) {
             Bin* row = bins[axis];
-            Box acc = empty_box(); size_t cnt = 0;
-            for (size_t i = kBins - 1; i > 0; --i) { grow(acc, row[i].box); cnt += row[i].count; row[i].right = box_half_area(acc) * cnt; }
-            acc = empty_box(); cnt = 0;
-            best_cost[axis] = FLT_MAX; best_split[axis] = kBins;
+            Box acc = empty_box<S>(); size_t cnt = 0;
+            for (size_t i = kBins - 1; i > 0; --i) { grow(acc, row[i].box); cnt += row[i].count; row[i].right = box_half_area(acc) * S(cnt); }
+            acc = empty_box<S>(); cnt = 0;
+            best_cost[axis] = std::numeric_limits<S>::max(); best_split[axis] = kBins;
             for (size_t i = 0; i + 1 < kBins; ++i) {
                 grow(acc, row[i].box); cnt += row[i].count;
-                float cost = box_half_area(acc) * cnt + row[i + 1].right;
+                S cost = box_half_area(acc) * S(cnt) + row[i + 1].right;
                 if (cost < best_cost[axis]) { best_cost[axis] = cost; best_split[axis] = i + 1; }
             }
         }
@@ -214,7 +295,7 @@ struct SahBuild {
         if (best_cost[0] > best_cost[1]) axis = 1;
         if (best_cost[axis] > best_cost[2]) axis = 2;
         size_t split_at = best_split[axis];
-        const float leaf_cost = box_half_area(bb) * (n - 1.0f);   // traversal_cost = 1
+        const S leaf_cost = box_half_area(bb) * (S(n) - S(1));   // traversal_cost = 1
         if (best_split[axis] == kBins || best_cost[axis] >= leaf_cost) {
             if (n <= kMaxLeaf) return make_leaf();
             // largest_axis (bounding_box.hpp:53-59), then the 0.4 quantile of the bin counts
@@ -231,9 +312,9 @@ struct SahBuild {
         const size_t m = size_t(mid - prim);
         if (m <= t.begin || m >= t.end) return make_leaf();
         const size_t child = node_count.fetch_add(2);
-        node.first_child_or_primitive = uint32_t(child);
+        node.first_child_or_primitive = child;
         node.primitive_count = 0;
-        Box lb = empty_box(), rb = empty_box();
+        Box lb = empty_box<S>(), rb = empty_box<S>();
         for (size_t i = 0; i < best_split[axis]; ++i) grow(lb, bins[axis][i].box);
         for (size_t i = split_at; i < kBins; ++i) grow(rb, bins[axis][i].box);
         store_box(nodes[child], lb);
@@ -261,13 +342,110 @@ struct SahBuild {
     }
 };
 
+template <class S>
+int bvh_build(const S* tri, size_t n_tri, NodeT<S>** nodes_out, size_t* n_nodes, uint64_t** prim64) {
+    if (!tri || !nodes_out || !n_nodes || !prim64) return set_error(CERES_EINVAL, "ceres_bvh_build: null argument");
+    if (n_tri == 0) return set_error(CERES_EINVAL, "The given scene is empty or cannot be loaded");
+    if (n_tri > 0x7fffffffu) return set_error(CERES_EUNSUPPORTED, "more than 2^31 triangles");
+    const TriT<S>* t = reinterpret_cast<const TriT<S>*>(tri);
+    std::vector<BoxT<S>> boxes(n_tri);
+    std::vector<V3<S>> centers(n_tri);
+    #pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n_tri; ++i) {                   // Triangle::bounding_box / center, triangle.hpp:39-48
+        const V3<S> p0 = P0(t[i]), p1 = P0(t[i]) - E1(t[i]), p2 = P0(t[i]) + E2(t[i]);
+        BoxT<S> b{p0, p0};
+        grow(b, BoxT<S>{p1, p1});
+        grow(b, BoxT<S>{p2, p2});
+        boxes[i] = b;
+        centers[i] = scale(p0 + p1 + p2, S(1.0) / S(3.0));
+    }
+    BoxT<S> global = empty_box<S>();
+    for (size_t i = 0; i < n_tri; ++i) grow(global, boxes[i]);
+    std::vector<NodeT<S>> nodes(2 * n_tri + 1);
+    std::vector<size_t> prim(n_tri);
+    for (size_t i = 0; i < n_tri; ++i) prim[i] = i;
+    SahBuild<S> sb;
+    sb.nodes = nodes.data(); sb.prim = prim.data(); sb.boxes = boxes.data(); sb.centers = centers.data();
+    SahBuild<S>::store_box(nodes[0], global);
+    #pragma omp parallel
+    #pragma omp single
+    sb.run({0, 0, n_tri, 0});
+    const size_t m = sb.node_count.load();
+    *n_nodes = m;
+    *nodes_out = static_cast<NodeT<S>*>(std::malloc(m * sizeof(NodeT<S>)));
+    *prim64 = static_cast<uint64_t*>(std::malloc(n_tri * 8));
+    if (!*nodes_out || !*prim64) { std::free(*nodes_out); std::free(*prim64); return set_error(CERES_ENOMEM, "out of host memory"); }
+    std::memcpy(*nodes_out, nodes.data(), m * sizeof(NodeT<S>));
+    for (size_t i = 0; i < n_tri; ++i) (*prim64)[i] = prim[i];
+    return CERES_OK;
+}
+
+// render.hpp:91-97 (the basis; eye is passed through by the callers)
+template <class S>
+int camera_basis(const S dir[3], const S up[3], S fov_deg, size_t width, size_t height, S out9[9]) {
+    if (!dir || !up || !out9 || !width || !height) return set_error(CERES_EINVAL, "ceres_camera_basis: bad argument");
+    const V3<S> d = vnormalize(V3<S>{dir[0], dir[1], dir[2]});
+    V3<S> u = vnormalize(vcross(d, V3<S>{up[0], up[1], up[2]}));
+    V3<S> v = vnormalize(vcross(u, d));
+    const S w = std::tan(fov_deg * S(3.14159265 * (1.0 / 180.0) * 0.5));
+    const S ratio = S(height) / S(width);
+    u = scale(u, w);
+    v = scale(scale(v, w), ratio);
+    const S o[9] = {d.x, d.y, d.z, u.x, u.y, u.z, v.x, v.y, v.z};
+    std::memcpy(out9, o, sizeof o);
+    return CERES_OK;
+}
+
+// The orbit of anim.cpp:76-88: t = Transform<S>().rotate(axis, step / 180 * pi)
+// (transform.hpp:67-104, Markley-Crassidis matrix composed onto the identity) applied to the
+// camera eye, camera dir and sun once per frame; `up` is not rotated.
+template <class S>
+int orbit_cameras(const S eye[3], const S dir[3], const S up[3], const S sun[3], S fov_deg, size_t width, size_t height,
+                  const S axis[3], S step_deg, uint32_t n_frames, int rotate_first, S* basis12, S* sun3, S* dir3) {
+    if (!eye || !dir || !up || !sun || !axis || !basis12 || !sun3 || !width || !height)
+        return set_error(CERES_EINVAL, "ceres_orbit_cameras: bad argument");
+    const S pi = S(3.14159265359);
+    const S angle = step_deg / 180.0f * pi;                  // anim.cpp:77, a float literal 180
+    const V3<S> n = vnormalize(V3<S>{axis[0], axis[1], axis[2]});
+    const S s = std::sin(angle), c = std::cos(angle);
+    const S m[3][3] = {
+        {c + (1 - c) * n.x * n.x, (1 - c) * n.x * n.y + s * n.z, (1 - c) * n.x * n.z - s * n.y},
+        {(1 - c) * n.y * n.x - s * n.z, c + (1 - c) * n.y * n.y, (1 - c) * n.y * n.z + s * n.x},
+        {(1 - c) * n.z * n.x + s * n.y, (1 - c) * n.z * n.y - s * n.x, c + (1 - c) * n.z * n.z}};
+    S a[3][3];                                              // identity * m, summed like transform.hpp:96-102
+    const S id[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int r = 0; r < 3; ++r)
+        for (int col = 0; col < 3; ++col) {
+            S acc = 0;
+            for (int i = 0; i < 3; ++i) acc += id[r][i] * m[i][col];
+            a[r][col] = acc;
+        }
+    auto apply = [&](V3<S> p) -> V3<S> {                    // operator(), transform.hpp:106-112 (v = 0)
+        return {a[0][0] * p.x + a[0][1] * p.y + a[0][2] * p.z + S(0),
+                a[1][0] * p.x + a[1][1] * p.y + a[1][2] * p.z + S(0),
+                a[2][0] * p.x + a[2][1] * p.y + a[2][2] * p.z + S(0)};
+    };
+    V3<S> e{eye[0], eye[1], eye[2]}, d{dir[0], dir[1], dir[2]}, l{sun[0], sun[1], sun[2]};
+    for (uint32_t f = 0; f < n_frames; ++f) {
+        if (rotate_first || f > 0) { e = apply(e); d = apply(d); l = apply(l); }
+        const S dv[3] = {d.x, d.y, d.z};
+        basis12[12 * f] = e.x; basis12[12 * f + 1] = e.y; basis12[12 * f + 2] = e.z;
+        if (int rc = camera_basis(dv, up, fov_deg, width, height, basis12 + 12 * f + 3)) return rc;
+        sun3[3 * f] = l.x; sun3[3 * f + 1] = l.y; sun3[3 * f + 2] = l.z;
+        if (dir3) { dir3[3 * f] = d.x; dir3[3 * f + 1] = d.y; dir3[3 * f + 2] = d.z; }
+    }
+    return CERES_OK;
+}
+
 }  // namespace
 
-// Re-lay the reference BVH (nodes32 + prim64) as depth-first SiblingPair records and the
+// Re-lay the reference BVH (nodes + prim64) as depth-first SiblingPair records and the
 // triangles in leaf order (DESIGN.md "Data layout in HBM"), validating ranges and cycles.
-int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri48* tris,
-             std::vector<SiblingPair>& pairs, std::vector<Tri48>& leaf_tris, std::vector<uint32_t>& orig,
-             uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first) {
+// Node / Pair / Tri: float (RefNode, SiblingPair, Tri48) or double (RefNode64, SiblingPair64, Tri96).
+template <class Node, class Pair, class Tri>
+static int relayout_t(const Node* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri* tris,
+                      std::vector<Pair>& pairs, std::vector<Tri>& leaf_tris, std::vector<uint32_t>& orig,
+                      uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first) {
     leaf_tris.resize(n_tri);
     orig.resize(n_tri);
     for (size_t k = 0; k < n_tri; ++k) {
@@ -275,58 +453,70 @@ int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, siz
         leaf_tris[k] = tris[prim[k]];
         orig[k] = uint32_t(prim[k]);
     }
-    auto check_leaf = [&](const RefNode& n) -> bool {
-        return size_t(n.first_child_or_primitive) + n.primitive_count <= n_tri;
+    auto check_leaf = [&](const Node& n) -> bool {
+        return uint64_t(n.first_child_or_primitive) + uint64_t(n.primitive_count) <= n_tri;
     };
     depth = 0;
     root_leaf_count = root_leaf_first = 0;
     if (nodes[0].primitive_count) {
         if (!check_leaf(nodes[0])) return set_error(CERES_EINVAL, "root leaf range out of bounds");
-        root_leaf_count = nodes[0].primitive_count;
-        root_leaf_first = nodes[0].first_child_or_primitive;
-        pairs.assign(1, SiblingPair{});
+        root_leaf_count = uint32_t(nodes[0].primitive_count);
+        root_leaf_first = uint32_t(nodes[0].first_child_or_primitive);
+        pairs.assign(1, Pair{});
         return CERES_OK;
     }
     // pre-order DFS over inner nodes; each inner node's children become one record
-    struct Item { uint32_t node, pair, level; };
+    struct Item { uint64_t node; uint32_t pair, level; };
     pairs.clear();
     pairs.reserve(n_nodes / 2 + 1);
     std::vector<Item> st;
-    if (size_t(nodes[0].first_child_or_primitive) + 1 >= n_nodes) return set_error(CERES_EINVAL, "root child index out of range");
+    if (uint64_t(nodes[0].first_child_or_primitive) + 1 >= n_nodes) return set_error(CERES_EINVAL, "root child index out of range");
     pairs.emplace_back();
     st.push_back({0, 0, 1});
     size_t visited = 0;
     while (!st.empty()) {
         const Item it = st.back(); st.pop_back();
         if (++visited > n_nodes) return set_error(CERES_EINVAL, "BVH has a cycle");
-        const RefNode& n = nodes[it.node];
-        const uint32_t c = n.first_child_or_primitive;
+        const Node& n = nodes[it.node];
+        const uint64_t c = n.first_child_or_primitive;
         depth = std::max(depth, it.level);
-        SiblingPair& rec = pairs[it.pair];
-        std::memcpy(rec.lb, nodes[c].bounds, 24);
-        std::memcpy(rec.rb, nodes[c + 1].bounds, 24);
-        const RefNode* ch[2] = {&nodes[c], &nodes[c + 1]};
+        Pair& rec = pairs[it.pair];
+        std::memcpy(rec.lb, nodes[c].bounds, sizeof rec.lb);
+        std::memcpy(rec.rb, nodes[c + 1].bounds, sizeof rec.rb);
+        const Node* ch[2] = {&nodes[c], &nodes[c + 1]};
         uint32_t cnt[2], first[2];
         Item push[2]; int npush = 0;
         for (int k = 0; k < 2; ++k) {
-            cnt[k] = ch[k]->primitive_count;
-            if (cnt[k]) {
+            cnt[k] = uint32_t(ch[k]->primitive_count);
+            if (ch[k]->primitive_count) {
                 if (!check_leaf(*ch[k])) return set_error(CERES_EINVAL, "leaf range out of bounds");
-                first[k] = ch[k]->first_child_or_primitive;
+                first[k] = uint32_t(ch[k]->first_child_or_primitive);
             } else {
-                const uint32_t gc = ch[k]->first_child_or_primitive;
-                if (size_t(gc) + 1 >= n_nodes) return set_error(CERES_EINVAL, "child index out of range");
+                const uint64_t gc = ch[k]->first_child_or_primitive;
+                if (gc + 1 >= n_nodes) return set_error(CERES_EINVAL, "child index out of range");
                 first[k] = uint32_t(pairs.size());
                 pairs.emplace_back();
-                push[npush++] = {c + uint32_t(k), first[k], it.level + 1};
+                push[npush++] = {c + uint64_t(k), first[k], it.level + 1};
             }
         }
-        SiblingPair& r2 = pairs[it.pair];                            // (emplace_back may have moved rec)
+        Pair& r2 = pairs[it.pair];                                   // (emplace_back may have moved rec)
         r2.lcount = cnt[0]; r2.lfirst = first[0];
         r2.rcount = cnt[1]; r2.rfirst = first[1];
         for (int k = npush - 1; k >= 0; --k) st.push_back(push[k]);   // left subtree first
     }
     return CERES_OK;
+}
+
+int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri48* tris,
+                 std::vector<SiblingPair>& pairs, std::vector<Tri48>& leaf_tris, std::vector<uint32_t>& orig,
+                 uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first) {
+    return relayout_t(nodes, n_nodes, prim, n_tri, tris, pairs, leaf_tris, orig, depth, root_leaf_count, root_leaf_first);
+}
+
+int relayout_bvh64(const RefNode64* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri96* tris,
+                   std::vector<SiblingPair64>& pairs, std::vector<Tri96>& leaf_tris, std::vector<uint32_t>& orig,
+                   uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first) {
+    return relayout_t(nodes, n_nodes, prim, n_tri, tris, pairs, leaf_tris, orig, depth, root_leaf_count, root_leaf_first);
 }
 
 
@@ -404,156 +594,50 @@ extern "C" {
 
 void ceres_free(void* p) { std::free(p); }
 
-int ceres_obj_load(const char* path, float** tri48, float** norm36, size_t* n_tri) {
-    if (!path || !tri48 || !norm36 || !n_tri) return set_error(CERES_EINVAL, "ceres_obj_load: null argument");
-    *tri48 = *norm36 = nullptr; *n_tri = 0;
-    std::vector<char> buf;
-    if (FILE* f = std::fopen(path, "rb")) {
-        char chunk[1 << 16];
-        size_t got;
-        while ((got = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + got);
-        std::fclose(f);
-    }   // unreadable file: empty mesh, like obj_norms.hpp:123-126
-    MeshBuilder mb;
-    int rc = parse_obj(buf.data(), buf.size(), mb);
-    if (rc) return rc;
-    return mb.finish(tri48, norm36, n_tri);
-}
-
-int ceres_proc_mesh(int n, float** tri48, float** norm36, size_t* n_tri) {
-    if (n < 2 || !tri48 || !norm36 || !n_tri) return set_error(CERES_EINVAL, "ceres_proc_mesh: need n >= 2");
-    MeshBuilder mb;
-    const size_t nv = size_t(n) * size_t(n);
-    mb.verts.reserve(nv); mb.vn.reserve(nv);
-    mb.tris.reserve(2 * size_t(n - 1) * size_t(n - 1));
-    mb.corner.reserve(6 * size_t(n - 1) * size_t(n - 1));
-    for (int j = 0; j < n; ++j)
-        for (int i = 0; i < n; ++i) {
-            double x = double(i) / double(n - 1), y = double(j) / double(n - 1);
-            double z = 0.05 * (std::sin(40.0 * x) + std::cos(37.0 * y)) + 0.01 * std::sin(400.0 * x + 300.0 * y);
-            mb.add_vertex({float(x), float(y), float(z)});
-        }
-    for (int j = 0; j + 1 < n; ++j)
-        for (int i = 0; i + 1 < n; ++i) {
-            size_t a = size_t(j) * n + i, b = a + 1, c = a + n + 1, d = a + n;
-            mb.add_triangle(a, b, c);
-            mb.add_triangle(a, c, d);
-        }
-    return mb.finish(tri48, norm36, n_tri);
-}
-
-int ceres_rotate_triangles(float* tri48, size_t n_tri, int axis, float degrees) {
-    if ((!tri48 && n_tri) || axis < 0 || axis > 2) return set_error(CERES_EINVAL, "ceres_rotate_triangles: bad argument");
-    const float pi = float(3.14159265359);
-    const float c = std::cos(degrees * pi / float(180));
-    const float s = std::sin(degrees * pi / float(180));
-    auto rot = [&](Vec p) -> Vec {
-        if (axis == 0) return {p.x, p.y * c - p.z * s, p.y * s + p.z * c};
-        if (axis == 1) return {p.x * c + p.z * s, p.y, -p.x * s + p.z * c};
-        return {p.x * c - p.y * s, p.x * s + p.y * c, p.z};
-    };
-    Tri48* t = reinterpret_cast<Tri48*>(tri48);
-    #pragma omp parallel for schedule(static)
-    for (size_t i = 0; i < n_tri; ++i) {
-        const Vec p0 = P0(t[i]), p1 = P0(t[i]) - E1(t[i]), p2 = P0(t[i]) + E2(t[i]);   // p1(), p2()
-        t[i] = tri_from_points(rot(p0), rot(p1), rot(p2));
-    }
-    return CERES_OK;
-}
+int ceres_obj_load(const char* path, float** tri48, float** norm36, size_t* n_tri) { return obj_load<float>(path, tri48, norm36, n_tri); }
+int ceres_obj_load_f64(const char* path, double** tri96, double** norm72, size_t* n_tri) { return obj_load<double>(path, tri96, norm72, n_tri); }
+int ceres_proc_mesh(int n, float** tri48, float** norm36, size_t* n_tri) { return proc_mesh<float>(n, tri48, norm36, n_tri); }
+int ceres_proc_mesh_f64(int n, double** tri96, double** norm72, size_t* n_tri) { return proc_mesh<double>(n, tri96, norm72, n_tri); }
+int ceres_rotate_triangles(float* tri48, size_t n_tri, int axis, float degrees) { return rotate_triangles<float>(tri48, n_tri, axis, degrees); }
+int ceres_rotate_triangles_f64(double* tri96, size_t n_tri, int axis, double degrees) { return rotate_triangles<double>(tri96, n_tri, axis, degrees); }
 
 int ceres_bvh_build(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64) {
-    if (!tri48 || !nodes32 || !n_nodes || !prim64) return set_error(CERES_EINVAL, "ceres_bvh_build: null argument");
-    if (n_tri == 0) return set_error(CERES_EINVAL, "The given scene is empty or cannot be loaded");
-    if (n_tri > 0x7fffffffu) return set_error(CERES_EUNSUPPORTED, "more than 2^31 triangles");
-    const Tri48* t = reinterpret_cast<const Tri48*>(tri48);
-    std::vector<Box> boxes(n_tri);
-    std::vector<Vec> centers(n_tri);
-    #pragma omp parallel for schedule(static)
-    for (size_t i = 0; i < n_tri; ++i) {                   // Triangle::bounding_box / center, triangle.hpp:39-48
-        const Vec p0 = P0(t[i]), p1 = P0(t[i]) - E1(t[i]), p2 = P0(t[i]) + E2(t[i]);
-        Box b{p0, p0};
-        grow(b, Box{p1, p1});
-        grow(b, Box{p2, p2});
-        boxes[i] = b;
-        centers[i] = scale(p0 + p1 + p2, float(1.0) / float(3.0));
-    }
-    Box global = empty_box();
-    for (size_t i = 0; i < n_tri; ++i) grow(global, boxes[i]);
-    std::vector<RefNode> nodes(2 * n_tri + 1);
-    std::vector<size_t> prim(n_tri);
-    for (size_t i = 0; i < n_tri; ++i) prim[i] = i;
-    SahBuild sb;
-    sb.nodes = nodes.data(); sb.prim = prim.data(); sb.boxes = boxes.data(); sb.centers = centers.data();
-    SahBuild::store_box(nodes[0], global);
-    #pragma omp parallel
-    #pragma omp single
-    sb.run({0, 0, n_tri, 0});
-    const size_t m = sb.node_count.load();
-    *n_nodes = m;
-    *nodes32 = static_cast<uint32_t*>(std::malloc(m * sizeof(RefNode)));
-    *prim64 = static_cast<uint64_t*>(std::malloc(n_tri * 8));
-    if (!*nodes32 || !*prim64) { std::free(*nodes32); std::free(*prim64); return set_error(CERES_ENOMEM, "out of host memory"); }
-    std::memcpy(*nodes32, nodes.data(), m * sizeof(RefNode));
-    for (size_t i = 0; i < n_tri; ++i) (*prim64)[i] = prim[i];
-    return CERES_OK;
+    if (!nodes32) return set_error(CERES_EINVAL, "ceres_bvh_build: null argument");
+    NodeT<float>* nodes = nullptr;
+    const int rc = bvh_build<float>(tri48, n_tri, &nodes, n_nodes, prim64);
+    *nodes32 = reinterpret_cast<uint32_t*>(nodes);
+    return rc;
+}
+int ceres_bvh_build_f64(const double* tri96, size_t n_tri, uint64_t** nodes64, size_t* n_nodes, uint64_t** prim64) {
+    if (!nodes64) return set_error(CERES_EINVAL, "ceres_bvh_build_f64: null argument");
+    NodeT<double>* nodes = nullptr;
+    const int rc = bvh_build<double>(tri96, n_tri, &nodes, n_nodes, prim64);
+    *nodes64 = reinterpret_cast<uint64_t*>(nodes);
+    return rc;
 }
 
 int ceres_camera_basis(const float eye[3], const float dir[3], const float up[3], float fov_deg,
                        size_t width, size_t height, float out9[9]) {
     (void)eye;
-    if (!dir || !up || !out9 || !width || !height) return set_error(CERES_EINVAL, "ceres_camera_basis: bad argument");
-    const Vec d = vnormalize({dir[0], dir[1], dir[2]});
-    Vec u = vnormalize(vcross(d, {up[0], up[1], up[2]}));
-    Vec v = vnormalize(vcross(u, d));
-    const float w = std::tan(fov_deg * float(3.14159265 * (1.0 / 180.0) * 0.5));
-    const float ratio = float(height) / float(width);
-    u = scale(u, w);
-    v = scale(scale(v, w), ratio);
-    const float o[9] = {d.x, d.y, d.z, u.x, u.y, u.z, v.x, v.y, v.z};
-    std::memcpy(out9, o, sizeof o);
-    return CERES_OK;
+    return camera_basis<float>(dir, up, fov_deg, width, height, out9);
+}
+int ceres_camera_basis_f64(const double eye[3], const double dir[3], const double up[3], double fov_deg,
+                           size_t width, size_t height, double out9[9]) {
+    (void)eye;
+    return camera_basis<double>(dir, up, fov_deg, width, height, out9);
 }
 
-// The orbit of anim.cpp:76-88: t = Transform<float>().rotate(axis, step / 180 * pi)
-// (transform.hpp:67-104, Markley-Crassidis matrix composed onto the identity) applied to the
-// camera eye, camera dir and sun once per frame; `up` is not rotated.  rotate_first = 1 is
-// anim.cpp's order (rotate, then render); 0 renders frame 0 at the start pose.
 int ceres_orbit_cameras(const float eye[3], const float dir[3], const float up[3], const float sun[3], float fov_deg,
                         size_t width, size_t height, const float axis[3], float step_deg, uint32_t n_frames,
                         int rotate_first, float* basis12, float* sun3, float* dir3) {
-    if (!eye || !dir || !up || !sun || !axis || !basis12 || !sun3 || !width || !height)
-        return set_error(CERES_EINVAL, "ceres_orbit_cameras: bad argument");
-    const float pi = float(3.14159265359);
-    const float angle = step_deg / 180.0f * pi;
-    const Vec n = vnormalize({axis[0], axis[1], axis[2]});
-    const float s = std::sin(angle), c = std::cos(angle);
-    const float m[3][3] = {
-        {c + (1 - c) * n.x * n.x, (1 - c) * n.x * n.y + s * n.z, (1 - c) * n.x * n.z - s * n.y},
-        {(1 - c) * n.y * n.x - s * n.z, c + (1 - c) * n.y * n.y, (1 - c) * n.y * n.z + s * n.x},
-        {(1 - c) * n.z * n.x + s * n.y, (1 - c) * n.z * n.y - s * n.x, c + (1 - c) * n.z * n.z}};
-    float a[3][3];                                          // identity * m, summed like transform.hpp:96-102
-    const float id[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
-    for (int r = 0; r < 3; ++r)
-        for (int col = 0; col < 3; ++col) {
-            float acc = 0;
-            for (int i = 0; i < 3; ++i) acc += id[r][i] * m[i][col];
-            a[r][col] = acc;
-        }
-    auto apply = [&](Vec p) -> Vec {                        // operator(), transform.hpp:106-112 (v = 0)
-        return {a[0][0] * p.x + a[0][1] * p.y + a[0][2] * p.z + 0.0f,
-                a[1][0] * p.x + a[1][1] * p.y + a[1][2] * p.z + 0.0f,
-                a[2][0] * p.x + a[2][1] * p.y + a[2][2] * p.z + 0.0f};
-    };
-    Vec e{eye[0], eye[1], eye[2]}, d{dir[0], dir[1], dir[2]}, l{sun[0], sun[1], sun[2]};
-    for (uint32_t f = 0; f < n_frames; ++f) {
-        if (rotate_first || f > 0) { e = apply(e); d = apply(d); l = apply(l); }
-        const float ev[3] = {e.x, e.y, e.z}, dv[3] = {d.x, d.y, d.z};
-        basis12[12 * f] = e.x; basis12[12 * f + 1] = e.y; basis12[12 * f + 2] = e.z;
-        if (int rc = ceres_camera_basis(ev, dv, up, fov_deg, width, height, basis12 + 12 * f + 3)) return rc;
-        sun3[3 * f] = l.x; sun3[3 * f + 1] = l.y; sun3[3 * f + 2] = l.z;
-        if (dir3) { dir3[3 * f] = d.x; dir3[3 * f + 1] = d.y; dir3[3 * f + 2] = d.z; }
-    }
-    return CERES_OK;
+    return orbit_cameras<float>(eye, dir, up, sun, fov_deg, width, height, axis, step_deg, n_frames, rotate_first,
+                                basis12, sun3, dir3);
+}
+int ceres_orbit_cameras_f64(const double eye[3], const double dir[3], const double up[3], const double sun[3],
+                            double fov_deg, size_t width, size_t height, const double axis[3], double step_deg,
+                            uint32_t n_frames, int rotate_first, double* basis12, double* sun3, double* dir3) {
+    return orbit_cameras<double>(eye, dir, up, sun, fov_deg, width, height, axis, step_deg, n_frames, rotate_first,
+                                 basis12, sun3, dir3);
 }
 
 }  // extern "C"

@@ -1,0 +1,55 @@
+// scene_internal.hpp -- the opaque ceres_scene of include/ceres_render.h, shared by the
+// translation units that implement the ABI (render_hip.hip: float path, render64.hip: double).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "ceres_types.hpp"
+
+using ceres::SiblingPair; using ceres::SiblingPair64; using ceres::Node4; using ceres::Tri48; using ceres::Tri96;
+using ceres::Shard; using ceres::ShadowJob;
+
+struct ceres_scene {
+    int device = 0;
+    uint32_t flags = 0;
+    size_t n_tri = 0, n_pairs = 0;
+    uint32_t depth = 0, stack_entries = 1, root_leaf_count = 0, root_leaf_first = 0;
+    uint32_t shadow_stack_entries = 1;
+    size_t n_nodes4 = 0;
+    SiblingPair* d_pairs = nullptr;
+    Node4* d_nodes4 = nullptr;
+    uint32_t* d_order = nullptr;          // fused kernel tile order, for order_key
+    size_t order_cap = 0;
+    uint64_t order_key = ~0ull;
+    Tri48* d_tris = nullptr;
+    uint32_t* d_orig = nullptr;
+    float* d_norms = nullptr;
+    Shard* d_shards = nullptr;
+    bool shards_dirty = true;          // shards not known to be zero (see ceres_render_batch)
+    uint64_t* d_counters = nullptr;
+    ShadowJob* d_jobs = nullptr;
+    size_t jobs_cap = 0;
+    float* d_pixels = nullptr;
+    uint8_t* d_rgb8 = nullptr;
+    size_t px_cap = 0;
+    hipStream_t stream = nullptr;
+    int num_cus = 256;
+    unsigned long long* d_wave_log = nullptr;   // stats scenes: per-wave diagnostic records
+    size_t wave_log_waves = 0, last_grid_waves = 0;
+    // optional per-kernel device timing (bench.py roofline leg)
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<hipEvent_t> ev_used;   // triples: start, after primary, after shadow
+    std::vector<char> ev_fused;        // per triple: one ceres_fused launch (no separate shadow kernel)
+    // double-precision scene (render<double>, render64.hip): set instead of the float layout
+    bool f64 = false;
+    SiblingPair64* d_pairs64 = nullptr;
+    Tri96* d_tris64 = nullptr;
+    double* d_norms64 = nullptr;
+};
+
+namespace ceres {
+void scene_release(ceres_scene* s);          // frees every device buffer and the stream (render_hip.hip)
+}

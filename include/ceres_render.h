@@ -117,6 +117,20 @@ int ceres_orbit_cameras(const float eye[3], const float dir[3], const float up[3
                         uint32_t n_frames, int rotate_first, float* basis12, float* sun3, float* dir3);
 void ceres_free(void* p);
 
+/* ---- double precision (render<double>, anim.cpp's -d mode, anim.cpp:146-155) ----
+ * The same host steps with Scalar = double: bvh::Triangle<double> (96 B), tri_norms as
+ * 3 x Vector3<double> (72 B), bvh::Bvh<double>::Node (6 doubles + 2 x u64 = 64 B); OBJ
+ * coordinates are strtof floats widened to double (obj_norms.hpp:78-80). */
+int ceres_obj_load_f64(const char* path, double** tri96, double** norm72, size_t* n_tri);
+int ceres_proc_mesh_f64(int n, double** tri96, double** norm72, size_t* n_tri);
+int ceres_rotate_triangles_f64(double* tri96, size_t n_tri, int axis, double degrees);
+int ceres_bvh_build_f64(const double* tri96, size_t n_tri, uint64_t** nodes64, size_t* n_nodes, uint64_t** prim64);
+int ceres_camera_basis_f64(const double eye[3], const double dir[3], const double up[3], double fov_deg,
+                           size_t width, size_t height, double out9[9]);
+int ceres_orbit_cameras_f64(const double eye[3], const double dir[3], const double up[3], const double sun[3],
+                            double fov_deg, size_t width, size_t height, const double axis[3], double step_deg,
+                            uint32_t n_frames, int rotate_first, double* basis12, double* sun3, double* dir3);
+
 /* ---- device scene ---- */
 
 #define CERES_SCENE_STATS 1u   /* flag: build the kernels' traversal-statistics variant */
@@ -136,6 +150,11 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
 ceres_scene* ceres_scene_create_device(const float* d_tri48, size_t n_tri, const float* d_norm36,
                                        const uint32_t* d_nodes32, size_t n_nodes, const uint32_t* d_prim32,
                                        int device, uint32_t flags, void* stream);
+/* Double-precision scene (render<double>, anim.cpp -d): tri96 / norm72 / nodes64 / prim64 as
+ * produced by the _f64 host calls (or the reference's own Bvh<double>).  Render it with
+ * ceres_render_f64 / ceres_render_records_f64; the float render calls reject it. */
+ceres_scene* ceres_scene_create_f64(const double* tri96, size_t n_tri, const double* norm72, const void* nodes64,
+                                    size_t n_nodes, const uint64_t* prim64, int device, uint32_t flags);
 void ceres_scene_destroy(ceres_scene* scene);
 /* depth of the BVH (levels below the root) and the traversal-stack entries the kernels use */
 int ceres_scene_info(const ceres_scene* scene, uint32_t* depth, uint32_t* stack_entries,
@@ -186,6 +205,13 @@ int ceres_render_records(ceres_scene* scene, const float basis12[12], const floa
                          ceres_stats* stats);
 /* rows a rank owns under a tiling */
 size_t ceres_tiling_local_rows(size_t height, const ceres_tiling* tiling);
+/* render<double>() (render.hpp:86-156 with Scalar = double): pixels = 3*W*H doubles (bottom row
+ * first) and/or the RGB8 PPM body, basis12 / sun in double.  Records: t/u/v as doubles. */
+int ceres_render_f64(ceres_scene* scene, const double basis12[12], const double sun[3], int mode,
+                     double* pixels, uint8_t* rgb8, size_t width, size_t height, ceres_stats* stats);
+int ceres_render_records_f64(ceres_scene* scene, const double basis12[12], const double sun[3], int mode,
+                             size_t width, size_t height, int32_t* prim, double* tuv, int8_t* shadow,
+                             ceres_stats* stats);
 
 /* Per-kernel device timing (bench.py roofline leg): while enabled, every render records HIP
  * events around ceres_primary and ceres_shadow on the stream it was launched on.

@@ -1,0 +1,92 @@
+"""render<double> on the GPU (render64.hip) against the reference's own double build
+(tests/golden/f64/, oracle/_ref/ref_render_f64_exact): PPM sha256 equal, rays/hits equal, and
+per-pixel hit records {prim, t, u, v, shadow} and colours bit-identical (t/u/v as doubles).
+The shading's std::pow(double, 24) is evaluated as a correctly rounded x^24 and narrowed to
+float like blinn_phong_spec's return type (render.hpp:52-54)."""
+import gzip
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+import configs
+
+pytestmark = pytest.mark.gpu
+
+F64 = os.path.join(GOLDEN, "f64")
+NAMES = sorted(f[:-5] for f in os.listdir(F64) if f.endswith(".json"))
+
+
+@pytest.fixture(scope="module")
+def gpu(pkg):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device (no CPU fallback exists)")
+    return pkg
+
+
+def _hex64(hx):
+    return np.asarray([int(h, 16) for h in hx], np.uint64).view(np.float64)
+
+
+def load(name):
+    meta = json.load(open(os.path.join(F64, name + ".json")))
+    rec = dict(np.load(os.path.join(F64, name + ".records.npz")))
+    p = os.path.join(F64, name + ".exact.ppm.gz")
+    ppm = gzip.decompress(open(p, "rb").read()) if os.path.exists(p) else None
+    return meta, rec, ppm
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_f64_frame_matches_reference(gpu, name):
+    pkg = gpu
+    meta, rec, ppm = load(name)
+    cfg = configs.CONFIGS[name]
+    mesh, bvh, _ = pkg.prepare(cfg, f64=True)
+    scene = pkg.Scene(mesh, bvh)
+    basis = np.concatenate([_hex64(meta["pose"]["eye"]), _hex64(meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"])])
+    sun = _hex64(meta["pose"]["sun"])
+    mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
+    W, H = cfg["W"], cfg["H"]
+    px, rgb, st = scene.render(basis, sun, W, H, mode=mode)
+    assert (st["rays"], st["hits"]) == (meta["exact"]["rays"], meta["exact"]["hits"])
+    body = pkg.ppm(W, H, rgb)
+    assert hashlib.sha256(body).hexdigest() == meta["ppm_sha256"]["exact"]
+    if ppm is not None:
+        assert body == ppm
+    pix = rec["pixel"].astype(np.int64)
+    np.testing.assert_array_equal(px.reshape(-1, 3)[pix].view(np.uint64), rec["rgb"].view(np.uint64))
+    prim, tuv, sh, st2 = scene.records(basis, sun, W, H, mode=mode)
+    np.testing.assert_array_equal(prim[pix], rec["prim"])
+    hit = rec["prim"] >= 0
+    for k, key in enumerate("tuv"):
+        np.testing.assert_array_equal(tuv[pix, k][hit].view(np.uint64), rec[key][hit].view(np.uint64))
+    if mode == pkg.MODE_FULL:
+        np.testing.assert_array_equal(sh[pix], rec["shadow"])
+    scene.close()
+
+
+def test_f64_and_f32_scenes_reject_each_others_calls(gpu):
+    pkg = gpu
+    cfg = configs.CONFIGS["tri1"]
+    m64, b64, c64 = pkg.prepare(cfg, f64=True)
+    m32, b32, c32 = pkg.prepare(cfg)
+    s64, s32 = pkg.Scene(m64, b64), pkg.Scene(m32, b32)
+    import ctypes
+    px = np.empty(3 * 16, np.float32)
+    st = pkg._Stats()
+    b = c32.basis(4, 4)
+    with pytest.raises(pkg.CeresError):
+        pkg._check(pkg.lib().ceres_render_f32(s64._h, pkg._p(b, ctypes.c_float), pkg._p(np.zeros(3, np.float32), ctypes.c_float),
+                                              0, pkg._p(px, ctypes.c_float), None, 4, 4, ctypes.byref(st)))
+    pxd = np.empty(3 * 16, np.float64)
+    bd = c64.basis(4, 4)
+    with pytest.raises(pkg.CeresError):
+        pkg._check(pkg.lib().ceres_render_f64(s32._h, pkg._p(bd, ctypes.c_double), pkg._p(np.zeros(3), ctypes.c_double),
+                                              0, pkg._p(pxd, ctypes.c_double), None, 4, 4, ctypes.byref(st)))
+    s64.close()
+    s32.close()
