@@ -8,8 +8,10 @@
 //   render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]
 //                [--rotate x|y|z deg] [--size W H] [-o|--out file.ppm] [--primary-only]
 //                [--proc N] [--device D] [--bench reps] [--json]
-//                [--orbit ax ay az step_deg count] [--frames N] [--gpu-bvh]
+//                [--orbit ax ay az step_deg count] [--frames N] [--gpu-bvh] [--double|-d]
 //
+// --double (anim.cpp's -d, anim.cpp:146-155) runs the whole sequence as render<double>:
+// numbers parsed with strtod, double mesh / BVH / camera, the double GPU kernel.
 // --gpu-bvh builds the same BinnedSahBuilder BVH with the gfx950 builder (bvh_build.hip).
 //
 // --orbit / --frames are the anim.cpp:76-125 driver without Magick++: the camera eye, dir and
@@ -32,16 +34,21 @@
 
 namespace {
 
+// Every number is kept as float (strtof, render<float>) and as double (strtod: the double
+// literals of anim.cpp's -d mode); --double selects the double pipeline.
+template <class S> struct Num {
+    S eye[3] = {0, -15, 2}, dir[3] = {0, 1, 0}, up[3] = {0, 0, 1}, sun[3] = {-50, -20, 0};
+    S fov = 60, rot_deg = 0, orbit_axis[3] = {0, 1, 0}, orbit_step = 0;
+};
+
 struct Opts {
     std::string obj, out = "render.ppm";
-    float eye[3] = {0.f, -15.f, 2.f}, dir[3] = {0.f, 1.f, 0.f}, up[3] = {0.f, 0.f, 1.f}, sun[3] = {-50.f, -20.f, 0.f};
-    float fov = 60.f;
+    Num<float> f;
+    Num<double> d;
     int rot_axis = -1;
-    float rot_deg = 0.f;
     size_t W = 1920, H = 1080;
     int mode = CERES_MODE_FULL, proc = 0, device = 0, bench = 0;
-    bool json = false, gpu_bvh = false;
-    float orbit_axis[3] = {0.f, 1.f, 0.f}, orbit_step = 0.f;
+    bool json = false, gpu_bvh = false, f64 = false;
     int orbit_count = 0, frames = 1;
 };
 
@@ -50,26 +57,37 @@ int usage() {
                  "usage: render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]\n"
                  "              [--rotate x|y|z deg] [--size W H] [-o out.ppm] [--primary-only] [--proc N]\n"
                  "              [--device D] [--bench reps] [--json] [--orbit ax ay az step_deg count] [--frames N]\n"
-                 "              [--gpu-bvh]\n");
+                 "              [--gpu-bvh] [--double]\n");
     return 2;
 }
 
 bool parse(int argc, char** argv, Opts& o) {
-    auto f = [](const char* s, float* dst) { char* e; *dst = std::strtof(s, &e); return *e == '\0'; };
+    // one number into both precisions; the whole string must convert
+    auto num = [](const char* s, float* f, double* d) {
+        char* e1; char* e2;
+        *f = std::strtof(s, &e1);
+        *d = std::strtod(s, &e2);
+        return *e1 == '\0' && *e2 == '\0';
+    };
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto have = [&](int n) { return i + n < argc; };
-        auto vec = [&](float* v) { if (!have(3)) return false; bool ok = f(argv[i + 1], v) && f(argv[i + 2], v + 1) && f(argv[i + 3], v + 2); i += 3; return ok; };
-        if (a == "--eye") { if (!vec(o.eye)) return false; }
-        else if (a == "--dir") { if (!vec(o.dir)) return false; }
-        else if (a == "--up") { if (!vec(o.up)) return false; }
-        else if (a == "--sun") { if (!vec(o.sun)) return false; }
-        else if (a == "--fov") { if (!have(1) || !f(argv[++i], &o.fov)) return false; }
+        auto vec = [&](float* v, double* w) {
+            if (!have(3)) return false;
+            bool ok = num(argv[i + 1], v, w) && num(argv[i + 2], v + 1, w + 1) && num(argv[i + 3], v + 2, w + 2);
+            i += 3;
+            return ok;
+        };
+        if (a == "--eye") { if (!vec(o.f.eye, o.d.eye)) return false; }
+        else if (a == "--dir") { if (!vec(o.f.dir, o.d.dir)) return false; }
+        else if (a == "--up") { if (!vec(o.f.up, o.d.up)) return false; }
+        else if (a == "--sun") { if (!vec(o.f.sun, o.d.sun)) return false; }
+        else if (a == "--fov") { if (!have(1) || !num(argv[++i], &o.f.fov, &o.d.fov)) return false; }
         else if (a == "--rotate") {
             if (!have(2)) return false;
             const char c = argv[i + 1][0];
             o.rot_axis = c == 'x' ? 0 : c == 'y' ? 1 : c == 'z' ? 2 : -2;
-            if (o.rot_axis == -2 || argv[i + 1][1] != '\0' || !f(argv[i + 2], &o.rot_deg)) return false;
+            if (o.rot_axis == -2 || argv[i + 1][1] != '\0' || !num(argv[i + 2], &o.f.rot_deg, &o.d.rot_deg)) return false;
             i += 2;
         } else if (a == "--size") {
             if (!have(2)) return false;
@@ -82,8 +100,9 @@ bool parse(int argc, char** argv, Opts& o) {
         else if (a == "--bench") { if (!have(1)) return false; o.bench = std::atoi(argv[++i]); }
         else if (a == "--json") o.json = true;
         else if (a == "--gpu-bvh") o.gpu_bvh = true;
+        else if (a == "--double" || a == "-d") o.f64 = true;                   // anim.cpp:146-147
         else if (a == "--orbit") {
-            if (!vec(o.orbit_axis) || !have(2) || !f(argv[i + 1], &o.orbit_step)) return false;
+            if (!vec(o.f.orbit_axis, o.d.orbit_axis) || !have(2) || !num(argv[i + 1], &o.f.orbit_step, &o.d.orbit_step)) return false;
             o.orbit_count = std::atoi(argv[i + 2]); i += 2;
             if (o.orbit_count < 0) return false;
         } else if (a == "--frames") { if (!have(1)) return false; o.frames = std::atoi(argv[++i]); if (o.frames < 1) return false; }
@@ -95,37 +114,73 @@ bool parse(int argc, char** argv, Opts& o) {
     return !o.obj.empty() || o.proc > 0;
 }
 
+// The C ABI per precision (render<float> / render<double>).
+template <class S> struct Api;
+template <> struct Api<float> {
+    using Node = uint32_t;
+    static int load(const char* p, float** t, float** n, size_t* c) { return ceres_obj_load(p, t, n, c); }
+    static int proc(int k, float** t, float** n, size_t* c) { return ceres_proc_mesh(k, t, n, c); }
+    static int rotate(float* t, size_t c, int ax, float deg) { return ceres_rotate_triangles(t, c, ax, deg); }
+    static int bvh(const float* t, size_t c, Node** nodes, size_t* m, uint64_t** prim, bool gpu, int dev) {
+        return gpu ? ceres_bvh_build_gpu(t, c, nodes, m, prim, dev) : ceres_bvh_build(t, c, nodes, m, prim);
+    }
+    static ceres_scene* scene(const float* t, size_t c, const float* n, const Node* nodes, size_t m, const uint64_t* prim, int dev) {
+        return ceres_scene_create(t, c, n, nodes, m, prim, dev, 0);
+    }
+    static int orbit(const Num<float>& v, size_t W, size_t H, uint32_t k, float* b, float* s) {
+        return ceres_orbit_cameras(v.eye, v.dir, v.up, v.sun, v.fov, W, H, v.orbit_axis, v.orbit_step, k, 0, b, s, nullptr);
+    }
+    static int render(ceres_scene* sc, const float* b, const float* s, int mode, uint8_t* rgb, size_t W, size_t H, ceres_stats* st) {
+        return ceres_render_f32(sc, b, s, mode, nullptr, rgb, W, H, st);
+    }
+};
+template <> struct Api<double> {
+    using Node = uint64_t;
+    static int load(const char* p, double** t, double** n, size_t* c) { return ceres_obj_load_f64(p, t, n, c); }
+    static int proc(int k, double** t, double** n, size_t* c) { return ceres_proc_mesh_f64(k, t, n, c); }
+    static int rotate(double* t, size_t c, int ax, double deg) { return ceres_rotate_triangles_f64(t, c, ax, deg); }
+    static int bvh(const double* t, size_t c, Node** nodes, size_t* m, uint64_t** prim, bool gpu, int) {
+        if (gpu) { std::fprintf(stderr, "error: --gpu-bvh builds single-precision BVHs only\n"); return CERES_EUNSUPPORTED; }
+        return ceres_bvh_build_f64(t, c, nodes, m, prim);
+    }
+    static ceres_scene* scene(const double* t, size_t c, const double* n, const Node* nodes, size_t m, const uint64_t* prim, int dev) {
+        return ceres_scene_create_f64(t, c, n, nodes, m, prim, dev, 0);
+    }
+    static int orbit(const Num<double>& v, size_t W, size_t H, uint32_t k, double* b, double* s) {
+        return ceres_orbit_cameras_f64(v.eye, v.dir, v.up, v.sun, v.fov, W, H, v.orbit_axis, v.orbit_step, k, 0, b, s, nullptr);
+    }
+    static int render(ceres_scene* sc, const double* b, const double* s, int mode, uint8_t* rgb, size_t W, size_t H, ceres_stats* st) {
+        return ceres_render_f64(sc, b, s, mode, nullptr, rgb, W, H, st);
+    }
+};
+
 double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
-}  // namespace
-
-int main(int argc, char** argv) {
-    Opts o;
-    if (!parse(argc, argv, o)) return usage();
-    float* tri = nullptr; float* norm = nullptr; size_t n_tri = 0;
-    const int rc_load = o.proc ? ceres_proc_mesh(o.proc, &tri, &norm, &n_tri) : ceres_obj_load(o.obj.c_str(), &tri, &norm, &n_tri);
+template <class S>
+int run(const Opts& o, const Num<S>& v) {
+    using A = Api<S>;
+    S* tri = nullptr; S* norm = nullptr; size_t n_tri = 0;
+    const int rc_load = o.proc ? A::proc(o.proc, &tri, &norm, &n_tri) : A::load(o.obj.c_str(), &tri, &norm, &n_tri);
     if (rc_load != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
     if (n_tri == 0) { std::fprintf(stderr, "The given scene is empty or cannot be loaded\n"); return 1; }   // static.cpp:77-80
-    if (o.rot_axis >= 0) ceres_rotate_triangles(tri, n_tri, o.rot_axis, o.rot_deg);
+    if (o.rot_axis >= 0) A::rotate(tri, n_tri, o.rot_axis, v.rot_deg);
 
     std::printf("Building BVH ( using BinnedSahBuilder%s )...\n", o.gpu_bvh ? " on the GPU" : "");
     const double t0 = now_s();
-    uint32_t* nodes = nullptr; uint64_t* prim = nullptr; size_t n_nodes = 0;
-    const int rc_bvh = o.gpu_bvh ? ceres_bvh_build_gpu(tri, n_tri, &nodes, &n_nodes, &prim, o.device)
-                                 : ceres_bvh_build(tri, n_tri, &nodes, &n_nodes, &prim);
+    typename A::Node* nodes = nullptr; uint64_t* prim = nullptr; size_t n_nodes = 0;
+    const int rc_bvh = A::bvh(tri, n_tri, &nodes, &n_nodes, &prim, o.gpu_bvh, o.device);
     if (rc_bvh != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
     std::printf("%g\n", now_s() - t0);
     std::printf("BVH of %zu node(s) and %zu reference(s)\n", n_nodes, n_tri);
 
-    ceres_scene* scene = ceres_scene_create(tri, n_tri, norm, nodes, n_nodes, prim, o.device, 0);
+    ceres_scene* scene = A::scene(tri, n_tri, norm, nodes, n_nodes, prim, o.device);
     ceres_free(nodes); ceres_free(prim); ceres_free(tri); ceres_free(norm);
     if (!scene) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
 
     // frame poses: count + k orbit rotations for frame k (count = 0, frames = 1: the plain camera)
     const uint32_t n_pose = uint32_t(o.orbit_count + o.frames);
-    std::vector<float> bases(12 * size_t(n_pose)), suns(3 * size_t(n_pose));
-    if (ceres_orbit_cameras(o.eye, o.dir, o.up, o.sun, o.fov, o.W, o.H, o.orbit_axis, o.orbit_step, n_pose, 0,
-                            bases.data(), suns.data(), nullptr) != CERES_OK) {
+    std::vector<S> bases(12 * size_t(n_pose)), suns(3 * size_t(n_pose));
+    if (A::orbit(v, o.W, o.H, n_pose, bases.data(), suns.data()) != CERES_OK) {
         std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1;
     }
     std::vector<uint8_t> rgb(3 * o.W * o.H);
@@ -133,11 +188,11 @@ int main(int argc, char** argv) {
     unsigned long long tot_rays = 0;
     std::vector<double> ms;
     for (int k = 0; k < o.frames; ++k) {
-        const float* basis = bases.data() + 12 * size_t(o.orbit_count + k);
-        const float* sun = suns.data() + 3 * size_t(o.orbit_count + k);
+        const S* basis = bases.data() + 12 * size_t(o.orbit_count + k);
+        const S* sun = suns.data() + 3 * size_t(o.orbit_count + k);
         std::printf("Rendering image %d (%zux%zu) on HIP device %d...\n", k, o.W, o.H, o.device);
         const double t1 = now_s();
-        int rc = ceres_render_f32(scene, basis, sun, o.mode, nullptr, rgb.data(), o.W, o.H, &st);
+        int rc = A::render(scene, basis, sun, o.mode, rgb.data(), o.W, o.H, &st);
         const double t2 = now_s();
         if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1; }
         std::printf("%g\n", t2 - t1);
@@ -145,7 +200,7 @@ int main(int argc, char** argv) {
         tot_rays += st.rays;
         for (int r = 0; r < o.bench; ++r) {
             ceres_stats s2{};
-            rc = ceres_render_f32(scene, basis, sun, o.mode, nullptr, rgb.data(), o.W, o.H, &s2);
+            rc = A::render(scene, basis, sun, o.mode, rgb.data(), o.W, o.H, &s2);
             if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1; }
             ms.push_back(s2.ms);
         }
@@ -179,4 +234,12 @@ int main(int argc, char** argv) {
     }
     ceres_scene_destroy(scene);
     return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Opts o;
+    if (!parse(argc, argv, o)) return usage();
+    return o.f64 ? run<double>(o, o.d) : run<float>(o, o.f);
 }

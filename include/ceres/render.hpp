@@ -16,8 +16,9 @@
 // Semantics kept: the caller owns every buffer; pixels (3*W*H) are fully overwritten with
 // row j = 0 at the bottom; the return value is {rays traced, hits} (render.hpp:155).
 // Differences, all loud: HIP/launch errors throw std::runtime_error (the reference has no
-// error path); Scalar = double throws (GPU double path not built yet);
-// tri_norms == nullptr throws instead of dereferencing null (render.hpp:142).
+// error path); tri_norms == nullptr throws instead of dereferencing null (render.hpp:142).
+// Scalar = double (anim.cpp -d) runs the double-precision GPU path (ceres_render_f64) over the
+// caller's bvh::Bvh<double> / bvh::Triangle<double> (64-B nodes, 96-B triangles).
 // The uploaded scene is cached per (bvh, triangles, tri_norms, node_count, fingerprint), so
 // multi-frame callers like anim.cpp:82-125 upload once.  Link with -lceres_hip.
 #ifndef CERES_RENDER_HPP_DROPIN
@@ -56,20 +57,28 @@ struct vec3 {
     Scalar operator[](size_t i) const { return v[i]; }
 };
 
-// Self-contained equivalents of bvh::Triangle<float> / bvh::Bvh<float> (same layouts).
-struct HostTriangle { vec3<float> p0, e1, e2, n; };
-struct HostBvh {
-    struct Node { float bounds[6]; uint32_t primitive_count, first_child_or_primitive; };
+// Self-contained equivalents of bvh::Triangle<S> / bvh::Bvh<S> (same layouts; S = float or
+// double, whose nodes carry 64-bit counts like bvh::Bvh<double>'s IndexType).
+template <typename Scalar> struct BasicHostTriangle { vec3<Scalar> p0, e1, e2, n; };
+template <typename Scalar>
+struct BasicHostBvh {
+    using Index = std::conditional_t<std::is_same<Scalar, double>::value, uint64_t, uint32_t>;
+    struct Node { Scalar bounds[6]; Index primitive_count, first_child_or_primitive; };
     std::unique_ptr<Node[]> nodes;
     std::unique_ptr<size_t[]> primitive_indices;
     size_t node_count = 0;
 };
+using HostTriangle = BasicHostTriangle<float>;
+using HostBvh = BasicHostBvh<float>;
+using HostTriangle64 = BasicHostTriangle<double>;
+using HostBvh64 = BasicHostBvh<double>;
 
 namespace detail {
 
 struct SceneCache {
     const void *bvh = nullptr, *tris = nullptr, *norms = nullptr;
     size_t node_count = 0, n_tri = 0;
+    bool f64 = false;
     uint64_t fingerprint = 0;
     ceres_scene* scene = nullptr;
     std::mutex mu;
@@ -83,12 +92,13 @@ inline uint64_t fnv(uint64_t h, const void* p, size_t n) {
     return h;
 }
 // Sampled fingerprint (every 4096th record + both ends) so an edited mesh re-uploads.
-inline uint64_t fingerprint(const void* nodes, size_t n_nodes, const void* tris, size_t n_tri) {
+inline uint64_t fingerprint(const void* nodes, size_t n_nodes, size_t node_bytes, const void* tris, size_t n_tri,
+                            size_t tri_bytes) {
     uint64_t h = 1469598103934665603ull;
-    for (size_t i = 0; i < n_nodes; i += 4096) h = fnv(h, static_cast<const char*>(nodes) + 32 * i, 32);
-    if (n_nodes) h = fnv(h, static_cast<const char*>(nodes) + 32 * (n_nodes - 1), 32);
-    for (size_t i = 0; i < n_tri; i += 4096) h = fnv(h, static_cast<const char*>(tris) + 48 * i, 48);
-    if (n_tri) h = fnv(h, static_cast<const char*>(tris) + 48 * (n_tri - 1), 48);
+    for (size_t i = 0; i < n_nodes; i += 4096) h = fnv(h, static_cast<const char*>(nodes) + node_bytes * i, node_bytes);
+    if (n_nodes) h = fnv(h, static_cast<const char*>(nodes) + node_bytes * (n_nodes - 1), node_bytes);
+    for (size_t i = 0; i < n_tri; i += 4096) h = fnv(h, static_cast<const char*>(tris) + tri_bytes * i, tri_bytes);
+    if (n_tri) h = fnv(h, static_cast<const char*>(tris) + tri_bytes * (n_tri - 1), tri_bytes);
     return h;
 }
 
@@ -111,51 +121,61 @@ struct Camera {                                                      // render.h
 // p1() = p0 - e1, p2() = p0 + e2 (bit-identical to the reference; runs on the host).
 template <size_t Axis, typename Scalar, typename Tri>
 static void rotate_triangles(Scalar degrees, Tri* triangles, size_t triangle_count) {
-    static_assert(std::is_same<Scalar, float>::value && sizeof(Tri) == 48, "ceres: float triangles (48 B) only");
-    if (ceres_rotate_triangles(reinterpret_cast<float*>(triangles), triangle_count, int(Axis), degrees) != CERES_OK)
-        ceres::detail::fail("rotate_triangles");
+    static_assert((std::is_same<Scalar, float>::value && sizeof(Tri) == 48) ||
+                  (std::is_same<Scalar, double>::value && sizeof(Tri) == 96), "ceres: bvh::Triangle<float|double> only");
+    const int rc = std::is_same<Scalar, double>::value
+        ? ceres_rotate_triangles_f64(reinterpret_cast<double*>(triangles), triangle_count, int(Axis), double(degrees))
+        : ceres_rotate_triangles(reinterpret_cast<float*>(triangles), triangle_count, int(Axis), float(degrees));
+    if (rc != CERES_OK) ceres::detail::fail("rotate_triangles");
 }
 
 // render.hpp:86-156 -- renders W x H pixels on the GPU, returns {rays, hits}.
 template <typename Scalar, typename Vec, typename BvhT, typename TriT, typename NormT>
 std::pair<int, int> render(const Camera<Scalar>& camera, const Vec& sun_position, const BvhT& bvh,
                            const TriT* triangles, NormT* tri_norms, Scalar* pixels, size_t width, size_t height) {
-    if (!std::is_same<Scalar, float>::value)
-        throw std::runtime_error("ceres render(): Scalar=double is not supported on the GPU path");
-    static_assert(sizeof(TriT) == 48 || !std::is_same<Scalar, float>::value, "triangle must be bvh::Triangle<float> layout");
+    constexpr bool kF64 = std::is_same<Scalar, double>::value;
+    static_assert(kF64 || std::is_same<Scalar, float>::value, "ceres render(): Scalar must be float or double");
+    static_assert(sizeof(TriT) == 12 * sizeof(Scalar), "triangle must be bvh::Triangle<Scalar> layout");
     if (!triangles || !tri_norms || !pixels) throw std::runtime_error("ceres render(): null triangles/tri_norms/pixels");
     const auto* nodes = bvh.nodes.get();
     const size_t n_nodes = bvh.node_count;
-    static_assert(sizeof(*nodes) == 32, "bvh node must be bvh::Bvh<float>::Node layout");
+    static_assert(sizeof(*nodes) == 8 * sizeof(Scalar), "bvh node must be bvh::Bvh<Scalar>::Node layout");
     // triangle count = end of the furthest leaf (the reference never passes it explicitly)
     size_t n_tri = 0;
     for (size_t k = 0; k < n_nodes; ++k)
         if (nodes[k].primitive_count)
-            n_tri = std::max<size_t>(n_tri, size_t(nodes[k].first_child_or_primitive) + nodes[k].primitive_count);
+            n_tri = std::max<size_t>(n_tri, size_t(nodes[k].first_child_or_primitive) + size_t(nodes[k].primitive_count));
     auto& c = ceres::detail::cache();
     std::lock_guard<std::mutex> lock(c.mu);
-    const uint64_t fp = ceres::detail::fingerprint(nodes, n_nodes, triangles, n_tri);
+    const uint64_t fp = ceres::detail::fingerprint(nodes, n_nodes, sizeof(*nodes), triangles, n_tri, sizeof(TriT));
     if (!c.scene || c.bvh != &bvh || c.tris != triangles || c.norms != tri_norms || c.node_count != n_nodes ||
-        c.n_tri != n_tri || c.fingerprint != fp) {
+        c.n_tri != n_tri || c.fingerprint != fp || c.f64 != kF64) {
         if (c.scene) ceres_scene_destroy(c.scene);
-        c.scene = ceres_scene_create(reinterpret_cast<const float*>(triangles), n_tri,
-                                     reinterpret_cast<const float*>(tri_norms), nodes, n_nodes,
-                                     reinterpret_cast<const uint64_t*>(bvh.primitive_indices.get()), 0, 0);
+        const uint64_t* prim = reinterpret_cast<const uint64_t*>(bvh.primitive_indices.get());
+        c.scene = kF64 ? ceres_scene_create_f64(reinterpret_cast<const double*>(triangles), n_tri,
+                                                reinterpret_cast<const double*>(tri_norms), nodes, n_nodes, prim, 0, 0)
+                       : ceres_scene_create(reinterpret_cast<const float*>(triangles), n_tri,
+                                            reinterpret_cast<const float*>(tri_norms), nodes, n_nodes, prim, 0, 0);
         if (!c.scene) ceres::detail::fail("ceres_scene_create");
         c.bvh = &bvh; c.tris = triangles; c.norms = tri_norms; c.node_count = n_nodes; c.n_tri = n_tri; c.fingerprint = fp;
+        c.f64 = kF64;
     }
-    float eye[3] = {float(camera.eye[0]), float(camera.eye[1]), float(camera.eye[2])};
-    float dir[3] = {float(camera.dir[0]), float(camera.dir[1]), float(camera.dir[2])};
-    float up[3] = {float(camera.up[0]), float(camera.up[1]), float(camera.up[2])};
-    float basis[12];
+    Scalar eye[3] = {Scalar(camera.eye[0]), Scalar(camera.eye[1]), Scalar(camera.eye[2])};
+    Scalar dir[3] = {Scalar(camera.dir[0]), Scalar(camera.dir[1]), Scalar(camera.dir[2])};
+    Scalar up[3] = {Scalar(camera.up[0]), Scalar(camera.up[1]), Scalar(camera.up[2])};
+    Scalar basis[12];
     std::memcpy(basis, eye, sizeof eye);
-    if (ceres_camera_basis(eye, dir, up, float(camera.fov), width, height, basis + 3) != CERES_OK)
-        ceres::detail::fail("camera basis");
-    const float sun[3] = {float(sun_position[0]), float(sun_position[1]), float(sun_position[2])};
+    const Scalar sun[3] = {Scalar(sun_position[0]), Scalar(sun_position[1]), Scalar(sun_position[2])};
     ceres_stats st{};
-    if (ceres_render_f32(c.scene, basis, sun, CERES_MODE_FULL, reinterpret_cast<float*>(pixels), nullptr, width,
-                         height, &st) != CERES_OK)
-        ceres::detail::fail("ceres_render_f32");
+    int rc;
+    if constexpr (kF64) {
+        if (ceres_camera_basis_f64(eye, dir, up, camera.fov, width, height, basis + 3) != CERES_OK) ceres::detail::fail("camera basis");
+        rc = ceres_render_f64(c.scene, basis, sun, CERES_MODE_FULL, pixels, nullptr, width, height, &st);
+    } else {
+        if (ceres_camera_basis(eye, dir, up, camera.fov, width, height, basis + 3) != CERES_OK) ceres::detail::fail("camera basis");
+        rc = ceres_render_f32(c.scene, basis, sun, CERES_MODE_FULL, pixels, nullptr, width, height, &st);
+    }
+    if (rc != CERES_OK) ceres::detail::fail("ceres render");
     return std::pair<int, int>(int(st.rays), int(st.hits));
 }
 

@@ -72,6 +72,12 @@ int main() {
     std::vector<float> px(3 * 4 * 4);
     rotate_triangles<0>(90.0f, tris.data(), tris.size());
     if (false) render(cam, ceres::vec3<float>(-50, -20, 0), bvh, tris.data(), norms.data(), px.data(), 4, 4);
+    ceres::HostBvh64 bvh64; std::vector<ceres::HostTriangle64> tris64(1);
+    std::vector<std::array<ceres::vec3<double>, 3>> norms64(1);
+    Camera<double> cam64{ceres::vec3<double>(-150, -20, 0), ceres::vec3<double>(1, -0.1, 0), ceres::vec3<double>(0, -1, 0), 60};
+    std::vector<double> px64(3 * 4 * 4);
+    rotate_triangles<1>(45.0, tris64.data(), tris64.size());
+    if (false) render(cam64, ceres::vec3<double>(-500, 300, 10), bvh64, tris64.data(), norms64.data(), px64.data(), 4, 4);
     return 0;
 }
 ''')
@@ -103,6 +109,13 @@ int main() {
     return 0;
 }
 ''')
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I/root/reference/lib", "-I" + os.path.join(REPO, "include"),
+                        str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    # anim.cpp -d: the same calls with Scalar = double (anim.cpp:146-155, camera as double literals)
+    src.write_text(src.read_text().replace("using Scalar = float;", "using Scalar = double;")
+                   .replace("Vector3(0.0, -15.0, 2.0), Vector3(0, 1, 0), Vector3(0, 0, 1)",
+                            "Vector3(-150.0, -20.0, 0.0), Vector3(1, -0.1, 0), Vector3(0, -1, 0)"))
     r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I/root/reference/lib", "-I" + os.path.join(REPO, "include"),
                         str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr

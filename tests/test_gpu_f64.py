@@ -90,3 +90,55 @@ def test_f64_and_f32_scenes_reject_each_others_calls(gpu):
                                               0, pkg._p(pxd, ctypes.c_double), None, 4, 4, ctypes.byref(st)))
     s64.close()
     s32.close()
+
+
+def test_cli_double_writes_reference_ppm(gpu, tmp_path):
+    """./render --double (anim.cpp's -d): the reference's double-precision PPM, byte for byte."""
+    import subprocess
+    pkg = gpu
+    meta, _, ppm = load("bunny_640")
+    out = tmp_path / "b.ppm"
+    args = configs.cli_args(configs.CONFIGS["bunny_640"]) + ["--double", "-o", str(out)]
+    r = subprocess.run([pkg.CLI_PATH] + args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Rays: %d\tHits: %d" % (meta["exact"]["rays"], meta["exact"]["hits"]) in r.stdout
+    assert out.read_bytes() == ppm
+
+
+def test_dropin_render_hpp_double_runs(gpu, tmp_path):
+    """A static.cpp-style program with Scalar = double on include/ceres/render.hpp."""
+    import subprocess
+    from conftest import REPO
+    pkg = gpu
+    meta, _, _ = load("dragon_333x217")
+    src = tmp_path / "app.cpp"
+    src.write_text(r'''
+#include <cstdio>
+#include <vector>
+#include "ceres/render.hpp"
+int main(int argc, char** argv) {
+    double* tri; double* nrm; size_t n;
+    if (ceres_obj_load_f64(argv[1], &tri, &nrm, &n)) return 3;
+    rotate_triangles<0>(90.0, reinterpret_cast<ceres::HostTriangle64*>(tri), n);
+    uint64_t* nodes; uint64_t* prim; size_t m;
+    if (ceres_bvh_build_f64(tri, n, &nodes, &m, &prim)) return 4;
+    ceres::HostBvh64 bvh;
+    bvh.nodes.reset(new ceres::HostBvh64::Node[m]); std::memcpy(bvh.nodes.get(), nodes, 64 * m);
+    bvh.primitive_indices.reset(new size_t[n]); std::memcpy(bvh.primitive_indices.get(), prim, 8 * n);
+    bvh.node_count = m;
+    Camera<double> cam{ceres::vec3<double>(0, -15, 2), ceres::vec3<double>(0, 1, 0), ceres::vec3<double>(0, 0, 1), 60};
+    std::vector<double> px(3 * 333 * 217);
+    auto rh = render(cam, ceres::vec3<double>(-50, -20, 0), bvh, reinterpret_cast<ceres::HostTriangle64*>(tri),
+                     reinterpret_cast<std::array<ceres::vec3<double>, 3>*>(nrm), px.data(), 333, 217);
+    std::printf("%d %d\n", rh.first, rh.second);
+    return 0;
+}
+''')
+    exe = tmp_path / "app"
+    pkgdir = os.path.dirname(pkg.LIB_PATH)
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-I" + os.path.join(REPO, "include"), str(src), "-o", str(exe),
+                        "-L" + pkgdir, "-lceres_hip", "-Wl,-rpath," + pkgdir], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe), os.path.join(REPO, "data", "dragon.obj")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert tuple(map(int, r.stdout.split())) == (meta["exact"]["rays"], meta["exact"]["hits"])
