@@ -41,6 +41,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef CERES_STEP_SELECT
+#define CERES_STEP_SELECT 0   // branch-free next-node step in trace() (A/B switch)
+#endif
+
 namespace ceres {
 
 char* error_buffer() {
@@ -157,6 +161,9 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         const float4* q = reinterpret_cast<const float4*>(P.pairs + cur);
         const float4 A = q[0], B = q[1], C = q[2];
         const uint4 L = reinterpret_cast<const uint4*>(q)[3];
+#if CERES_STEP_SELECT
+        const uint32_t top = stk[(sp ? sp - 1 : 0) * kBlock];         // popped if this step descends nowhere
+#endif
         // left bounds A.x A.y | A.z A.w | B.x B.y ; right bounds B.z B.w | C.x C.y | C.z C.w
         const float l0 = __builtin_fmaf(A.x, ix, sx), l1 = __builtin_fmaf(A.y, ix, sx);
         const float l2 = __builtin_fmaf(A.z, iy, sy), l3 = __builtin_fmaf(A.w, iy, sy);
@@ -187,6 +194,19 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         }
         if (kStats && ss) { c2 = stamp(); ss->box += c1 - c0; ss->leaf += c2 - c1; ss->iters++; }
         const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
+#if CERES_STEP_SELECT
+        // the same three cases with selects: the far child is written to slot sp every step
+        // (a free slot unless this step pushes; the LDS stack has stack_entries + 1 slots), the
+        // stack top was read at the start of the step, only the exit branches
+        const bool both = go_l && go_r, none = !go_l && !go_r;
+        const bool swap = le > re;                                    // near first, ties left (:109-115)
+        overflow |= both && sp >= P.stack_entries;
+        stk[(sp < P.stack_entries ? sp : P.stack_entries) * kBlock] = swap ? L.y : L.w;
+        if (none && sp == 0) { if (kStats && ss) ss->next += stamp() - c2; break; }   // :118-121
+        const uint32_t near = both ? (swap ? L.w : L.y) : (go_l ? L.y : L.w);        // :115-117
+        cur = none ? top : near;
+        sp = both ? (sp < P.stack_entries ? sp + 1 : sp) : (none ? sp - 1 : sp);
+#else
         if (go_l && go_r) {                                           // near first, ties left (:109-115)
             const bool swap = le > re;
             if (sp >= P.stack_entries) { overflow = true; return have; }
@@ -200,6 +220,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
             --sp;
             cur = stk[sp * kBlock];
         }
+#endif
         if (kStats && ss) ss->next += stamp() - c2;
     }
     return have;
@@ -552,7 +573,7 @@ struct StealLds {
 template <bool kStats>
 __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, uint32_t* stk, StealLds& L,
                                                uint32_t tid, uint32_t lane, uint32_t& n_pairs, uint32_t& n_tests,
-                                               bool& overflow) {
+                                               bool& overflow, uint32_t* n_iters = nullptr) {
     const float tmin = 0.0f, tmax = FLT_MAX;
     const uint32_t cap = P.shadow_stack_entries;
     const uint32_t wbase = tid & ~63u;
@@ -569,6 +590,7 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
     }
     __builtin_amdgcn_wave_barrier();
     while (__ballot(active)) {
+        if (kStats && n_iters) ++*n_iters;
         if (active && L.blocked[owner]) active = false;                 // another piece found an occluder
         if (active) {
             if (kStats) ++n_pairs;
@@ -782,6 +804,8 @@ __global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
     uint32_t n_pairs = 0, n_tests = 0;
     bool overflow = false;
     RayWork w{};
+    uint64_t t_start = 0;
+    if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
     if (active) {
         const F3 view = primary_dir(P, f, i, global_row(P, lr));
         hit = trace<false, kStats>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
@@ -805,9 +829,25 @@ __global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
         }
     }
     const uint32_t n_shadow = __popcll(__ballot(hit));
-    steal_traverse<kStats>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow);
+    uint64_t t_primary = 0;
+    uint32_t prim_pairs = n_pairs, shadow_iters = 0;
+    if (kStats && P.wave_log) t_primary = __builtin_amdgcn_s_memrealtime();
+    steal_traverse<kStats>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
     uint32_t occluded = 0;
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
+    if (kStats && P.wave_log) {
+        // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
+        // primary hits, wave primary pairs, wave shadow pairs
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        uint32_t mx = prim_pairs;
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), off, 64)));
+        const uint32_t sp = wave_sum(prim_pairs), ss = wave_sum(n_pairs - prim_pairs);
+        if (lane == 0) {
+            unsigned long long* wl = P.wave_log + 8 * size_t(blockIdx.x * (kBlock / 64) + wave);
+            wl[0] = t_start; wl[1] = t_primary; wl[2] = t_end; wl[3] = mx; wl[4] = shadow_iters;
+            wl[5] = n_shadow; wl[6] = sp; wl[7] = ss;
+        }
+    }
     const uint32_t wo = wave_sum(occluded);
     const uint32_t wave_id = blockIdx.x * (kBlock / 64) + wave;
     const uint32_t shard = wave_id % kShards;
@@ -1029,14 +1069,25 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     s->shards_dirty = true;
     if (rows) {                                                      // a rank may own no rows
         if (e0) HIP_TRY(hipEventRecord(e0, stream));
-        const size_t lds = size_t(s->stack_entries) * dev::kBlock * 4;
+        const size_t lds = size_t(s->stack_entries + CERES_STEP_SELECT) * dev::kBlock * 4;
         const dim3 grid(bx, by * frames), block(dev::kBlock);
         if (CERES_FUSED && mode == CERES_MODE_FULL) {
             // one kernel: primary + work-stealing shadow + shading per 8x8 tile
-            const size_t flds = size_t(std::max(s->stack_entries, s->shadow_stack_entries)) * dev::kBlock * 4;
+            const size_t flds = size_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries)) * dev::kBlock * 4;
             P.tile_order = s->d_order;
             P.tiles_x = bx;
             const dim3 fgrid(bx * by * frames);
+            if (stats) {                                             // per-wave diagnostic timeline
+                const size_t waves = size_t(bx) * by * frames * (dev::kBlock / 64);
+                if (s->wave_log_waves < waves) {
+                    dfree(s->d_wave_log);
+                    HIP_TRY(hipMalloc(&s->d_wave_log, waves * 64));
+                    s->wave_log_waves = waves;
+                }
+                HIP_TRY(hipMemsetAsync(s->d_wave_log, 0, waves * 64, stream));
+                P.wave_log = s->d_wave_log;
+                s->last_grid_waves = waves;
+            }
             if (stats) hipLaunchKernelGGL((dev::ceres_fused<true>), fgrid, block, flds, stream, P);
             else hipLaunchKernelGGL((dev::ceres_fused<false>), fgrid, block, flds, stream, P);
             HIP_TRY(hipGetLastError());
@@ -1056,7 +1107,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             // one lane per queued shadow ray (at most one per pixel), grid-stride beyond 8 workgroups/CU
             const size_t want = (size_t(frames) * W * rows + dev::kBlock - 1) / dev::kBlock;
             uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, size_t(s->num_cus) * 8)));
-            const size_t slds = size_t(std::max(s->stack_entries, s->shadow_stack_entries)) * dev::kBlock * 4;
+            const size_t slds = size_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries)) * dev::kBlock * 4;
             if (stats) {
                 const size_t waves = size_t(sgrid) * (dev::kBlock / 64);
                 if (s->wave_log_waves < waves) {
