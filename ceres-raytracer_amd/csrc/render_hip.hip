@@ -42,7 +42,7 @@
 #pragma clang fp contract(off)
 
 #ifndef CERES_STEP_SELECT
-#define CERES_STEP_SELECT 0   // branch-free next-node step in trace() (A/B switch)
+#define CERES_STEP_SELECT 1   // select-based next-node step in trace() (0: the branchy A/B baseline)
 #endif
 
 namespace ceres {
