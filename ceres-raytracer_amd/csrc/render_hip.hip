@@ -131,7 +131,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 // whenever y is not NaN (y is tmin / tmax / a previous robust_max -- never NaN) up to the
 // sign of zero, which no comparison below can observe; likewise robust_min and fminf.  The
 // slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
-template <bool kAnyHit, bool kStats>
+template <bool kAnyHit, bool kStats, int kS = kBlock>
 __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* stk, Hit& best,
                                       uint32_t& n_pairs, uint32_t& n_tests, bool& overflow, Stamps* ss = nullptr) {
     const float tmin = 0.0f;
@@ -157,12 +157,13 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
     unsigned long long c0 = 0, c1 = 0, c2 = 0;
     while (true) {                                                    // :82-123
         if (kStats) ++n_pairs;
+
         if (kStats && ss) c0 = stamp();
         const float4* q = reinterpret_cast<const float4*>(P.pairs + cur);
         const float4 A = q[0], B = q[1], C = q[2];
         const uint4 L = reinterpret_cast<const uint4*>(q)[3];
 #if CERES_STEP_SELECT
-        const uint32_t top = stk[(sp ? sp - 1 : 0) * kBlock];         // popped if this step descends nowhere
+        const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];         // popped if this step descends nowhere
 #endif
         // left bounds A.x A.y | A.z A.w | B.x B.y ; right bounds B.z B.w | C.x C.y | C.z C.w
         const float l0 = __builtin_fmaf(A.x, ix, sx), l1 = __builtin_fmaf(A.y, ix, sx);
@@ -201,7 +202,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         const bool both = go_l && go_r, none = !go_l && !go_r;
         const bool swap = le > re;                                    // near first, ties left (:109-115)
         overflow |= both && sp >= P.stack_entries;
-        stk[(sp < P.stack_entries ? sp : P.stack_entries) * kBlock] = swap ? L.y : L.w;
+        stk[(sp < P.stack_entries ? sp : P.stack_entries) * kS] = swap ? L.y : L.w;
         if (none && sp == 0) { if (kStats && ss) ss->next += stamp() - c2; break; }   // :118-121
         const uint32_t near = both ? (swap ? L.w : L.y) : (go_l ? L.y : L.w);        // :115-117
         cur = none ? top : near;
@@ -210,7 +211,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         if (go_l && go_r) {                                           // near first, ties left (:109-115)
             const bool swap = le > re;
             if (sp >= P.stack_entries) { overflow = true; return have; }
-            stk[sp * kBlock] = swap ? L.y : L.w;
+            stk[sp * kS] = swap ? L.y : L.w;
             ++sp;
             cur = swap ? L.w : L.y;
         } else if (go_l || go_r) {
@@ -218,7 +219,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
         } else {
             if (sp == 0) { if (kStats && ss) ss->next += stamp() - c2; break; }   // :118-121
             --sp;
-            cur = stk[sp * kBlock];
+            cur = stk[sp * kS];
         }
 #endif
         if (kStats && ss) ss->next += stamp() - c2;
@@ -240,13 +241,13 @@ __device__ __forceinline__ N4 load_n4(const Node4* n) {
 __device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 __device__ __forceinline__ uint32_t pick(uint4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 
-template <bool kStats>
+template <bool kStats, int kS = kBlock>
 __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, uint32_t* stk, uint32_t& n_pairs,
                                            uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f, tmax = FLT_MAX;
     if (P.root_leaf_count) {
         Hit h;
-        return trace<true, kStats>(P, o, d, stk, h, n_pairs, n_tests, overflow);
+        return trace<true, kStats, kS>(P, o, d, stk, h, n_pairs, n_tests, overflow);
     }
     auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
     const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
@@ -303,14 +304,14 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, uint32_
             while (rest) {
                 const uint32_t c = __builtin_ctz(rest);
                 rest &= rest - 1;
-                stk[sp * kBlock] = c == 0 ? fst[0] : c == 1 ? fst[1] : c == 2 ? fst[2] : fst[3];
+                stk[sp * kS] = c == 0 ? fst[0] : c == 1 ? fst[1] : c == 2 ? fst[2] : fst[3];
                 ++sp;
             }
             cur = best == 0 ? fst[0] : best == 1 ? fst[1] : best == 2 ? fst[2] : fst[3];
         } else {
             if (sp == 0) break;
             --sp;
-            cur = stk[sp * kBlock];
+            cur = stk[sp * kS];
         }
     }
     return false;
@@ -452,6 +453,10 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
 }
 
+#ifndef CERES_FUSED_WG
+#define CERES_FUSED_WG 64        // fused kernel workgroup: 64 (8x8 tile, default) or 256 (16x16 tile)
+#endif
+static_assert(CERES_FUSED_WG == 256 || CERES_FUSED_WG == 64, "CERES_FUSED_WG must be 64 or 256");
 #ifndef CERES_FUSED
 #define CERES_FUSED 1            // full mode as ONE kernel (ceres_fused) instead of primary + shadow
 #endif
@@ -561,17 +566,19 @@ struct RayWork {
 };
 
 // LDS scratch of the work-stealing loop, per workgroup
-struct StealLds {
-    uint32_t blocked[kBlock];        // pixel of lane tid occluded (set by any piece of its ray)
-    uint32_t mail[kBlock];           // stolen node, by thief rank within the wavefront
-    uint32_t from[kBlock];           // donor lane, by thief rank
+template <int kS>
+struct StealLdsT {
+    uint32_t blocked[kS];            // pixel of lane tid occluded (set by any piece of its ray)
+    uint32_t mail[kS];               // stolen node, by thief rank within the wavefront
+    uint32_t from[kS];               // donor lane, by thief rank
 };
+using StealLds = StealLdsT<kBlock>;
 
 // Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
 // intra-wavefront work stealing; on return L.blocked[tid] holds the lane's answer.  Must be
 // reached by all 64 lanes of the wavefront (it loops on wavefront ballots).
-template <bool kStats>
-__device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, uint32_t* stk, StealLds& L,
+template <bool kStats, int kS = kBlock>
+__device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, uint32_t* stk, StealLdsT<kS>& L,
                                                uint32_t tid, uint32_t lane, uint32_t& n_pairs, uint32_t& n_tests,
                                                bool& overflow, uint32_t* n_iters = nullptr) {
     const float tmin = 0.0f, tmax = FLT_MAX;
@@ -584,13 +591,14 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
     if (P.root_leaf_count) {                                           // single-leaf scene
         if (has_job) {
             Hit h;
-            L.blocked[tid] = trace<true, kStats>(P, w.o, w.d, stk, h, n_pairs, n_tests, overflow) ? 1u : 0u;
+            L.blocked[tid] = trace<true, kStats, kS>(P, w.o, w.d, stk, h, n_pairs, n_tests, overflow) ? 1u : 0u;
         }
         active = false;
     }
     __builtin_amdgcn_wave_barrier();
     while (__ballot(active)) {
         if (kStats && n_iters) ++*n_iters;
+
         if (active && L.blocked[owner]) active = false;                 // another piece found an occluder
         if (active) {
             if (kStats) ++n_pairs;
@@ -638,14 +646,14 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
                 while (rest) {
                     const uint32_t c = __builtin_ctz(rest);
                     rest &= rest - 1;
-                    stk[top * kBlock] = pick(n.fst, c);
+                    stk[top * kS] = pick(n.fst, c);
                     top = top + 1 == cap ? 0 : top + 1;
                     ++cnt;
                 }
                 cur = pick(n.fst, best);
             } else if (cnt) {
                 top = (top == 0 ? cap : top) - 1;
-                cur = stk[top * kBlock];
+                cur = stk[top * kS];
                 --cnt;
             } else {
                 active = false;                                       // this piece is done, no hit
@@ -659,7 +667,7 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
             if (active && cnt > 0) {
                 const uint32_t r = __popcll(donors & lt_mask);
                 if (r < n_idle) {
-                    L.mail[wbase + r] = stk[bot * kBlock];
+                    L.mail[wbase + r] = stk[bot * kS];
                     L.from[wbase + r] = lane;
                     bot = bot + 1 == cap ? 0 : bot + 1;
                     --cnt;
@@ -782,21 +790,25 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
 // own hits with intra-wavefront work stealing (lanes whose pixel missed help the others), then
 // shades.  No shadow-ray queue in HBM, no second launch: the shadow work of early tiles
 // overlaps the primary work of later ones.  Same results as ceres_primary + ceres_shadow.
-template <bool kStats>
-__global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
+template <bool kStats, int kB>
+__global__ __launch_bounds__(kB) void ceres_fused(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ StealLds L;
+    __shared__ StealLdsT<kB> L;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* stk = lds + tid;
-    // 1-D grid over the batch's 16x16 tiles in tile_order (centre of the image first, so the
-    // expensive tiles start early and cheap background tiles fill the end of the launch)
+    // 1-D grid over the batch's tiles in tile_order (centre of the image first, so the
+    // expensive tiles start early and cheap background tiles fill the end of the launch).
+    // kB = 256: a 16x16 tile per workgroup, its four 8x8 quarters one per wavefront;
+    // kB = 64: one 8x8 tile per single-wavefront workgroup, so a long tile holds only its own
+    // LDS and wave slot, never three finished siblings' (LDS is released per workgroup).
+    constexpr uint32_t kTile = kB == 256 ? 16 : 8;
     const uint32_t t = __builtin_amdgcn_readfirstlane(P.tile_order[blockIdx.x]);
     const uint32_t per_frame = P.tiles_x * P.row_blocks_per_frame;
     const uint32_t f = t / per_frame;
     const uint32_t rem = t - f * per_frame;
     const uint32_t by = rem / P.tiles_x, bx = rem - by * P.tiles_x;
-    const uint32_t i = bx * 16 + (wave & 1) * 8 + (lane & 7);
-    const uint32_t lr = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const uint32_t i = bx * kTile + (kB == 256 ? (wave & 1) * 8 : 0) + (lane & 7);
+    const uint32_t lr = by * kTile + (kB == 256 ? (wave >> 1) * 8 : 0) + (lane >> 3);
     const bool active = i < P.W && lr < P.local_rows;
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;
     bool hit = false;
@@ -808,7 +820,7 @@ __global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
     if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
     if (active) {
         const F3 view = primary_dir(P, f, i, global_row(P, lr));
-        hit = trace<false, kStats>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
+        hit = trace<false, kStats, kB>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
             P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
@@ -832,7 +844,7 @@ __global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
     uint64_t t_primary = 0;
     uint32_t prim_pairs = n_pairs, shadow_iters = 0;
     if (kStats && P.wave_log) t_primary = __builtin_amdgcn_s_memrealtime();
-    steal_traverse<kStats>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
+    steal_traverse<kStats, kB>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
     uint32_t occluded = 0;
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
     if (kStats && P.wave_log) {
@@ -843,13 +855,13 @@ __global__ __launch_bounds__(kBlock) void ceres_fused(const KParams P) {
         for (int off = 32; off > 0; off >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), off, 64)));
         const uint32_t sp = wave_sum(prim_pairs), ss = wave_sum(n_pairs - prim_pairs);
         if (lane == 0) {
-            unsigned long long* wl = P.wave_log + 8 * size_t(blockIdx.x * (kBlock / 64) + wave);
+            unsigned long long* wl = P.wave_log + 8 * size_t(blockIdx.x * (kB / 64) + wave);
             wl[0] = t_start; wl[1] = t_primary; wl[2] = t_end; wl[3] = mx; wl[4] = shadow_iters;
             wl[5] = n_shadow; wl[6] = sp; wl[7] = ss;
         }
     }
     const uint32_t wo = wave_sum(occluded);
-    const uint32_t wave_id = blockIdx.x * (kBlock / 64) + wave;
+    const uint32_t wave_id = blockIdx.x * (kB / 64) + wave;
     const uint32_t shard = wave_id % kShards;
     if (lane == 0 && n_shadow) {
         atomicAdd(&P.shards[shard].queued, n_shadow);                  // shadow rays traced
@@ -971,23 +983,26 @@ int ensure_workspace(ceres_scene* s, size_t jobs, size_t px, bool want_px, bool 
     return CERES_OK;
 }
 
-// Centre-first order of a batch's 16x16 tiles for the fused kernel: ascending distance of the
+constexpr uint32_t kFusedWG = CERES_FUSED_WG;
+
+// Centre-first order of a batch's tile x tile tiles for the fused kernel: ascending distance of the
 // tile centre (global pixel coordinates) from the image centre, frames interleaved.  Cached
 // on the scene per (W, H, tiling, frames).
 int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, size_t rows, uint32_t frames,
-                      uint32_t bx, uint32_t by, hipStream_t stream) {
+                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream) {
     const uint64_t key = (uint64_t(W) << 44) ^ (uint64_t(H) << 24) ^ (uint64_t(t.row_block) << 12) ^
-                         (uint64_t(t.rank) << 36) ^ (uint64_t(t.world) << 52) ^ (uint64_t(frames) << 5) ^ rows;
+                         (uint64_t(t.rank) << 36) ^ (uint64_t(t.world) << 52) ^ (uint64_t(frames) << 5) ^ rows ^
+                         (uint64_t(tile) << 60);
     const size_t n = size_t(bx) * by * frames;
     if (key == s->order_key && s->d_order && n <= s->order_cap) return CERES_OK;
     std::vector<std::pair<double, uint32_t>> k(n);
     const double cx = 0.5 * double(W), cy = 0.5 * double(H);
     for (uint32_t f = 0; f < frames; ++f)
         for (uint32_t y = 0; y < by; ++y) {
-            const size_t lr = std::min<size_t>(size_t(y) * 16 + 8, rows - 1);
+            const size_t lr = std::min<size_t>(size_t(y) * tile + tile / 2, rows - 1);
             const size_t j = ((lr / t.row_block) * t.world + t.rank) * t.row_block + lr % t.row_block;
             for (uint32_t x = 0; x < bx; ++x) {
-                const double dx = double(x) * 16 + 8 - cx, dy = double(j) - cy;
+                const double dx = double(x) * tile + tile / 2 - cx, dy = double(j) - cy;
                 const uint32_t id = (f * by + y) * bx + x;
                 k[id] = {dx * dx + dy * dy, id};
             }
@@ -1059,8 +1074,11 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         s->ev_used.push_back(e0); s->ev_used.push_back(e1); s->ev_used.push_back(e2);
         s->ev_fused.push_back(char(CERES_FUSED && mode == CERES_MODE_FULL));
     }
+    // fused kernel tiles: kFusedWG = 256 -> 16x16 per workgroup, 64 -> 8x8
+    constexpr uint32_t ftile = kFusedWG == 256 ? 16 : 8;
+    const uint32_t fbx = uint32_t((W + ftile - 1) / ftile), fby = uint32_t((rows + ftile - 1) / ftile);
     if (CERES_FUSED && mode == CERES_MODE_FULL && rows)
-        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, bx, by, stream)) return rc;
+        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream)) return rc;
     // The shards must start at zero when they are read back (counters) or hold the two-pass
     // shadow queue; the fused kernel without counters only adds to them, so its steady-state
     // frames skip the memset (ceres_finalize re-zeroes them after every counted render).
@@ -1073,12 +1091,13 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         const dim3 grid(bx, by * frames), block(dev::kBlock);
         if (CERES_FUSED && mode == CERES_MODE_FULL) {
             // one kernel: primary + work-stealing shadow + shading per 8x8 tile
-            const size_t flds = size_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries)) * dev::kBlock * 4;
+            const size_t flds = size_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries)) * kFusedWG * 4;
             P.tile_order = s->d_order;
-            P.tiles_x = bx;
-            const dim3 fgrid(bx * by * frames);
+            P.tiles_x = fbx;
+            P.row_blocks_per_frame = fby;
+            const dim3 fgrid(fbx * fby * frames), fblock(kFusedWG);
             if (stats) {                                             // per-wave diagnostic timeline
-                const size_t waves = size_t(bx) * by * frames * (dev::kBlock / 64);
+                const size_t waves = size_t(fbx) * fby * frames * (kFusedWG / 64);
                 if (s->wave_log_waves < waves) {
                     dfree(s->d_wave_log);
                     HIP_TRY(hipMalloc(&s->d_wave_log, waves * 64));
@@ -1088,8 +1107,8 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
                 P.wave_log = s->d_wave_log;
                 s->last_grid_waves = waves;
             }
-            if (stats) hipLaunchKernelGGL((dev::ceres_fused<true>), fgrid, block, flds, stream, P);
-            else hipLaunchKernelGGL((dev::ceres_fused<false>), fgrid, block, flds, stream, P);
+            if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG>), fgrid, fblock, flds, stream, P);
+            else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG>), fgrid, fblock, flds, stream, P);
             HIP_TRY(hipGetLastError());
             if (e1) HIP_TRY(hipEventRecord(e1, stream));
             if (e2) HIP_TRY(hipEventRecord(e2, stream));

@@ -44,7 +44,22 @@ def main():
            "us_per_primary_step_pct": q(prim[chain > 0] / chain[chain > 0]),
            "us_per_shadow_iter_pct": q(shad[iters > 0] / iters[iters > 0]),
            "waves_ending_after_half_span": int((end > 0.5 * end.max()).sum()),
-           "waves_with_shadow": int((hits > 0).sum())}
+           "waves_with_shadow": int((hits > 0).sum()),
+           # lane efficiency: node-pair visits / (64 x the wave's loop trips) per phase, and how
+           # the summed wave-time splits between the phases
+           "primary_lane_eff": round(float(ppairs.sum() / max(1, 64 * chain.sum())), 3),
+           "shadow_lane_eff": round(float(spairs.sum() / max(1, 64 * iters.sum())), 3),
+           "wave_us_primary_sum": round(float(prim.sum()), 1), "wave_us_shadow_sum": round(float(shad.sum()), 1),
+           "wave_us_primary_sum_chain_gt1": round(float(prim[chain > 1].sum()), 1),
+           "primary_steps_sum": int(chain.sum()), "shadow_iters_sum": int(iters.sum())}
+    # waves resident over time (10 samples across the span) and the peak
+    ev = np.concatenate([np.stack([start, np.ones_like(start)], 1), np.stack([end, -np.ones_like(end)], 1)])
+    ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+    conc = np.cumsum(ev[:, 1])
+    out["resident_waves_peak"] = int(conc.max())
+    out["resident_waves_at"] = {f"{f:.1f}": int(conc[np.searchsorted(ev[:, 0], f * end.max(), side="right") - 1])
+                                for f in np.linspace(0.05, 0.95, 10)}
+    out["mean_resident_waves"] = round(float(life.sum() / end.max()), 1)
     top = np.argsort(-end)[:12]
     out["last_to_finish"] = [{"start": round(float(start[i]), 1), "primary": round(float(prim[i]), 1),
                               "shadow": round(float(shad[i]), 1), "chain": int(chain[i]), "shadow_iters": int(iters[i]),
