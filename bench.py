@@ -41,6 +41,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(REPO, "ceres-raytracer_amd")
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md §L2: aggregate over the 8 XCD L2s, ~34.5 TB/s
 
 
 def import_package():
@@ -143,6 +144,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
+    ap.add_argument("--streams", type=int, default=8,
+                    help="HIP streams the steps rotate over (step k on stream k %% S, its own buffers): step k+1 "
+                         "fills the tail of step k")
     args = ap.parse_args()
 
     import torch
@@ -175,38 +179,53 @@ def main():
     mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
     row_block = args.row_block if world > 1 else H
     tiling = pkg.Tiling(row_block, rank, world)
-    gather = D.BatchGather(W, H, row_block, rank, world, frames=F, device=dev, slots=2)
+    S = max(1, args.streams)
+    gather = D.BatchGather(W, H, row_block, rank, world, frames=F, device=dev, slots=max(2, S))
     rows = gather.local_rows
-    d_px = None if args.no_float else torch.empty(F * 3 * W * max(rows, 1), dtype=torch.float32, device=dev)
+    d_px = [None if args.no_float else torch.empty(F * 3 * W * max(rows, 1), dtype=torch.float32, device=dev)
+            for _ in range(S)]
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    pending = [False, False]
+    # steps rotate over S streams, each with its own framebuffers / gather slot: a step's frames
+    # are complete when its stream is, and step k+1's kernel fills the tail of step k (a single
+    # frame ends with a few long wavefronts resident, DESIGN.md "Where the time goes")
+    streams = [stream] if S == 1 else [torch.cuda.Stream(device=dev) for _ in range(S)]
+    slots = max(2, S)
+    pending = [False] * slots
 
-    def render(slot, with_counters=False):
+    def render(slot, st, with_counters=False):
+        px = d_px[slot % S]
         scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=tiling,
-                                  d_pixels=0 if d_px is None else d_px.data_ptr(), d_rgb8=gather.local_ptr(slot),
-                                  d_counters=counters.data_ptr() if with_counters else 0, stream=sh)
+                                  d_pixels=0 if px is None else px.data_ptr(), d_rgb8=gather.local_ptr(slot),
+                                  d_counters=counters.data_ptr() if with_counters else 0, stream=st.cuda_stream)
 
     def step(k):
-        slot = k % 2
-        render(slot)
-        gather.start(slot)
-        prev = 1 - slot
-        if pending[prev]:
-            gather.finish(prev)
-            pending[prev] = False
-        pending[slot] = True
+        slot = k % slots
+        st = streams[k % S]
+        with torch.cuda.stream(st):
+            if pending[slot]:                  # the previous use of this slot (step k - slots)
+                gather.finish(slot)
+                pending[slot] = False
+            render(slot, st)
+            gather.start(slot)
+            pending[slot] = True
+            if S == 1:                         # one stream: complete the previous step's gather now
+                prev = (k - 1) % slots
+                if pending[prev] and prev != slot:
+                    gather.finish(prev)
+                    pending[prev] = False
 
     def drain():
-        for s_ in (0, 1):
-            if pending[s_]:
-                gather.finish(s_)
-                pending[s_] = False
+        for k_ in range(slots):
+            if pending[k_]:
+                with torch.cuda.stream(streams[k_ % S]):
+                    gather.finish(k_)
+                pending[k_] = False
         gather.wait_assembled()
 
     # validation step (not timed): exact counts of the F-frame batch + frame-0 PPM parity on rank 0
-    render(0, with_counters=True)
+    render(0, stream, with_counters=True)
     gather.start(0)
     full = gather.finish(0)
     gather.wait_assembled()
@@ -280,7 +299,10 @@ def main():
                     "algorithmic_bytes_per_launch": nbytes, "mean_launch_ms": round(ms, 5),
                     "kernels_ms": {k: round(v[0], 5) for k, v in kern.items()},
                     "frame_algorithmic_bytes": frame_bytes,
-                    "frame_frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                    "frame_frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    # a scene that fits the XCD L2s (dragon 3.8 MB, bunny 0.8 MB) is served from L2, not HBM
+                    # (traffic << algorithmic bytes): the same bytes against the L2 ceiling
+                    "l2_peak": L2_PEAK_GBS, "l2_frac": round(achieved / L2_PEAK_GBS, 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, cfg, rays_step if F == 1 else meta["exact"]["rays"])
 
@@ -299,7 +321,7 @@ def main():
                        "W": W, "H": H, "frames_per_step": F, "rays_per_step": rays_step, "hits_per_step": hits_step,
                        "row_block": row_block, "parallelism": f"row-interleaved frames x{world}"
                        + (" + one RCCL gather per step to rank 0 (pipelined)" if world > 1 else ""),
-                       "float_framebuffer": d_px is not None},
+                       "float_framebuffer": d_px[0] is not None, "streams": S},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
         }
         print(json.dumps(line), flush=True)

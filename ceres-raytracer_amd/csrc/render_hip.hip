@@ -6,19 +6,18 @@
 // the offset shadow ray (render.hpp:119-138) and smooth Blinn-Phong shading (render.hpp:46-84),
 // plus the PPM quantiser of static.cpp:135-147.
 //
-// Two kernels per batch of frames (DESIGN.md "Kernels"):
-//   ceres_primary  one lane per pixel, 8x8 pixel tile per wavefront (coherent primary rays),
-//                  closest-hit traversal; misses / primary-only pixels are written directly;
-//                  hits are COMPACTED into a sharded shadow-ray queue with a wavefront
-//                  __ballot + popcount prefix (one queue atomic per wavefront), so no lane
-//                  idles on missed pixels while other lanes trace 28-node-pair shadow rays.
-//   ceres_shadow   one lane per queued shadow ray (dense wavefronts), any-hit traversal (only
-//                  the boolean matters, render.hpp:139 -- result-identical to the reference's
-//                  closest-hit with tmax = FLT_MAX), then smooth shading of lit pixels.
+// Full mode (default): ONE kernel per batch of frames, ceres_fused (DESIGN.md "Kernels"): one
+// 64-thread workgroup per 8x8 pixel tile (coherent primary rays), tiles walked centre-first;
+// closest-hit BVH2 traversal per pixel (software-pipelined: the next record is loaded before
+// the step's triangle tests), then the tile's shadow rays with intra-wavefront work stealing
+// over an exact BVH4 collapse (any-hit: only the boolean matters, render.hpp:139), then
+// shading of the lit pixels.  Kept for A/B and the primary-only mode: ceres_primary (hits
+// COMPACTED into a sharded shadow-ray queue with a wavefront __ballot + popcount prefix) and
+// ceres_shadow / ceres_shadow_steal over that queue.
 // A batch is 1..kMaxFrames frames (own camera + sun each, e.g. the anim.cpp:93-110 orbit),
-// each restricted to this rank's rows (ceres_tiling): one launch pair per batch.
-// The traversal stack lives in LDS ([entries][threads], lane-contiguous = bank-conflict
-// free), sized from the BVH depth at scene creation (<= 63 entries for max_depth 64).
+// each restricted to this rank's rows (ceres_tiling).
+// Traversal stacks live in LDS ([entries][lanes], lane-contiguous = bank-conflict free),
+// sized from the BVH at scene creation, 16-bit entries when every node index fits.
 //
 // Numerics: compiled with -ffp-contract=off and correctly rounded f32 div/sqrt, explicit
 // fmaf only where the reference calls fast_multiply_add, x^24 in double-double for std::pow
@@ -43,6 +42,9 @@
 
 #ifndef CERES_STEP_SELECT
 #define CERES_STEP_SELECT 1   // select-based next-node step in trace() (0: the branchy A/B baseline)
+#endif
+#ifndef CERES_PREFETCH_NEXT
+#define CERES_PREFETCH_NEXT 1 // trace(): issue the next record's load before the step's triangle tests
 #endif
 
 namespace ceres {
@@ -131,8 +133,8 @@ __device__ __forceinline__ unsigned long long stamp() {
 // whenever y is not NaN (y is tmin / tmax / a previous robust_max -- never NaN) up to the
 // sign of zero, which no comparison below can observe; likewise robust_min and fminf.  The
 // slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
-template <bool kAnyHit, bool kStats, int kS = kBlock>
-__device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* stk, Hit& best,
+template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t>
+__device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT* stk, Hit& best,
                                       uint32_t& n_pairs, uint32_t& n_tests, bool& overflow, Stamps* ss = nullptr) {
     const float tmin = 0.0f;
     float tmax = FLT_MAX;                                           // ray.hpp:17-21
@@ -153,6 +155,62 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, uint32_t* st
     const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
     const float sx = (-o.x) * ix, sy = (-o.y) * iy, sz = (-o.z) * iz;
     uint32_t sp = 0;
+#if CERES_PREFETCH_NEXT
+    if (!(kStats && ss)) {
+        // Same steps, software-pipelined: the next record (near child or stack top) follows from
+        // this step's box tests alone (the leaf hits only lower tmax for LATER steps, :89-121),
+        // so its load is issued before this step's triangle tests and overlaps them.
+        const float4* q = reinterpret_cast<const float4*>(P.pairs);  // pair of the root's children (:81)
+        float4 A = q[0], B = q[1], C = q[2];
+        uint4 L = reinterpret_cast<const uint4*>(q)[3];
+        while (true) {                                                // :82-123
+            if (kStats) ++n_pairs;
+            const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];
+            const float l0 = __builtin_fmaf(A.x, ix, sx), l1 = __builtin_fmaf(A.y, ix, sx);
+            const float l2 = __builtin_fmaf(A.z, iy, sy), l3 = __builtin_fmaf(A.w, iy, sy);
+            const float l4 = __builtin_fmaf(B.x, iz, sz), l5 = __builtin_fmaf(B.y, iz, sz);
+            const float r0 = __builtin_fmaf(B.z, ix, sx), r1 = __builtin_fmaf(B.w, ix, sx);
+            const float r2 = __builtin_fmaf(C.x, iy, sy), r3 = __builtin_fmaf(C.y, iy, sy);
+            const float r4 = __builtin_fmaf(C.z, iz, sz), r5 = __builtin_fmaf(C.w, iz, sz);
+            const float le = fmaxf(fminf(l0, l1), fmaxf(fminf(l2, l3), fmaxf(fminf(l4, l5), tmin)));
+            const float lx = fminf(fmaxf(l0, l1), fminf(fmaxf(l2, l3), fminf(fmaxf(l4, l5), tmax)));
+            const float re = fmaxf(fminf(r0, r1), fmaxf(fminf(r2, r3), fmaxf(fminf(r4, r5), tmin)));
+            const float rx = fminf(fmaxf(r0, r1), fminf(fmaxf(r2, r3), fminf(fmaxf(r4, r5), tmax)));
+            const bool hit_l = le <= lx, hit_r = re <= rx;
+            const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
+            const bool both = go_l && go_r, none = !go_l && !go_r;
+            const bool swap = le > re;                                // near first, ties left (:109-115)
+            overflow |= both && sp >= P.stack_entries;
+            stk[(sp < P.stack_entries ? sp : P.stack_entries) * kS] = swap ? L.y : L.w;
+            const bool done = none && sp == 0;                        // :118-121
+            const uint32_t near = both ? (swap ? L.w : L.y) : (go_l ? L.y : L.w);   // :115-117
+            const uint32_t nxt = none ? top : near;
+            sp = both ? (sp < P.stack_entries ? sp + 1 : sp) : (none ? (sp ? sp - 1 : 0) : sp);
+            uint32_t k = 0, k_end = 0, k2 = 0, k2_end = 0;
+            if (hit_l && L.x) { k = L.y; k_end = L.y + L.x; }
+            if (hit_r && L.z) { k2 = L.w; k2_end = L.w + L.z; }
+            if (kStats) n_tests += (k_end - k) + (k2_end - k2);
+            float4 nA{}, nB{}, nC{};
+            uint4 nL{};
+            if (!done) {
+                const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
+                nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
+            }
+            while (k < k_end || k2 < k2_end) {
+                const uint32_t idx = k < k_end ? k++ : k2++;
+                float t, u, v;
+                if (tri_test(load_tri(P.tris + idx), o, d, tmin, tmax, t, u, v)) {
+                    best = {idx, t, u, v}; have = true;
+                    if (kAnyHit) return true;
+                    tmax = t;
+                }
+            }
+            if (done) break;
+            A = nA; B = nB; C = nC; L = nL;
+        }
+        return have;
+    }
+#endif
     uint32_t cur = 0;                                                 // pair of the root's children (:81)
     unsigned long long c0 = 0, c1 = 0, c2 = 0;
     while (true) {                                                    // :82-123
@@ -241,8 +299,8 @@ __device__ __forceinline__ N4 load_n4(const Node4* n) {
 __device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 __device__ __forceinline__ uint32_t pick(uint4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 
-template <bool kStats, int kS = kBlock>
-__device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, uint32_t* stk, uint32_t& n_pairs,
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t>
+__device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT* stk, uint32_t& n_pairs,
                                            uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f, tmax = FLT_MAX;
     if (P.root_leaf_count) {
@@ -453,6 +511,17 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
 }
 
+#ifndef CERES_FUSED_MINW
+#define CERES_FUSED_MINW 0       // >0: ask the compiler for this many waves per SIMD (VGPR budget)
+#endif
+#if CERES_FUSED_MINW > 0
+#define CERES_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(CERES_FUSED_MINW)))
+#else
+#define CERES_FUSED_ATTR
+#endif
+#ifndef CERES_STACK16
+#define CERES_STACK16 1          // 16-bit LDS stack entries for scenes with < 65536 pairs and BVH4 nodes
+#endif
 #ifndef CERES_FUSED_WG
 #define CERES_FUSED_WG 64        // fused kernel workgroup: 64 (8x8 tile, default) or 256 (16x16 tile)
 #endif
@@ -577,8 +646,8 @@ using StealLds = StealLdsT<kBlock>;
 // Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
 // intra-wavefront work stealing; on return L.blocked[tid] holds the lane's answer.  Must be
 // reached by all 64 lanes of the wavefront (it loops on wavefront ballots).
-template <bool kStats, int kS = kBlock>
-__device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, uint32_t* stk, StealLdsT<kS>& L,
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t>
+__device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, StkT* stk, StealLdsT<kS>& L,
                                                uint32_t tid, uint32_t lane, uint32_t& n_pairs, uint32_t& n_tests,
                                                bool& overflow, uint32_t* n_iters = nullptr) {
     const float tmin = 0.0f, tmax = FLT_MAX;
@@ -790,12 +859,13 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
 // own hits with intra-wavefront work stealing (lanes whose pixel missed help the others), then
 // shades.  No shadow-ray queue in HBM, no second launch: the shadow work of early tiles
 // overlaps the primary work of later ones.  Same results as ceres_primary + ceres_shadow.
-template <bool kStats, int kB>
-__global__ __launch_bounds__(kB) void ceres_fused(const KParams P) {
+template <bool kStats, int kB, typename StkT>
+__global__ __launch_bounds__(kB) CERES_FUSED_ATTR void ceres_fused(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ StealLdsT<kB> L;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t* stk = lds + tid;
+    // traversal stacks [entry][lane]: 16-bit entries when every node index fits (scene flag)
+    StkT* stk = reinterpret_cast<StkT*>(lds) + tid;
     // 1-D grid over the batch's tiles in tile_order (centre of the image first, so the
     // expensive tiles start early and cheap background tiles fill the end of the launch).
     // kB = 256: a 16x16 tile per workgroup, its four 8x8 quarters one per wavefront;
@@ -1091,7 +1161,9 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         const dim3 grid(bx, by * frames), block(dev::kBlock);
         if (CERES_FUSED && mode == CERES_MODE_FULL) {
             // one kernel: primary + work-stealing shadow + shading per 8x8 tile
-            const size_t flds = size_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries)) * kFusedWG * 4;
+            const bool st16 = CERES_STACK16 && s->n_pairs < 65536 && s->n_nodes4 < 65536;
+            const size_t flds = size_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries)) * kFusedWG *
+                                (st16 ? 2 : 4);
             P.tile_order = s->d_order;
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
@@ -1107,8 +1179,10 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
                 P.wave_log = s->d_wave_log;
                 s->last_grid_waves = waves;
             }
-            if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG>), fgrid, fblock, flds, stream, P);
-            else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG>), fgrid, fblock, flds, stream, P);
+            if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint16_t>), fgrid, fblock, flds, stream, P);
+            else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint32_t>), fgrid, fblock, flds, stream, P);
+            else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint16_t>), fgrid, fblock, flds, stream, P);
+            else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint32_t>), fgrid, fblock, flds, stream, P);
             HIP_TRY(hipGetLastError());
             if (e1) HIP_TRY(hipEventRecord(e1, stream));
             if (e2) HIP_TRY(hipEventRecord(e2, stream));

@@ -69,7 +69,7 @@ def test_gather_reassembles_reference_frame(world, row_block):
     assert q.get(timeout=10) is True
 
 
-def _batch_worker(rank, world, port, W, H, row_block, frames, q):
+def _batch_worker(rank, world, port, W, H, row_block, frames, q, slots=2):
     import sys
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from conftest import import_package as ip
@@ -86,40 +86,56 @@ def _batch_worker(rank, world, port, W, H, row_block, frames, q):
             hdr = len(b"P6 %d %d 255\n" % (W, H))
             bodies.append(np.frombuffer(ppm[hdr:], np.uint8).reshape(H, 3 * W))
         rng = np.random.default_rng(7)
-        while len(bodies) < 2 * frames:
+        steps = 3 * slots                          # bench.py's rotation: step k uses slot k % slots
+        while len(bodies) < steps * frames:
             bodies.append(rng.integers(0, 256, size=(H, 3 * W), dtype=np.uint8))
-        g = D.BatchGather(W, H, row_block, rank, world, frames=frames, device="cpu", slots=2)
+        g = D.BatchGather(W, H, row_block, rank, world, frames=frames, device="cpu", slots=slots)
         rows = D.row_map(H, row_block, world)[rank]
         n = len(rows)
         assert g.local_rows == n
-        for slot in range(2):                      # two steps in flight (double buffering)
-            for f in range(frames):
-                body = bodies[slot * frames + f]
-                for k, j in enumerate(rows):
-                    g.bufs[slot][f * n + n - 1 - k] = torch.from_numpy(body[H - 1 - j].copy())
-            g.start(slot)
         ok = True
-        for slot in range(2):
+        owner = [None] * slots                     # step whose batch a slot holds in flight
+
+        def check(slot):
+            nonlocal ok
             full = g.finish(slot)
+            k = owner[slot]
             if rank == 0:
                 for f in range(frames):
-                    ok &= bool(np.array_equal(full[f].numpy(), bodies[slot * frames + f]))
+                    ok &= bool(np.array_equal(full[f].numpy(), bodies[k * frames + f]))
             else:
                 ok &= full is None
+            owner[slot] = None
+
+        for k in range(steps):                     # up to `slots` steps in flight
+            slot = k % slots
+            if owner[slot] is not None:
+                check(slot)
+            for f in range(frames):
+                body = bodies[k * frames + f]
+                for i, j in enumerate(rows):
+                    g.bufs[slot][f * n + n - 1 - i] = torch.from_numpy(body[H - 1 - j].copy())
+            g.start(slot)
+            owner[slot] = k
+        for slot in range(slots):
+            if owner[slot] is not None:
+                check(slot)
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,row_block,frames", [(2, 16, 2), (3, 7, 3), (4, 16, 4)])
-def test_batch_gather_double_buffered(world, row_block, frames):
-    """F-frame batches (the bench's weak-scaling step), two steps in flight, gloo on CPU."""
+@pytest.mark.parametrize("world,row_block,frames,slots", [(2, 16, 2, 2), (3, 7, 3, 2), (4, 16, 4, 2), (2, 8, 2, 4),
+                                                           (3, 8, 3, 4)])
+def test_batch_gather_double_buffered(world, row_block, frames, slots):
+    """F-frame batches (the bench's weak-scaling step), `slots` steps in flight rotating as in
+    bench.py (the step-stream rotation), gloo on CPU."""
     import_package()
     W, H = 333, 217
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_batch_worker, args=(r, world, port, W, H, row_block, frames, q))
+    procs = [ctx.Process(target=_batch_worker, args=(r, world, port, W, H, row_block, frames, q, slots))
              for r in range(world)]
     for p in procs:
         p.start()
