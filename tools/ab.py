@@ -51,14 +51,37 @@ def main():
         ok[k] = hashlib.sha256(builds[k].ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
     want_px = os.environ.get("AB_FLOAT", "1") == "1"
     res = {k: [] for k in scenes}
-    for _ in range(rounds):
+    n_streams = int(os.environ.get("AB_STREAMS", "0"))
+    if n_streams:
+        # throughput regime (bench.py --streams S): AB_FRAMES frames round-robin over S streams
+        # per round, wall ms per frame
+        import time
+        import torch
+        W, H = cfg["W"], cfg["H"]
+        per = int(os.environ.get("AB_FRAMES", "64"))
+        strs = [torch.cuda.Stream() for _ in range(n_streams)]
+        px = [torch.empty(3 * W * H, dtype=torch.float32, device="cuda") for _ in range(n_streams)]
+        rgb = [torch.empty(3 * W * H, dtype=torch.uint8, device="cuda") for _ in range(n_streams)]
+        b12 = basis[None, :].astype(np.float32)
+        s3 = np.asarray(cfg["sun"], np.float32)[None, :]
+        for _ in range(rounds):
+            for k, sc in scenes.items():
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for f in range(per):
+                    i = f % n_streams
+                    sc.render_batch_device(b12, s3, W, H, mode=mode, d_pixels=px[i].data_ptr() if want_px else 0,
+                                           d_rgb8=rgb[i].data_ptr(), stream=strs[i].cuda_stream)
+                torch.cuda.synchronize()
+                res[k].append((time.perf_counter() - t0) * 1e3 / per)
+    for _ in range(0 if n_streams else rounds):
         for k, sc in scenes.items():
             _, _, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=want_px, want_rgb8=True)
             res[k].append(st["ms"])
     out = {k: {"median_ms": round(float(np.median(r)), 4), "min_ms": round(float(np.min(r)), 4),
                "mrays_s_median": round(meta["exact"]["rays"] / (np.median(r) * 1e3), 1), "parity": ok[k]}
            for k, r in res.items()}
-    print(json.dumps({"config": name, "rounds": rounds, "results": out}))
+    print(json.dumps({"config": name, "rounds": rounds, "streams": n_streams, "results": out}))
 
 
 if __name__ == "__main__":
