@@ -136,8 +136,8 @@ def pmc_traffic(cfg_name, kernel):
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="dragon_1080")
     ap.add_argument("--frames", type=int, default=0, help="orbit frames per step (default: number of GPUs)")
     ap.add_argument("--row-block", type=int, default=8)

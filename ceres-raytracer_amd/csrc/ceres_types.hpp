@@ -107,7 +107,8 @@ struct KParams {
     uint32_t root_leaf_count, root_leaf_first;   // root is a leaf (single_ray_traverser.hpp:72-73)
     uint32_t shard_capacity;                     // jobs per shard
     uint32_t shadow_stack_entries;               // BVH4 traversal stack (shadow kernel)
-    uint32_t tiles_x;                            // 16-pixel column blocks per row (fused kernel)
+    uint32_t tiles_x;                            // tile columns per row (fused kernel)
+    uint32_t lds_entries;                        // fused kernel: LDS stack slots per lane (24-bit planes)
     const uint32_t* tile_order;                  // fused kernel: block -> batch tile (centre first)
     const SiblingPair* pairs;
     const Node4* nodes4;                         // shadow-ray BVH4 over the same leaf slots

@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "ceres_render.h"
@@ -91,6 +92,20 @@ __device__ __forceinline__ float rcp_exact(float x) {
 #endif
 }
 
+// 24-bit LDS stack entries for scenes whose node indices need more than 16 bits but fewer
+// than 24 (C5: 5.3M pairs): a u16 plane + a u8 plane, [entry][lane] each.  3 B per entry
+// instead of 4 keeps a 28-deep stack's LDS under the 6-waves/SIMD budget.
+struct Stk24 {
+    uint16_t* lo;
+    uint8_t* hi;
+    struct Ref {
+        uint16_t* lo; uint8_t* hi;
+        __device__ __forceinline__ operator uint32_t() const { return uint32_t(*lo) | (uint32_t(*hi) << 16); }
+        __device__ __forceinline__ Ref& operator=(uint32_t v) { *lo = uint16_t(v); *hi = uint8_t(v >> 16); return *this; }
+    };
+    __device__ __forceinline__ Ref operator[](uint32_t i) const { return {lo + i, hi + i}; }
+};
+
 // Per-ray hit; closest hit keeps the LAST accepted hit with t <= tmax (intersect_leaf :54-60).
 struct Hit { uint32_t slot; float t, u, v; };
 
@@ -133,8 +148,8 @@ __device__ __forceinline__ unsigned long long stamp() {
 // whenever y is not NaN (y is tmin / tmax / a previous robust_max -- never NaN) up to the
 // sign of zero, which no comparison below can observe; likewise robust_min and fminf.  The
 // slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
-template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t>
-__device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT* stk, Hit& best,
+template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t*>
+__device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hit& best,
                                       uint32_t& n_pairs, uint32_t& n_tests, bool& overflow, Stamps* ss = nullptr) {
     const float tmin = 0.0f;
     float tmax = FLT_MAX;                                           // ray.hpp:17-21
@@ -299,8 +314,8 @@ __device__ __forceinline__ N4 load_n4(const Node4* n) {
 __device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 __device__ __forceinline__ uint32_t pick(uint4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 
-template <bool kStats, int kS = kBlock, typename StkT = uint32_t>
-__device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT* stk, uint32_t& n_pairs,
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t*>
+__device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT stk, uint32_t& n_pairs,
                                            uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f, tmax = FLT_MAX;
     if (P.root_leaf_count) {
@@ -520,6 +535,9 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 #ifndef CERES_STACK16
 #define CERES_STACK16 1          // 16-bit LDS stack entries for scenes with < 65536 pairs and BVH4 nodes
 #endif
+#ifndef CERES_STACK24
+#define CERES_STACK24 1          // 24-bit LDS stack entries for scenes with < 2^24 pairs and BVH4 nodes
+#endif
 #ifndef CERES_FUSED_WG
 #define CERES_FUSED_WG 64        // fused kernel workgroup: 64 (8x8 tile, default) or 256 (16x16 tile)
 #endif
@@ -644,8 +662,8 @@ using StealLds = StealLdsT<kBlock>;
 // Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
 // intra-wavefront work stealing; on return L.blocked[tid] holds the lane's answer.  Must be
 // reached by all 64 lanes of the wavefront (it loops on wavefront ballots).
-template <bool kStats, int kS = kBlock, typename StkT = uint32_t>
-__device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, StkT* stk, StealLdsT<kS>& L,
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t*>
+__device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, StkT stk, StealLdsT<kS>& L,
                                                uint32_t tid, uint32_t lane, uint32_t& n_pairs, uint32_t& n_tests,
                                                bool& overflow, uint32_t* n_iters = nullptr) {
     const float tmin = 0.0f, tmax = FLT_MAX;
@@ -862,8 +880,14 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ StealLdsT<kB> L;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // traversal stacks [entry][lane]: 16-bit entries when every node index fits (scene flag)
-    StkT* stk = reinterpret_cast<StkT*>(lds) + tid;
+    // traversal stacks [entry][lane]: 16-, 24- or 32-bit entries, the narrowest every node index
+    // of the scene fits (host choice)
+    StkT stk;
+    if constexpr (std::is_same<StkT, Stk24>::value)
+        stk = Stk24{reinterpret_cast<uint16_t*>(lds) + tid,
+                    reinterpret_cast<uint8_t*>(lds) + size_t(P.lds_entries) * kB * 2 + tid};
+    else
+        stk = reinterpret_cast<StkT>(lds) + tid;
     // 1-D grid over the batch's tiles in tile_order (centre of the image first, so the
     // expensive tiles start early and cheap background tiles fill the end of the launch).
     // kB = 256: a 16x16 tile per workgroup, its four 8x8 quarters one per wavefront;
@@ -1159,9 +1183,11 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         const dim3 grid(bx, by * frames), block(dev::kBlock);
         if (CERES_FUSED && mode == CERES_MODE_FULL) {
             // one kernel: primary + work-stealing shadow + shading per 8x8 tile
-            const bool st16 = CERES_STACK16 && s->n_pairs < 65536 && s->n_nodes4 < 65536;
-            const size_t flds = size_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries)) * kFusedWG *
-                                (st16 ? 2 : 4);
+            const size_t nmax = std::max(s->n_pairs, s->n_nodes4);
+            const int stw = CERES_STACK16 && nmax < (1u << 16) ? 2 : CERES_STACK24 && nmax < (1u << 24) ? 3 : 4;
+            const bool st16 = stw == 2;
+            P.lds_entries = uint32_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries));
+            const size_t flds = size_t(P.lds_entries) * kFusedWG * stw;
             P.tile_order = s->d_order;
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
@@ -1180,10 +1206,12 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             // small scenes (16-bit stacks, LDS for 7+ waves/SIMD) get a 7-wave VGPR budget: +3.7 % C3
             // frames/s with 8 frames in flight; C5-size scenes keep the unconstrained allocation
             constexpr int w16 = CERES_FUSED_MINW16, w32 = CERES_FUSED_MINW32;
-            if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint16_t, 1>), fgrid, fblock, flds, stream, P);
-            else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint32_t, w32>), fgrid, fblock, flds, stream, P);
-            else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint16_t, w16>), fgrid, fblock, flds, stream, P);
-            else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint32_t, w32>), fgrid, fblock, flds, stream, P);
+            if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint16_t*, 1>), fgrid, fblock, flds, stream, P);
+            else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, dev::Stk24, w32>), fgrid, fblock, flds, stream, P);
+            else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint32_t*, w32>), fgrid, fblock, flds, stream, P);
+            else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint16_t*, w16>), fgrid, fblock, flds, stream, P);
+            else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, dev::Stk24, w32>), fgrid, fblock, flds, stream, P);
+            else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint32_t*, w32>), fgrid, fblock, flds, stream, P);
             HIP_TRY(hipGetLastError());
             if (e1) HIP_TRY(hipEventRecord(e1, stream));
             if (e2) HIP_TRY(hipEventRecord(e2, stream));
