@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "ceres_bvh_build_f64", "ceres_camera_basis_f64", "ceres_orbit_cameras_f64", "ceres_scene_create_f64",
     "ceres_render_f64", "ceres_render_records_f64",
     "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
-    "ceres_render_device", "ceres_render_batch_device", "ceres_render_records", "ceres_tiling_local_rows",
+    "ceres_render_device", "ceres_render_batch_device", "ceres_render_multi_f32", "ceres_device_count", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
 )
@@ -138,6 +138,8 @@ def lib():
     L.ceres_render_device.argtypes = [_vp, _fp, _fp, ctypes.c_int, _sz, _sz, ctypes.POINTER(Tiling), _vp, _vp, _vp, _vp]
     L.ceres_render_batch_device.argtypes = [_vp, ctypes.c_uint32, _fp, _fp, ctypes.c_int, _sz, _sz,
                                             ctypes.POINTER(Tiling), _vp, _vp, _vp, _vp]
+    L.ceres_render_multi_f32.argtypes = [ctypes.POINTER(_vp), ctypes.c_uint32, ctypes.c_uint32, _fp, _fp, ctypes.c_int, _fp,
+                                         ctypes.POINTER(ctypes.c_uint8), _sz, _sz, ctypes.POINTER(_Stats)]
     L.ceres_assemble_rgb8.argtypes = [_vp, _sz, _vp, ctypes.c_uint32, _sz, _sz, ctypes.c_uint32, ctypes.c_uint32, _vp]
     L.ceres_render_records.argtypes = [_vp, _fp, _fp, ctypes.c_int, _sz, _sz, ctypes.POINTER(ctypes.c_int32), _fp,
                                        ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(_Stats)]
@@ -426,6 +428,22 @@ class Scene:
         p, q, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
         _check(lib().ceres_scene_read_timing(self._h, ctypes.byref(p), ctypes.byref(q), ctypes.byref(n)))
         return p.value, q.value, n.value
+
+
+def render_multi(scenes, basis12, sun, W, H, row_block=8, mode=MODE_FULL, want_pixels=True, want_rgb8=True):
+    """ceres_render_multi_f32: one frame split over len(scenes) ranks (one Scene per rank, e.g. one
+    per device) in this process; returns (pixels, rgb8, stats) like Scene.render."""
+    b = np.ascontiguousarray(basis12, np.float32)
+    s = np.ascontiguousarray(sun, np.float32)
+    px = np.empty(3 * W * H, np.float32) if want_pixels else None
+    rgb = np.empty(3 * W * H, np.uint8) if want_rgb8 else None
+    hs = (_vp * len(scenes))(*[sc._h for sc in scenes])
+    st = _Stats()
+    _check(lib().ceres_render_multi_f32(hs, len(scenes), int(row_block), _p(b, ctypes.c_float), _p(s, ctypes.c_float),
+                                        int(mode), _p(px, ctypes.c_float), _p(rgb, ctypes.c_uint8), W, H,
+                                        ctypes.byref(st)))
+    return px, rgb, dict(rays=st.rays, hits=st.hits, primary_rays=st.primary_rays, shadow_rays=st.shadow_rays,
+                         node_pairs=st.node_pairs, tri_tests=st.tri_tests, ms=st.ms)
 
 
 def orbit_cameras(camera, sun, W, H, n_frames, axis=(0, 1, 0), step_deg=None, rotate_first=True, want_dirs=False):

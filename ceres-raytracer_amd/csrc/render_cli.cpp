@@ -9,6 +9,13 @@
 //                [--rotate x|y|z deg] [--size W H] [-o|--out file.ppm] [--primary-only]
 //                [--proc N] [--device D] [--bench reps] [--json]
 //                [--orbit ax ay az step_deg count] [--frames N] [--gpu-bvh] [--double|-d]
+//                [--gpus N] [--row-block R]
+//
+// --gpus N splits every frame over N GPUs of this node in one process: rows
+// are dealt in blocks of R (default 8) rows round-robin to ranks on devices D, D+1, ... (mod
+// the device count, so N > devices reuses devices -- the test mode on a one-GPU box), each
+// rank with its own scene copy; the RGB8 rows are gathered peer-to-peer over xGMI to the first
+// device and assembled there (ceres_render_multi_f32).  The PPM is identical to --gpus 1.
 //
 // --double (anim.cpp's -d, anim.cpp:146-155) runs the whole sequence as render<double>:
 // numbers parsed with strtod, double mesh / BVH / camera, the double GPU kernel.
@@ -47,7 +54,7 @@ struct Opts {
     Num<double> d;
     int rot_axis = -1;
     size_t W = 1920, H = 1080;
-    int mode = CERES_MODE_FULL, proc = 0, device = 0, bench = 0;
+    int mode = CERES_MODE_FULL, proc = 0, device = 0, bench = 0, gpus = 1, row_block = 8;
     bool json = false, gpu_bvh = false, f64 = false;
     int orbit_count = 0, frames = 1;
 };
@@ -57,7 +64,7 @@ int usage() {
                  "usage: render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]\n"
                  "              [--rotate x|y|z deg] [--size W H] [-o out.ppm] [--primary-only] [--proc N]\n"
                  "              [--device D] [--bench reps] [--json] [--orbit ax ay az step_deg count] [--frames N]\n"
-                 "              [--gpu-bvh] [--double]\n");
+                 "              [--gpu-bvh] [--double] [--gpus N] [--row-block R]\n");
     return 2;
 }
 
@@ -97,6 +104,8 @@ bool parse(int argc, char** argv, Opts& o) {
         else if (a == "--primary-only") o.mode = CERES_MODE_PRIMARY;
         else if (a == "--proc") { if (!have(1)) return false; o.proc = std::atoi(argv[++i]); }
         else if (a == "--device") { if (!have(1)) return false; o.device = std::atoi(argv[++i]); }
+        else if (a == "--gpus") { if (!have(1)) return false; o.gpus = std::atoi(argv[++i]); if (o.gpus < 1) return false; }
+        else if (a == "--row-block") { if (!have(1)) return false; o.row_block = std::atoi(argv[++i]); if (o.row_block < 1) return false; }
         else if (a == "--bench") { if (!have(1)) return false; o.bench = std::atoi(argv[++i]); }
         else if (a == "--json") o.json = true;
         else if (a == "--gpu-bvh") o.gpu_bvh = true;
@@ -133,6 +142,10 @@ template <> struct Api<float> {
     static int render(ceres_scene* sc, const float* b, const float* s, int mode, uint8_t* rgb, size_t W, size_t H, ceres_stats* st) {
         return ceres_render_f32(sc, b, s, mode, nullptr, rgb, W, H, st);
     }
+    static int render_multi(ceres_scene* const* sc, uint32_t n, uint32_t rb, const float* b, const float* s, int mode,
+                            uint8_t* rgb, size_t W, size_t H, ceres_stats* st) {
+        return ceres_render_multi_f32(sc, n, rb, b, s, mode, nullptr, rgb, W, H, st);
+    }
 };
 template <> struct Api<double> {
     using Node = uint64_t;
@@ -151,6 +164,11 @@ template <> struct Api<double> {
     }
     static int render(ceres_scene* sc, const double* b, const double* s, int mode, uint8_t* rgb, size_t W, size_t H, ceres_stats* st) {
         return ceres_render_f64(sc, b, s, mode, nullptr, rgb, W, H, st);
+    }
+    static int render_multi(ceres_scene* const*, uint32_t, uint32_t, const double*, const double*, int, uint8_t*, size_t,
+                            size_t, ceres_stats*) {
+        std::fprintf(stderr, "error: --gpus > 1 renders single precision only\n");
+        return CERES_EUNSUPPORTED;
     }
 };
 
@@ -174,14 +192,34 @@ int run(const Opts& o, const Num<S>& v) {
     std::printf("BVH of %zu node(s) and %zu reference(s)\n", n_nodes, n_tri);
 
     ceres_scene* scene = A::scene(tri, n_tri, norm, nodes, n_nodes, prim, o.device);
+    // --gpus N: one scene copy per further rank, on the next devices (mod the device count)
+    std::vector<ceres_scene*> ranks(1, scene);
+    if (scene && o.gpus > 1) {
+        const int ndev = ceres_device_count();
+        for (int r = 1; r < o.gpus && ndev > 0; ++r) {
+            ceres_scene* sr = A::scene(tri, n_tri, norm, nodes, n_nodes, prim, (o.device + r) % ndev);
+            if (!sr) break;
+            ranks.push_back(sr);
+        }
+    }
     ceres_free(nodes); ceres_free(prim); ceres_free(tri); ceres_free(norm);
-    if (!scene) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
+    auto destroy = [&] { for (auto* sr : ranks) ceres_scene_destroy(sr); };
+    if (!scene || int(ranks.size()) != o.gpus) {
+        std::fprintf(stderr, "error: %s\n", ceres_last_error());
+        destroy();
+        return 1;
+    }
+    auto render = [&](const S* basis, const S* sun, uint8_t* rgb, ceres_stats* st) {
+        return o.gpus > 1 ? A::render_multi(ranks.data(), uint32_t(o.gpus), uint32_t(o.row_block), basis, sun, o.mode, rgb,
+                                            o.W, o.H, st)
+                          : A::render(scene, basis, sun, o.mode, rgb, o.W, o.H, st);
+    };
 
     // frame poses: count + k orbit rotations for frame k (count = 0, frames = 1: the plain camera)
     const uint32_t n_pose = uint32_t(o.orbit_count + o.frames);
     std::vector<S> bases(12 * size_t(n_pose)), suns(3 * size_t(n_pose));
     if (A::orbit(v, o.W, o.H, n_pose, bases.data(), suns.data()) != CERES_OK) {
-        std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1;
+        std::fprintf(stderr, "error: %s\n", ceres_last_error()); destroy(); return 1;
     }
     std::vector<uint8_t> rgb(3 * o.W * o.H);
     ceres_stats st{};
@@ -190,18 +228,19 @@ int run(const Opts& o, const Num<S>& v) {
     for (int k = 0; k < o.frames; ++k) {
         const S* basis = bases.data() + 12 * size_t(o.orbit_count + k);
         const S* sun = suns.data() + 3 * size_t(o.orbit_count + k);
-        std::printf("Rendering image %d (%zux%zu) on HIP device %d...\n", k, o.W, o.H, o.device);
+        if (o.gpus > 1) std::printf("Rendering image %d (%zux%zu) on %d HIP ranks from device %d...\n", k, o.W, o.H, o.gpus, o.device);
+        else std::printf("Rendering image %d (%zux%zu) on HIP device %d...\n", k, o.W, o.H, o.device);
         const double t1 = now_s();
-        int rc = A::render(scene, basis, sun, o.mode, rgb.data(), o.W, o.H, &st);
+        int rc = render(basis, sun, rgb.data(), &st);
         const double t2 = now_s();
-        if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1; }
+        if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); destroy(); return 1; }
         std::printf("%g\n", t2 - t1);
         std::printf("Rays: %llu\tHits: %llu\n", (unsigned long long)st.rays, (unsigned long long)st.hits);   // anim.cpp:109
         tot_rays += st.rays;
         for (int r = 0; r < o.bench; ++r) {
             ceres_stats s2{};
-            rc = A::render(scene, basis, sun, o.mode, rgb.data(), o.W, o.H, &s2);
-            if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); ceres_scene_destroy(scene); return 1; }
+            rc = render(basis, sun, rgb.data(), &s2);
+            if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); destroy(); return 1; }
             ms.push_back(s2.ms);
         }
         std::string path = o.out;
@@ -219,7 +258,7 @@ int run(const Opts& o, const Num<S>& v) {
             std::fclose(f);
         } else {
             std::fprintf(stderr, "error: cannot write %s\n", path.c_str());
-            ceres_scene_destroy(scene);
+            destroy();
             return 1;
         }
     }
@@ -232,7 +271,7 @@ int run(const Opts& o, const Num<S>& v) {
                     (unsigned long long)st.rays, (unsigned long long)st.hits, o.W, o.H, st.ms, med,
                     med > 0 ? double(st.rays) / (med * 1e3) : 0.0);
     }
-    ceres_scene_destroy(scene);
+    destroy();
     return 0;
 }
 

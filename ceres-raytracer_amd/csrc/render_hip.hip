@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -1270,6 +1271,11 @@ extern "C" {
 
 const char* ceres_last_error(void) { return error_buffer(); }
 const char* ceres_version(void) { return "ceres-mi355x 0.2 (gfx950)"; }
+int ceres_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return set_error(CERES_EHIP, "hipGetDeviceCount failed");
+    return n;
+}
 const char* ceres_kernel_names(void) {
     return CERES_FUSED ? "ceres_fused,ceres_primary,ceres_finalize,ceres_assemble"
                        : "ceres_primary,ceres_shadow,ceres_finalize,ceres_assemble";
@@ -1468,6 +1474,103 @@ int ceres_render_f32(ceres_scene* s, const float basis12[12], const float sun[3]
     (void)hipEventDestroy(b);
     fill_stats(stats, c, ms);
     if (c[6]) return set_error(CERES_ESTACK, "traversal stack overflow");
+    return CERES_OK;
+}
+
+// Single-process multi-GPU frame (the `./render --gpus N` path): rank r renders its rows
+// (ceres_tiling {row_block, r, world}) on scenes[r]'s device and stream; the RGB8 rows travel
+// to scenes[0]'s device peer-to-peer (hipMemcpyPeerAsync: xGMI between MI355X devices), where
+// ceres_assemble_rgb8 un-interleaves them into the PPM body -- one copy to the host.  Float
+// pixels (optional) come back per rank and are scattered by row on the host.
+int ceres_render_multi_f32(ceres_scene* const* scenes, uint32_t world, uint32_t row_block, const float basis12[12],
+                           const float sun[3], int mode, float* pixels, uint8_t* rgb8, size_t W, size_t H,
+                           ceres_stats* stats) {
+    if (!scenes || world == 0 || row_block == 0 || !basis12 || !sun || (!pixels && !rgb8))
+        return set_error(CERES_EINVAL, "ceres_render_multi_f32: bad argument");
+    for (uint32_t r = 0; r < world; ++r) {
+        if (!scenes[r]) return set_error(CERES_EINVAL, "ceres_render_multi_f32: null scene %u", r);
+        for (uint32_t q = 0; q < r; ++q)
+            if (scenes[q] == scenes[r]) return set_error(CERES_EINVAL, "ceres_render_multi_f32: ranks %u and %u share a scene", q, r);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    ceres_scene* s0 = scenes[0];
+    const size_t row_bytes = 3 * W;
+    const size_t max_rows = local_rows_of(H, row_block, 0, world);       // rank 0 owns the most rows
+    const size_t stride = (max_rows * row_bytes + 255) / 256 * 256;
+    uint8_t* gbuf = nullptr;
+    std::vector<hipEvent_t> done(world, nullptr);
+    auto cleanup = [&] {
+        for (auto e : done) if (e) (void)hipEventDestroy(e);
+        if (gbuf) { (void)hipSetDevice(s0->device); (void)hipFree(gbuf); }
+    };
+    int rc = CERES_OK;
+    if (rgb8) {
+        HIP_TRY(hipSetDevice(s0->device));
+        if (hipMalloc(&gbuf, stride * world) != hipSuccess) return set_error(CERES_ENOMEM, "ceres_render_multi_f32: gather buffer");
+    }
+    for (uint32_t r = 0; r < world && !rc; ++r) {
+        ceres_scene* s = scenes[r];
+        const ceres_tiling t{row_block, r, world};
+        const size_t rows = local_rows_of(H, row_block, r, world);
+        if (hipSetDevice(s->device) != hipSuccess) { rc = set_error(CERES_EHIP, "hipSetDevice(%d)", s->device); break; }
+        // rank 0's buffers also hold the assembled frame: size them for the whole frame up front
+        if ((rc = ensure_workspace(s, 0, r == 0 ? W * H : std::max<size_t>(rows, 1) * W, true, true))) break;
+        if ((rc = launch(s, 1, basis12, sun, mode, W, H, &t, pixels ? s->d_pixels : nullptr, s->d_rgb8, s->d_counters,
+                         s->stream)))
+            break;
+        if (rgb8 && rows &&
+            hipMemcpyPeerAsync(gbuf + r * stride, s0->device, s->d_rgb8, s->device, rows * row_bytes, s->stream) != hipSuccess) {
+            rc = set_error(CERES_EHIP, "ceres_render_multi_f32: peer copy from rank %u", r);
+            break;
+        }
+        if (hipEventCreateWithFlags(&done[r], hipEventDisableTiming) != hipSuccess || hipEventRecord(done[r], s->stream) != hipSuccess)
+            rc = set_error(CERES_EHIP, "ceres_render_multi_f32: event");
+    }
+    if (!rc && rgb8) {
+        (void)hipSetDevice(s0->device);
+        for (uint32_t r = 0; r < world && !rc; ++r)
+            if (hipStreamWaitEvent(s0->stream, done[r], 0) != hipSuccess) rc = set_error(CERES_EHIP, "stream wait");
+        // rank 0's rows were copied out of s0->d_rgb8 earlier on this stream: reuse it as the output
+        if (!rc) rc = ceres_assemble_rgb8(gbuf, stride, s0->d_rgb8, 1, W, H, row_block, world, s0->stream);
+        if (!rc && hipMemcpyAsync(rgb8, s0->d_rgb8, W * H * 3, hipMemcpyDeviceToHost, s0->stream) != hipSuccess)
+            rc = set_error(CERES_EHIP, "ceres_render_multi_f32: copy back");
+    }
+    uint64_t sum[8] = {0};
+    std::vector<float> local;
+    for (uint32_t r = 0; r < world && !rc; ++r) {
+        ceres_scene* s = scenes[r];
+        const size_t rows = local_rows_of(H, row_block, r, world);
+        uint64_t c[8] = {0};
+        (void)hipSetDevice(s->device);
+        if (hipMemcpyAsync(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost, s->stream) != hipSuccess) {
+            rc = set_error(CERES_EHIP, "ceres_render_multi_f32: counters");
+            break;
+        }
+        if (pixels && rows) {
+            local.resize(rows * W * 3);
+            if (hipMemcpyAsync(local.data(), s->d_pixels, local.size() * sizeof(float), hipMemcpyDeviceToHost, s->stream) != hipSuccess) {
+                rc = set_error(CERES_EHIP, "ceres_render_multi_f32: pixels");
+                break;
+            }
+        }
+        if (hipStreamSynchronize(s->stream) != hipSuccess) { rc = set_error(CERES_EHIP, "ceres_render_multi_f32: sync"); break; }
+        for (int k = 0; k < 6; ++k) sum[k] += c[k];
+        sum[6] |= c[6];
+        if (pixels)
+            for (size_t k = 0; k < rows; ++k) {                           // local row k -> global row j
+                const size_t j = ((k / row_block) * world + r) * row_block + k % row_block;
+                std::memcpy(pixels + j * W * 3, local.data() + k * W * 3, W * 3 * sizeof(float));
+            }
+    }
+    if (!rc && rgb8) {
+        (void)hipSetDevice(s0->device);
+        if (hipStreamSynchronize(s0->stream) != hipSuccess) rc = set_error(CERES_EHIP, "ceres_render_multi_f32: sync");
+    }
+    cleanup();
+    if (rc) return rc;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    fill_stats(stats, sum, ms);
+    if (sum[6]) return set_error(CERES_ESTACK, "traversal stack overflow");
     return CERES_OK;
 }
 

@@ -196,6 +196,17 @@ int ceres_render_batch_device(ceres_scene* scene, uint32_t frames, const float* 
  * RCCL gather to rank 0; the reference renders on one host (render.hpp:104). */
 int ceres_assemble_rgb8(const uint8_t* d_gathered, size_t rank_stride_bytes, uint8_t* d_out, uint32_t frames,
                         size_t width, size_t height, uint32_t row_block, uint32_t world, void* stream);
+/* number of HIP devices visible to this process (negative CERES_E* on error) */
+int ceres_device_count(void);
+/* render<float>() of one frame split over `world` GPUs in ONE process (`./render --gpus N`):
+ * scenes[r] (distinct scene objects, one per rank, each on its own device -- or several on one
+ * device for testing) renders rows {row_block, r, world}; the RGB8 rows move peer-to-peer
+ * (xGMI) to scenes[0]'s device and are assembled there.  pixels / rgb8 are HOST buffers as in
+ * ceres_render_f32 (either may be NULL, not both); the frame is identical to a one-GPU render.
+ * stats->ms = wall time of the whole call (render + gather + copy back). */
+int ceres_render_multi_f32(ceres_scene* const* scenes, uint32_t world, uint32_t row_block,
+                           const float basis12[12], const float sun[3], int mode, float* pixels,
+                           uint8_t* rgb8, size_t width, size_t height, ceres_stats* stats);
 /* Per-pixel hit records of one render (host buffers, W*H entries each, pixel = j*W + i):
  * prim = ORIGINAL triangle index of the primary hit or -1 (render.hpp:120), tuv = {t, u, v}
  * of that hit (triangle.hpp:95-115 convention), shadow = -1 (no shadow ray), 0 (lit) or
