@@ -1518,6 +1518,13 @@ int ceres_render_multi_f32(ceres_scene* const* scenes, uint32_t world, uint32_t 
         if ((rc = launch(s, 1, basis12, sun, mode, W, H, &t, pixels ? s->d_pixels : nullptr, s->d_rgb8, s->d_counters,
                          s->stream)))
             break;
+        if (rgb8 && rows && s->device != s0->device) {
+            // direct xGMI access for the copy engine of rank r's device (once per device pair)
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, s->device, s0->device) == hipSuccess && can &&
+                hipDeviceEnablePeerAccess(s0->device, 0) != hipSuccess)
+                (void)hipGetLastError();          // already enabled: clear the sticky error, copy as usual
+        }
         if (rgb8 && rows &&
             hipMemcpyPeerAsync(gbuf + r * stride, s0->device, s->d_rgb8, s->device, rows * row_bytes, s->stream) != hipSuccess) {
             rc = set_error(CERES_EHIP, "ceres_render_multi_f32: peer copy from rank %u", r);
