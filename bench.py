@@ -8,11 +8,13 @@ A step renders F frames (F = --frames, default = number of GPUs): the anim.cpp:7
 the C3 camera + sun about z in 45-degree steps, frame 0 = C3 exactly.  So at N = 1 a step is
 exactly one C3 frame, and at N GPUs a step is N frames -- WEAK scaling, fixed work per GPU.
 Every frame's rows are interleaved over the ranks in blocks of --row-block rows (balanced
-load); each rank renders its rows of all F frames with one ceres_render_batch_device launch
-pair (ceres_primary + ceres_shadow), RGB8 + float framebuffers in HBM, then ONE RCCL gather
-per step brings the F frames' rows to rank 0, where ceres_assemble_rgb8 un-interleaves them
-into F PPM bodies.  The gather/assembly of step k overlaps the render of step k+1 (double
-buffered); the timed region ends when the last step's frames are assembled on rank 0.
+load); each rank renders its rows of all F frames with one ceres_render_batch_device launch,
+RGB8 + float framebuffers in HBM, then ONE RCCL collective per step: by default frame f is
+gathered to rank f (all N per-frame gathers as one all-to-all, so no rank's xGMI ingress carries
+the whole step; ceres_assemble_rgb8_packed un-interleaves each rank's frame), or with
+--collect gather all F frames go to rank 0.  Steps rotate over --streams HIP streams (own
+buffers each): the collective/assembly of step k and the tail of its render overlap later
+steps; the timed region ends when every step's frames are assembled.
 Scene upload, OBJ load and BVH build are outside the timed region, as in the reference
 (static.cpp:129-133).  value = (primary + shadow rays of all F frames) x steps / wall time
 (max over ranks).  One process per GPU (torch.distributed, backend nccl = RCCL).
@@ -144,6 +146,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
+    ap.add_argument("--collect", choices=("exchange", "gather"), default="exchange",
+                    help="N > 1: frame f of a step to rank f in one all-to-all (exchange; needs frames = N) or all "
+                         "frames to rank 0 (gather)")
     ap.add_argument("--streams", type=int, default=8,
                     help="HIP streams the steps rotate over (step k on stream k %% S, its own buffers): step k+1 "
                          "fills the tail of step k")
@@ -163,10 +168,18 @@ def main():
         if world == 1 and args.gpus > 1:
             sys.stderr.write("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)\n")
             return 2
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # CERES_BENCH_SHARE_GPU=1 (rehearsal on a box with fewer GPUs than ranks): rank -> device
+    # local_rank mod device count
+    dev_id = local_rank % torch.cuda.device_count() if os.environ.get("CERES_BENCH_SHARE_GPU") else local_rank
+    torch.cuda.set_device(dev_id)
+    dev = torch.device("cuda", dev_id)
+    local_rank = dev_id
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        backend = os.environ.get("CERES_BENCH_BACKEND", "nccl")      # gloo: shared-GPU rehearsal only
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     W, H = cfg["W"], cfg["H"]
     F = args.frames or world
@@ -180,7 +193,11 @@ def main():
     row_block = args.row_block if world > 1 else H
     tiling = pkg.Tiling(row_block, rank, world)
     S = max(1, args.streams)
-    gather = D.BatchGather(W, H, row_block, rank, world, frames=F, device=dev, slots=max(2, S))
+    exchange = world > 1 and args.collect == "exchange" and F == world
+    if exchange:     # frame f -> rank f: each rank's ingress is (N-1)/N of one frame per step
+        gather = D.FrameExchange(W, H, row_block, rank, world, device=dev, slots=max(2, S))
+    else:            # every frame -> rank 0
+        gather = D.BatchGather(W, H, row_block, rank, world, frames=F, device=dev, slots=max(2, S))
     rows = gather.local_rows
     d_px = [None if args.no_float else torch.empty(F * 3 * W * max(rows, 1), dtype=torch.float32, device=dev)
             for _ in range(S)]
@@ -243,6 +260,21 @@ def main():
             parity = {"frame0_ppm_sha256_matches_reference": sha == meta["ppm_sha256"]["exact"]}
             if F == 1:
                 parity.update(rays_match=rays_step == meta["exact"]["rays"], hits_match=hits_step == meta["exact"]["hits"])
+    if world > 1:
+        # every assembled frame (frame `rank` here with the exchange, all F on rank 0 with the
+        # gather) == the same frame rendered whole on this GPU
+        mine = [(rank, full[0])] if exchange else ([(f, full[f]) for f in range(F)] if rank == 0 else [])
+        solo_rgb = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
+        same = True
+        for f, body in mine:
+            scene.render_device(b12[f], s3[f], W, H, mode=mode, tiling=pkg.Tiling(H, 0, 1),
+                                d_rgb8=solo_rgb.data_ptr(), stream=sh)
+            torch.cuda.synchronize(dev)
+            same &= bool(torch.equal(solo_rgb.view(H, 3 * W), body))
+        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if rank == 0 and parity is not None:
+            parity["all_frames_match_one_gpu_render"] = bool(flag.item())
 
     for k in range(args.warmup):
         step(k)
@@ -320,7 +352,8 @@ def main():
                                    f"{F} orbit frame(s) per step",
                        "W": W, "H": H, "frames_per_step": F, "rays_per_step": rays_step, "hits_per_step": hits_step,
                        "row_block": row_block, "parallelism": f"row-interleaved frames x{world}"
-                       + (" + one RCCL gather per step to rank 0 (pipelined)" if world > 1 else ""),
+                       + ((" + one RCCL all-to-all per step: frame f gathered to rank f (pipelined)" if exchange
+                           else " + one RCCL gather per step to rank 0 (pipelined)") if world > 1 else ""),
                        "float_framebuffer": d_px[0] is not None, "streams": S},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
         }

@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "ceres_bvh_build_f64", "ceres_camera_basis_f64", "ceres_orbit_cameras_f64", "ceres_scene_create_f64",
     "ceres_render_f64", "ceres_render_records_f64",
     "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
-    "ceres_render_device", "ceres_render_batch_device", "ceres_render_multi_f32", "ceres_device_count", "ceres_render_records", "ceres_tiling_local_rows",
+    "ceres_render_device", "ceres_render_batch_device", "ceres_render_multi_f32", "ceres_device_count", "ceres_assemble_rgb8_packed", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
 )
@@ -140,6 +140,7 @@ def lib():
                                             ctypes.POINTER(Tiling), _vp, _vp, _vp, _vp]
     L.ceres_render_multi_f32.argtypes = [ctypes.POINTER(_vp), ctypes.c_uint32, ctypes.c_uint32, _fp, _fp, ctypes.c_int, _fp,
                                          ctypes.POINTER(ctypes.c_uint8), _sz, _sz, ctypes.POINTER(_Stats)]
+    L.ceres_assemble_rgb8_packed.argtypes = [_vp, _vp, ctypes.c_uint32, _sz, _sz, ctypes.c_uint32, ctypes.c_uint32, _vp]
     L.ceres_assemble_rgb8.argtypes = [_vp, _sz, _vp, ctypes.c_uint32, _sz, _sz, ctypes.c_uint32, ctypes.c_uint32, _vp]
     L.ceres_render_records.argtypes = [_vp, _fp, _fp, ctypes.c_int, _sz, _sz, ctypes.POINTER(ctypes.c_int32), _fp,
                                        ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(_Stats)]
@@ -501,6 +502,12 @@ def assemble_rgb8(d_gathered, rank_stride, d_out, frames, W, H, row_block, world
     """ceres_assemble_rgb8 (device pointers): rank-major gathered batch rows -> F PPM bodies."""
     _check(lib().ceres_assemble_rgb8(d_gathered, rank_stride, d_out, int(frames), W, H, int(row_block), int(world),
                                      stream or None))
+
+
+def assemble_rgb8_packed(d_gathered, d_out, frames, W, H, row_block, world, stream=0):
+    """ceres_assemble_rgb8_packed (device pointers): packed rank-major rows -> F PPM bodies."""
+    _check(lib().ceres_assemble_rgb8_packed(d_gathered, d_out, int(frames), W, H, int(row_block), int(world),
+                                            stream or None))
 
 
 def local_rows(H, tiling):

@@ -996,7 +996,9 @@ __device__ __forceinline__ uint32_t rank_rows(uint32_t H, uint32_t rb, uint32_t 
     return mine * rb - (has_last ? nb * rb - H : 0);
 }
 
-template <bool kVec>
+// kPacked: the rank buffers are back to back without padding (an all-to-all's receive
+// buffer): rank r starts at row sum_{p<r} n_p instead of at r * rank_stride bytes.
+template <bool kVec, bool kPacked = false>
 __global__ __launch_bounds__(256) void ceres_assemble(const uint8_t* __restrict__ src, size_t rank_stride,
                                                       uint8_t* __restrict__ dst, uint32_t frames, uint32_t H,
                                                       uint32_t row_bytes, uint32_t rb, uint32_t world) {
@@ -1007,7 +1009,12 @@ __global__ __launch_bounds__(256) void ceres_assemble(const uint8_t* __restrict_
         const uint32_t b = j / rb, r = b % world;
         const uint32_t k = (b / world) * rb + j % rb;
         const uint32_t n = rank_rows(H, rb, r, world);
-        const uint8_t* s = src + r * rank_stride + (size_t(f) * n + (n - 1 - k)) * row_bytes;
+        size_t base = size_t(r) * rank_stride;
+        if (kPacked) {
+            base = 0;
+            for (uint32_t p = 0; p < r; ++p) base += size_t(frames) * rank_rows(H, rb, p, world) * row_bytes;
+        }
+        const uint8_t* s = src + base + (size_t(f) * n + (n - 1 - k)) * row_bytes;
         uint8_t* d = dst + size_t(oy) * row_bytes;
         for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
             if (kVec) reinterpret_cast<uint4*>(d)[u] = reinterpret_cast<const uint4*>(s)[u];
@@ -1446,6 +1453,29 @@ int ceres_assemble_rgb8(const uint8_t* d_gathered, size_t rank_stride_bytes, uin
     else
         hipLaunchKernelGGL(dev::ceres_assemble<false>, grid, dim3(256), 0, st, d_gathered, rank_stride_bytes, d_out,
                            frames, uint32_t(H), row_bytes, row_block, world);
+    HIP_TRY(hipGetLastError());
+    return CERES_OK;
+}
+
+int ceres_assemble_rgb8_packed(const uint8_t* d_gathered, uint8_t* d_out, uint32_t frames, size_t W, size_t H,
+                               uint32_t row_block, uint32_t world, void* stream) {
+    if (!d_gathered || !d_out || frames == 0 || W == 0 || H == 0 || row_block == 0 || world == 0)
+        return set_error(CERES_EINVAL, "ceres_assemble_rgb8_packed: bad argument");
+    if (3 * W > 0xffffffffull || size_t(frames) * H > 0xffffffffull)
+        return set_error(CERES_EINVAL, "ceres_assemble_rgb8_packed: frame too large");
+    const uint32_t row_bytes = uint32_t(3 * W);
+    const bool vec = row_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(d_gathered) % 16 == 0 &&
+                     reinterpret_cast<uintptr_t>(d_out) % 16 == 0;
+    const uint32_t units = vec ? row_bytes / 16 : row_bytes;
+    const dim3 grid(uint32_t(std::min<size_t>((units + 255) / 256, 64)),
+                    uint32_t(std::min<size_t>(size_t(frames) * H, 65535)));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (vec)
+        hipLaunchKernelGGL((dev::ceres_assemble<true, true>), grid, dim3(256), 0, st, d_gathered, size_t(0), d_out, frames,
+                           uint32_t(H), row_bytes, row_block, world);
+    else
+        hipLaunchKernelGGL((dev::ceres_assemble<false, true>), grid, dim3(256), 0, st, d_gathered, size_t(0), d_out, frames,
+                           uint32_t(H), row_bytes, row_block, world);
     HIP_TRY(hipGetLastError());
     return CERES_OK;
 }

@@ -7,8 +7,10 @@ would leave most ranks idle.  A step renders a BATCH of F frames (e.g. the anim.
 every rank renders its rows of all F frames with ONE ceres_render_batch_device launch pair
 into a compact RGB8 buffer (frame-major, local row k of a frame at position n - 1 - k), and
 ONE collective per step -- a gather of those buffers to rank 0 -- brings all F frames there,
-where ceres_assemble_rgb8 un-interleaves them into F PPM bodies.  BatchGather is
-double-buffered: the gather (RCCL stream) and assembly (side stream) of step k overlap the
+where ceres_assemble_rgb8 un-interleaves them into F PPM bodies (BatchGather), or -- the
+bench's default for F = N -- frame f is gathered to rank f, all N gathers as one all-to-all
+(FrameExchange), so no single rank's ingress carries the whole step.  Both are
+multi-buffered: the gather (RCCL stream) and assembly (side stream) of step k overlap the
 render of step k + 1.  The scene is replicated (uploaded per device, outside the timed
 region).  The reference has no distributed code (render.hpp:104 is an OpenMP loop).
 """
@@ -141,6 +143,105 @@ class BatchGather:
         """Make the current stream wait for every issued assembly (end of a timed region)."""
         import torch
         if self.is_dst and self.world > 1 and self.cuda:
+            for s, used in enumerate(self.reused):
+                if used:
+                    torch.cuda.current_stream(self.device).wait_event(self.assembled[s])
+
+
+def packed_row_permutation(H, row_block, world, frames):
+    """batch_row_permutation for PACKED rank buffers (no padding: rank r's frames * n_r rows start
+    right after rank r-1's) -- the receive layout of FrameExchange's all-to-all."""
+    rows = row_map(H, row_block, world)
+    off = np.cumsum([0] + [frames * len(r) for r in rows])
+    src = np.empty(frames * H, np.int64)
+    for f in range(frames):
+        for r, jr in enumerate(rows):
+            n = len(jr)
+            k = np.arange(n)
+            src[f * H + H - 1 - jr] = off[r] + f * n + (n - 1 - k)
+    return src
+
+
+class FrameExchange:
+    """Per-rank RGB8 rows of an N-frame batch (N = world) -> frame f's PPM body on rank f.
+
+    The weak-scaling step renders N frames, every frame's rows dealt over the N ranks; gathering
+    all N frames to rank 0 would make rank 0's xGMI ingress (7 links) carry (N-1)/N of every
+    frame of the step.  Instead frame f is gathered to rank f: all N gathers of a step are one
+    RCCL all-to-all (`all_to_all_single`, rank r's rows of frame f -> rank f), each rank
+    receives (N-1)/N of ONE frame over all its links, and un-interleaves it with
+    ceres_assemble_rgb8_packed on a side stream.  Same slot protocol as BatchGather.
+    """
+
+    def __init__(self, W, H, row_block, rank, world, device="cpu", group=None, slots=2):
+        import torch
+        self.W, self.H, self.rank, self.world, self.group = W, H, rank, world, group
+        self.frames, self.row_block, self.slots = world, row_block, slots
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.rows = [rank_rows(H, row_block, r, world) for r in range(world)]
+        self.local_rows = self.rows[rank]
+        self.maxrows = max(self.rows)
+        self.row_bytes = 3 * W
+        self.bufs = [torch.zeros((world * self.maxrows, self.row_bytes), dtype=torch.uint8, device=self.device)
+                     for _ in range(slots)]
+        self.work = [None] * slots
+        self.is_dst = True                  # every rank assembles one frame
+        if world > 1:
+            self.recv = [torch.zeros((H, self.row_bytes), dtype=torch.uint8, device=self.device) for _ in range(slots)]
+            self.full = [torch.empty((1, H, self.row_bytes), dtype=torch.uint8, device=self.device)
+                         for _ in range(slots)]
+            self.perm = torch.as_tensor(packed_row_permutation(H, row_block, world, 1), device=self.device)
+            self.in_splits = [self.local_rows * self.row_bytes] * world
+            self.out_splits = [n * self.row_bytes for n in self.rows]
+            if self.cuda:
+                self.side = torch.cuda.Stream(device=self.device)
+                self.assembled = [torch.cuda.Event() for _ in range(slots)]
+                self.reused = [False] * slots
+
+    def local_ptr(self, slot=0):
+        return self.bufs[slot].data_ptr()
+
+    def frame_view(self, slot=0):
+        return self.bufs[slot][: self.H].view(1, self.H, self.row_bytes)
+
+    def start(self, slot=0):
+        import torch
+        import torch.distributed as dist
+        if self.world == 1:
+            return
+        if self.cuda and self.reused[slot]:
+            torch.cuda.current_stream(self.device).wait_event(self.assembled[slot])
+        send = self.bufs[slot][: self.world * self.local_rows].view(-1)
+        self.work[slot] = dist.all_to_all_single(self.recv[slot].view(-1), send, self.out_splits, self.in_splits,
+                                                 group=self.group, async_op=True)
+
+    def finish(self, slot=0):
+        """Complete `slot`: returns this rank's frame (frame index = rank) as a (1, H, 3W) PPM
+        body (asynchronously, on the side stream for GPUs)."""
+        import torch
+        if self.world == 1:
+            return self.frame_view(slot)
+        w = self.work[slot]
+        self.work[slot] = None
+        if w is None:
+            raise RuntimeError("FrameExchange.finish without start")
+        w.wait()
+        if not self.cuda:
+            torch.index_select(self.recv[slot], 0, self.perm, out=self.full[slot].view(-1, self.row_bytes))
+            return self.full[slot]
+        import ceres_raytracer_amd as pkg
+        with torch.cuda.stream(self.side):
+            w.wait()
+            pkg.assemble_rgb8_packed(self.recv[slot].data_ptr(), self.full[slot].data_ptr(), 1, self.W, self.H,
+                                     self.row_block, self.world, self.side.cuda_stream)
+            self.assembled[slot].record(self.side)
+        self.reused[slot] = True
+        return self.full[slot]
+
+    def wait_assembled(self):
+        import torch
+        if self.world > 1 and self.cuda:
             for s, used in enumerate(self.reused):
                 if used:
                     torch.cuda.current_stream(self.device).wait_event(self.assembled[s])

@@ -207,6 +207,10 @@ int ceres_device_count(void);
 int ceres_render_multi_f32(ceres_scene* const* scenes, uint32_t world, uint32_t row_block,
                            const float basis12[12], const float sun[3], int mode, float* pixels,
                            uint8_t* rgb8, size_t width, size_t height, ceres_stats* stats);
+/* The same un-interleave for PACKED rank buffers (an all-to-all's receive buffer): rank r's
+ * `frames` x n_r rows start right after rank r-1's, n_r = ceres_tiling_local_rows of rank r. */
+int ceres_assemble_rgb8_packed(const uint8_t* d_gathered, uint8_t* d_out, uint32_t frames, size_t width,
+                               size_t height, uint32_t row_block, uint32_t world, void* stream);
 /* Per-pixel hit records of one render (host buffers, W*H entries each, pixel = j*W + i):
  * prim = ORIGINAL triangle index of the primary hit or -1 (render.hpp:120), tuv = {t, u, v}
  * of that hit (triangle.hpp:95-115 convention), shadow = -1 (no shadow ray), 0 (lit) or

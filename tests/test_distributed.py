@@ -167,3 +167,82 @@ def test_row_map_covers_every_row_once():
                 np.testing.assert_array_equal(allr, np.arange(H))
                 for r in range(world):
                     assert len(rows[r]) == pkg.local_rows(H, pkg.Tiling(rb, r, world))
+
+
+def _exchange_worker(rank, world, port, W, H, row_block, slots, q):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import import_package as ip
+    ip()
+    import torch
+    import torch.distributed as dist
+    import ceres_raytracer_amd.distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(11)
+        steps = 3 * slots
+        bodies = [rng.integers(0, 256, size=(H, 3 * W), dtype=np.uint8) for _ in range(steps * world)]
+        g = D.FrameExchange(W, H, row_block, rank, world, device="cpu", slots=slots)
+        rows = D.row_map(H, row_block, world)[rank]
+        n = len(rows)
+        assert g.local_rows == n
+        ok = True
+        owner = [None] * slots
+
+        def check(slot):
+            nonlocal ok
+            full = g.finish(slot)
+            k = owner[slot]
+            ok &= bool(np.array_equal(full[0].numpy(), bodies[k * world + rank]))   # frame f = rank
+            owner[slot] = None
+
+        for k in range(steps):
+            slot = k % slots
+            if owner[slot] is not None:
+                check(slot)
+            for f in range(world):                   # frame-major, compact (n rows per frame)
+                body = bodies[k * world + f]
+                for i, j in enumerate(rows):
+                    g.bufs[slot][f * n + n - 1 - i] = torch.from_numpy(body[H - 1 - j].copy())
+            g.start(slot)
+            owner[slot] = k
+        for slot in range(slots):
+            if owner[slot] is not None:
+                check(slot)
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,row_block,slots", [(2, 16, 2), (3, 7, 4), (4, 8, 2), (5, 3, 3)])
+def test_frame_exchange_alltoall(world, row_block, slots):
+    """bench.py's default N > 1 collective: frame f of the step's N frames is gathered to rank f
+    (one all-to-all), `slots` steps in flight, gloo on CPU; ragged row counts per rank."""
+    import_package()
+    W, H = 97, 61
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, W, H, row_block, slots, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert all(res.values()), res
+
+
+def test_packed_permutation_matches_padded():
+    """packed_row_permutation = batch_row_permutation with the padding rows squeezed out."""
+    import_package()
+    import ceres_raytracer_amd.distributed as D
+    for H, rb, world, frames in [(61, 3, 5, 1), (217, 16, 4, 3), (1080, 8, 8, 1)]:
+        rows = D.row_map(H, rb, world)
+        maxrows = max(len(r) for r in rows)
+        padded, _ = D.batch_row_permutation(H, rb, world, frames)
+        packed = D.packed_row_permutation(H, rb, world, frames)
+        off = np.cumsum([0] + [frames * len(r) for r in rows])
+        r_of = padded // (frames * maxrows)
+        np.testing.assert_array_equal(packed, off[r_of] + padded % (frames * maxrows))
