@@ -250,6 +250,24 @@ def test_assemble_kernel_matches_permutation(gpu, W, H, row_block, world, frames
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("W,H,row_block,world,frames", [(64, 48, 16, 3, 2), (333, 217, 7, 3, 1), (1920, 1080, 8, 8, 1),
+                                                        (97, 61, 3, 5, 1)])
+def test_assemble_packed_kernel_matches_permutation(gpu, W, H, row_block, world, frames):
+    """ceres_assemble_rgb8_packed (the all-to-all receive layout, no padding) == the host
+    permutation of distributed.py."""
+    import torch
+    pkg = gpu
+    import ceres_raytracer_amd.distributed as D
+    src = D.packed_row_permutation(H, row_block, world, frames)
+    g = torch.randint(0, 256, (frames * H, 3 * W), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((frames, H, 3 * W), dtype=torch.uint8, device="cuda")
+    pkg.assemble_rgb8_packed(g.data_ptr(), out.data_ptr(), frames, W, H, row_block, world,
+                             torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = g[torch.as_tensor(src, device="cuda")].view(frames, H, 3 * W)
+    assert torch.equal(out, ref)
+
+
 def test_batch_rejects_bad_frame_counts(gpu):
     pkg = gpu
     scene, _, _, _ = scene_for(pkg, "tri1")
