@@ -539,6 +539,9 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 #ifndef CERES_STACK24
 #define CERES_STACK24 1          // 24-bit LDS stack entries for scenes with < 2^24 pairs and BVH4 nodes
 #endif
+#ifndef CERES_FUSED_STEAL
+#define CERES_FUSED_STEAL 1      // fused kernel shadow phase: intra-wavefront work stealing (0: one ray per lane)
+#endif
 #ifndef CERES_FUSED_WG
 #define CERES_FUSED_WG 64        // fused kernel workgroup: 64 (8x8 tile, default) or 256 (16x16 tile)
 #endif
@@ -937,7 +940,11 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     uint64_t t_primary = 0;
     uint32_t prim_pairs = n_pairs, shadow_iters = 0;
     if (kStats && P.wave_log) t_primary = __builtin_amdgcn_s_memrealtime();
+#if CERES_FUSED_STEAL
     steal_traverse<kStats, kB>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
+#else
+    L.blocked[tid] = hit && trace_any4<kStats, kB>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
+#endif
     uint32_t occluded = 0;
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
     if (kStats && P.wave_log) {
