@@ -189,7 +189,7 @@ def main():
     b12, s3 = pkg.orbit_cameras(cam, cfg["sun"], W, H, F, axis=axis, step_deg=step_deg, rotate_first=False)
     b12[0] = pinned_basis(meta, cfg, cam)          # frame 0 = C3 (fixture bits)
     s3[0] = np.asarray(cfg["sun"], np.float32)
-    mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
+    mode = pkg.cfg_mode(cfg)
     row_block = args.row_block if world > 1 else H
     tiling = pkg.Tiling(row_block, rank, world)
     S = max(1, args.streams)

@@ -30,6 +30,12 @@ if _PKG not in sys.path:
 import configs  # noqa: E402,F401  (re-exported)
 
 MODE_FULL, MODE_PRIMARY = 0, 1
+MODE_ROBUST = 0x10          # OR-ed: RobustNodeIntersector traversal (node_intersectors.hpp:54-79)
+
+
+def cfg_mode(cfg):
+    """The C-ABI mode of a configs.CONFIGS entry."""
+    return (MODE_PRIMARY if cfg["mode"] == "primary" else MODE_FULL) | (MODE_ROBUST if cfg.get("robust") else 0)
 SCENE_STATS = 1
 
 EXPORTED_SYMBOLS = (

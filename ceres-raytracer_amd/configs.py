@@ -6,7 +6,8 @@ the framebuffer size.  Defaults of the single-frame app are static.cpp:39-47,72-
 
 `mode` is "full" (primary + shadow + smooth shading, render.hpp:104-153) or "primary"
 (primary rays only; pixel = |normalize(tri.n)|, the normal visualisation left commented
-out at render.hpp:123-125 -- the C2 "primary rays only" configuration).
+out at render.hpp:123-125 -- the C2 "primary rays only" configuration).  `robust` traverses
+with the library's RobustNodeIntersector instead of render()'s FastNodeIntersector.
 """
 import os
 
@@ -33,6 +34,7 @@ def _cfg(base, **kw):
     d.setdefault("mode", "full")
     d.setdefault("proc", 0)
     d.setdefault("orbit", None)
+    d.setdefault("robust", False)
     return d
 
 
@@ -62,6 +64,14 @@ CONFIGS = {
     # step_deg about the axis (the bench's weak-scaling frames are this orbit about z)
     "dragon_orbit3_333x217": _cfg(_DRAGON, W=333, H=217, orbit=((0.0, 0.0, 1.0), 45.0, 3)),
     "bunny_orbit7_160x120": _cfg(_BUNNY, W=160, H=120, orbit=((0.0, 1.0, 0.0), 6.0, 7)),
+    # RobustNodeIntersector traversal (node_intersectors.hpp:54-79): odd sizes
+    # give exactly axis-aligned view rays (inverse +-inf), the sun on the y axis axis-aligned
+    # shadow rays; reference = the harness's render loop with the library's robust intersector
+    "dragon_333x217_robust": _cfg(_DRAGON, W=333, H=217, sun=(0.0, -20.0, 0.0), robust=True),
+    "quad_65x49_robust": _cfg(_TINY, obj="@golden/quad.obj", W=65, H=49, robust=True),
+    "degenerate_65x49_robust": _cfg(_TINY, obj="@golden/degenerate.obj", W=65, H=49, robust=True),
+    "bunny_97x61_primary_robust": _cfg(_BUNNY, W=97, H=61, mode="primary", robust=True),
+    "dragon_1080_robust": _cfg(_DRAGON, W=1920, H=1080, robust=True),
 }
 
 # bench.py weak scaling: frame k of a step is the C3 pose rotated k times by 45 degrees about z
@@ -94,4 +104,6 @@ def cli_args(cfg):
         a += ["--orbit", repr(ax), repr(ay), repr(az), repr(step), str(count)]
     if cfg["mode"] == "primary":
         a += ["--primary-only"]
+    if cfg.get("robust"):
+        a += ["--robust"]
     return a

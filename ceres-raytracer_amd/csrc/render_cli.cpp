@@ -9,7 +9,10 @@
 //                [--rotate x|y|z deg] [--size W H] [-o|--out file.ppm] [--primary-only]
 //                [--proc N] [--device D] [--bench reps] [--json]
 //                [--orbit ax ay az step_deg count] [--frames N] [--gpu-bvh] [--double|-d]
-//                [--gpus N] [--row-block R]
+//                [--gpus N] [--row-block R] [--robust]
+//
+// --robust traverses with the library's RobustNodeIntersector (node_intersectors.hpp:54-79,
+// T. Ize's padded-inverse slab test) instead of render()'s FastNodeIntersector.
 //
 // --gpus N splits every frame over N GPUs of this node in one process: rows
 // are dealt in blocks of R (default 8) rows round-robin to ranks on devices D, D+1, ... (mod
@@ -64,7 +67,7 @@ int usage() {
                  "usage: render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]\n"
                  "              [--rotate x|y|z deg] [--size W H] [-o out.ppm] [--primary-only] [--proc N]\n"
                  "              [--device D] [--bench reps] [--json] [--orbit ax ay az step_deg count] [--frames N]\n"
-                 "              [--gpu-bvh] [--double] [--gpus N] [--row-block R]\n");
+                 "              [--gpu-bvh] [--double] [--gpus N] [--row-block R] [--robust]\n");
     return 2;
 }
 
@@ -101,7 +104,8 @@ bool parse(int argc, char** argv, Opts& o) {
             o.W = std::strtoul(argv[i + 1], nullptr, 10); o.H = std::strtoul(argv[i + 2], nullptr, 10); i += 2;
             if (!o.W || !o.H) return false;
         } else if (a == "-o" || a == "--out") { if (!have(1)) return false; o.out = argv[++i]; }
-        else if (a == "--primary-only") o.mode = CERES_MODE_PRIMARY;
+        else if (a == "--primary-only") o.mode = (o.mode & CERES_MODE_ROBUST) | CERES_MODE_PRIMARY;
+        else if (a == "--robust") o.mode |= CERES_MODE_ROBUST;             // RobustNodeIntersector traversal
         else if (a == "--proc") { if (!have(1)) return false; o.proc = std::atoi(argv[++i]); }
         else if (a == "--device") { if (!have(1)) return false; o.device = std::atoi(argv[++i]); }
         else if (a == "--gpus") { if (!have(1)) return false; o.gpus = std::atoi(argv[++i]); if (o.gpus < 1) return false; }

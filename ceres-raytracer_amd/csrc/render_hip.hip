@@ -126,6 +126,58 @@ __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin,
     return false;
 }
 
+// Per-ray constants of the ray-box (slab) test and the test of one box.
+//   kRobust = false: FastNodeIntersector (node_intersectors.hpp:83-103): inv = safe_inverse(d)
+//     (vector.hpp:69-74), s = -o * inv, slab = fma(bound, inv, s) -- restated octant-free below.
+//   kRobust = true: RobustNodeIntersector (node_intersectors.hpp:54-79): inv = 1 / d, entry slab
+//     (near - o) * inv, exit slab (far - o) * pinv with pinv = inv padded by 2 ulps of magnitude
+//     (add_ulp_magnitude, utilities.hpp:102-106); near/far chosen by the ray octant as in
+//     NodeIntersector::intersect (:35-47) -- inv may be +-inf here, so the octant-free min/max
+//     form does not apply: (p - o) * inf is NaN when p == o, which robust_max/min (and
+//     fmaxf/fminf) drop, but a min over both slabs would not.
+template <bool kRobust>
+struct Slab {
+    float ix, iy, iz;          // inverse direction
+    float sx, sy, sz;          // fast: -o * inv; robust: padded inverse
+    F3 o;                      // robust only
+};
+__device__ __forceinline__ float pad_ulps2(float x) {
+    return isfinite(x) ? __uint_as_float(__float_as_uint(x) + 2u) : x;
+}
+template <bool kRobust>
+__device__ __forceinline__ Slab<kRobust> make_slab(F3 o, F3 d) {
+    Slab<kRobust> s;
+    if constexpr (kRobust) {
+        s.ix = 1.0f / d.x; s.iy = 1.0f / d.y; s.iz = 1.0f / d.z;
+        s.sx = pad_ulps2(s.ix); s.sy = pad_ulps2(s.iy); s.sz = pad_ulps2(s.iz);
+    } else {
+        auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
+        s.ix = safe_inv(d.x); s.iy = safe_inv(d.y); s.iz = safe_inv(d.z);
+        s.sx = (-o.x) * s.ix; s.sy = (-o.y) * s.iy; s.sz = (-o.z) * s.iz;
+    }
+    s.o = o;
+    return s;
+}
+// entry / exit distances of one box (bounds lo, hi per axis); hit iff e <= x
+template <bool kRobust>
+__device__ __forceinline__ void slab_box(const Slab<kRobust>& s, float lox, float hix, float loy, float hiy, float loz,
+                                         float hiz, float tmin, float tmax, float& e, float& x) {
+    if constexpr (kRobust) {
+        const bool nx = __float_as_uint(s.ix) >> 31, ny = __float_as_uint(s.iy) >> 31, nz = __float_as_uint(s.iz) >> 31;
+        const float ex = ((nx ? hix : lox) - s.o.x) * s.ix, xx = ((nx ? lox : hix) - s.o.x) * s.sx;
+        const float ey = ((ny ? hiy : loy) - s.o.y) * s.iy, xy = ((ny ? loy : hiy) - s.o.y) * s.sy;
+        const float ez = ((nz ? hiz : loz) - s.o.z) * s.iz, xz = ((nz ? loz : hiz) - s.o.z) * s.sz;
+        e = fmaxf(ex, fmaxf(ey, fmaxf(ez, tmin)));
+        x = fminf(xx, fminf(xy, fminf(xz, tmax)));
+    } else {
+        const float a0 = __builtin_fmaf(lox, s.ix, s.sx), a1 = __builtin_fmaf(hix, s.ix, s.sx);
+        const float b0 = __builtin_fmaf(loy, s.iy, s.sy), b1 = __builtin_fmaf(hiy, s.iy, s.sy);
+        const float c0 = __builtin_fmaf(loz, s.iz, s.sz), c1 = __builtin_fmaf(hiz, s.iz, s.sz);
+        e = fmaxf(fminf(a0, a1), fmaxf(fminf(b0, b1), fmaxf(fminf(c0, c1), tmin)));
+        x = fminf(fmaxf(a0, a1), fminf(fmaxf(b0, b1), fminf(fmaxf(c0, c1), tmax)));
+    }
+}
+
 // Diagnostic section clocks (stats builds only): wave-uniform s_memtime sums per trace().
 struct Stamps { unsigned long long box = 0, leaf = 0, next = 0, iters = 0; };
 __device__ __forceinline__ unsigned long long stamp() {
@@ -149,7 +201,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 // whenever y is not NaN (y is tmin / tmax / a previous robust_max -- never NaN) up to the
 // sign of zero, which no comparison below can observe; likewise robust_min and fminf.  The
 // slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
-template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t*>
+template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false>
 __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hit& best,
                                       uint32_t& n_pairs, uint32_t& n_tests, bool& overflow, Stamps* ss = nullptr) {
     const float tmin = 0.0f;
@@ -167,9 +219,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         }
         return have;
     }
-    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };   // vector.hpp:69-74
-    const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
-    const float sx = (-o.x) * ix, sy = (-o.y) * iy, sz = (-o.z) * iz;
+    const Slab<kRobust> sl = make_slab<kRobust>(o, d);
     uint32_t sp = 0;
 #if CERES_PREFETCH_NEXT
     if (!(kStats && ss)) {
@@ -182,16 +232,9 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         while (true) {                                                // :82-123
             if (kStats) ++n_pairs;
             const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];
-            const float l0 = __builtin_fmaf(A.x, ix, sx), l1 = __builtin_fmaf(A.y, ix, sx);
-            const float l2 = __builtin_fmaf(A.z, iy, sy), l3 = __builtin_fmaf(A.w, iy, sy);
-            const float l4 = __builtin_fmaf(B.x, iz, sz), l5 = __builtin_fmaf(B.y, iz, sz);
-            const float r0 = __builtin_fmaf(B.z, ix, sx), r1 = __builtin_fmaf(B.w, ix, sx);
-            const float r2 = __builtin_fmaf(C.x, iy, sy), r3 = __builtin_fmaf(C.y, iy, sy);
-            const float r4 = __builtin_fmaf(C.z, iz, sz), r5 = __builtin_fmaf(C.w, iz, sz);
-            const float le = fmaxf(fminf(l0, l1), fmaxf(fminf(l2, l3), fmaxf(fminf(l4, l5), tmin)));
-            const float lx = fminf(fmaxf(l0, l1), fminf(fmaxf(l2, l3), fminf(fmaxf(l4, l5), tmax)));
-            const float re = fmaxf(fminf(r0, r1), fmaxf(fminf(r2, r3), fmaxf(fminf(r4, r5), tmin)));
-            const float rx = fminf(fmaxf(r0, r1), fminf(fmaxf(r2, r3), fminf(fmaxf(r4, r5), tmax)));
+            float le, lx, re, rx;
+            slab_box<kRobust>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
+            slab_box<kRobust>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
             const bool hit_l = le <= lx, hit_r = re <= rx;
             const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
             const bool both = go_l && go_r, none = !go_l && !go_r;
@@ -240,16 +283,9 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];         // popped if this step descends nowhere
 #endif
         // left bounds A.x A.y | A.z A.w | B.x B.y ; right bounds B.z B.w | C.x C.y | C.z C.w
-        const float l0 = __builtin_fmaf(A.x, ix, sx), l1 = __builtin_fmaf(A.y, ix, sx);
-        const float l2 = __builtin_fmaf(A.z, iy, sy), l3 = __builtin_fmaf(A.w, iy, sy);
-        const float l4 = __builtin_fmaf(B.x, iz, sz), l5 = __builtin_fmaf(B.y, iz, sz);
-        const float r0 = __builtin_fmaf(B.z, ix, sx), r1 = __builtin_fmaf(B.w, ix, sx);
-        const float r2 = __builtin_fmaf(C.x, iy, sy), r3 = __builtin_fmaf(C.y, iy, sy);
-        const float r4 = __builtin_fmaf(C.z, iz, sz), r5 = __builtin_fmaf(C.w, iz, sz);
-        const float le = fmaxf(fminf(l0, l1), fmaxf(fminf(l2, l3), fmaxf(fminf(l4, l5), tmin)));
-        const float lx = fminf(fmaxf(l0, l1), fminf(fmaxf(l2, l3), fminf(fmaxf(l4, l5), tmax)));
-        const float re = fmaxf(fminf(r0, r1), fmaxf(fminf(r2, r3), fmaxf(fminf(r4, r5), tmin)));
-        const float rx = fminf(fmaxf(r0, r1), fminf(fmaxf(r2, r3), fminf(fmaxf(r4, r5), tmax)));
+        float le, lx, re, rx;
+        slab_box<kRobust>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
+        slab_box<kRobust>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
         const bool hit_l = le <= lx, hit_r = re <= rx;
         if (kStats && ss) { volatile bool keep = hit_l | hit_r; (void)keep; c1 = stamp(); }
         // leaves of this step, left then right (intersect_leaf on each, :89-107), one loop so a
@@ -315,17 +351,15 @@ __device__ __forceinline__ N4 load_n4(const Node4* n) {
 __device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 __device__ __forceinline__ uint32_t pick(uint4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 
-template <bool kStats, int kS = kBlock, typename StkT = uint32_t*>
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false>
 __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT stk, uint32_t& n_pairs,
                                            uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f, tmax = FLT_MAX;
     if (P.root_leaf_count) {
         Hit h;
-        return trace<true, kStats, kS>(P, o, d, stk, h, n_pairs, n_tests, overflow);
+        return trace<true, kStats, kS, StkT, kRobust>(P, o, d, stk, h, n_pairs, n_tests, overflow);
     }
-    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
-    const float ix = safe_inv(d.x), iy = safe_inv(d.y), iz = safe_inv(d.z);
-    const float sx = (-o.x) * ix, sy = (-o.y) * iy, sz = (-o.z) * iz;
+    const Slab<kRobust> sl = make_slab<kRobust>(o, d);
     uint32_t sp = 0, cur = 0;
     while (true) {
         if (kStats) ++n_pairs;
@@ -341,11 +375,7 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
         uint32_t leaf_mask = 0, inner_mask = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const float a0 = __builtin_fmaf(lx[c], ix, sx), a1 = __builtin_fmaf(hx[c], ix, sx);
-            const float b0 = __builtin_fmaf(ly[c], iy, sy), b1 = __builtin_fmaf(hy[c], iy, sy);
-            const float c0 = __builtin_fmaf(lz[c], iz, sz), c1 = __builtin_fmaf(hz[c], iz, sz);
-            e[c] = fmaxf(fminf(a0, a1), fmaxf(fminf(b0, b1), fmaxf(fminf(c0, c1), tmin)));
-            x[c] = fminf(fmaxf(a0, a1), fminf(fmaxf(b0, b1), fminf(fmaxf(c0, c1), tmax)));
+            slab_box<kRobust>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e[c], x[c]);
             const bool hit = e[c] <= x[c] && cnt[c] != kNode4Empty;
             leaf_mask |= (hit && cnt[c] != 0) ? (1u << c) : 0u;
             inner_mask |= (hit && cnt[c] == 0) ? (1u << c) : 0u;
@@ -455,7 +485,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // grid.x: 16-pixel column blocks; grid.y: frames x 16-row blocks of this rank's rows.  The
 // four wavefronts of a workgroup take the 2x2 8x8 tiles of its 16x16 pixels.  Every wavefront
 // is independent: no workgroup barrier, one queue atomic per wavefront.
-template <int kMode, bool kStats>
+template <int kMode, bool kStats, bool kRobust>
 __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -473,7 +503,7 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     F3 shadow_o{0.f, 0.f, 0.f};
     if (active) {
         const F3 view = primary_dir(P, f, i, global_row(P, lr));
-        hit = trace<false, kStats>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
+        hit = trace<false, kStats, kBlock, uint32_t*, kRobust>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
             P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
@@ -559,7 +589,7 @@ static_assert(CERES_FUSED_WG == 256 || CERES_FUSED_WG == 64, "CERES_FUSED_WG mus
 #endif
 
 // ---------------------------------------------------------------- shadow kernel
-template <bool kStats>
+template <bool kStats, bool kRobust>
 __global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -601,10 +631,10 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
         const F3 sun_line = normalize(f3(P.cam[f].sun) - o);        // render.hpp:135
 #ifdef CERES_SHADOW_BVH2
         Hit h2{0, 0.f, 0.f, 0.f};
-        const bool blocked = trace<true, kStats>(P, o, sun_line, stk, h2, n_pairs, n_tests, overflow,
-                                                 kStats ? &stamps : nullptr);
+        const bool blocked = trace<true, kStats, kBlock, uint32_t*, kRobust>(P, o, sun_line, stk, h2, n_pairs, n_tests,
+                                                                             overflow, kStats ? &stamps : nullptr);
 #else
-        const bool blocked = trace_any4<kStats>(P, o, sun_line, stk, n_pairs, n_tests, overflow);
+        const bool blocked = trace_any4<kStats, kBlock, uint32_t*, kRobust>(P, o, sun_line, stk, n_pairs, n_tests, overflow);
 #endif
         if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
         if (blocked) {                                               // render.hpp:147-150
@@ -651,8 +681,10 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
 // together once the wavefront has no work left.  Stacks are per-lane ring buffers in LDS.
 struct RayWork {
     F3 o, d;
-    float ix, iy, iz, sx, sy, sz;
+    float ix, iy, iz, sx, sy, sz;    // Slab<kRobust> constants of the ray
 };
+template <bool kRobust>
+__device__ __forceinline__ Slab<kRobust> slab_of(const RayWork& w) { return {w.ix, w.iy, w.iz, w.sx, w.sy, w.sz, w.o}; }
 
 // LDS scratch of the work-stealing loop, per workgroup
 template <int kS>
@@ -666,7 +698,7 @@ using StealLds = StealLdsT<kBlock>;
 // Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
 // intra-wavefront work stealing; on return L.blocked[tid] holds the lane's answer.  Must be
 // reached by all 64 lanes of the wavefront (it loops on wavefront ballots).
-template <bool kStats, int kS = kBlock, typename StkT = uint32_t*>
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false>
 __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, StkT stk, StealLdsT<kS>& L,
                                                uint32_t tid, uint32_t lane, uint32_t& n_pairs, uint32_t& n_tests,
                                                bool& overflow, uint32_t* n_iters = nullptr) {
@@ -680,7 +712,7 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
     if (P.root_leaf_count) {                                           // single-leaf scene
         if (has_job) {
             Hit h;
-            L.blocked[tid] = trace<true, kStats, kS>(P, w.o, w.d, stk, h, n_pairs, n_tests, overflow) ? 1u : 0u;
+            L.blocked[tid] = trace<true, kStats, kS, StkT, kRobust>(P, w.o, w.d, stk, h, n_pairs, n_tests, overflow) ? 1u : 0u;
         }
         active = false;
     }
@@ -696,11 +728,9 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
             uint32_t leaf_mask = 0, inner_mask = 0;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                const float a0 = __builtin_fmaf(pick(n.lx, c), w.ix, w.sx), a1 = __builtin_fmaf(pick(n.hx, c), w.ix, w.sx);
-                const float b0 = __builtin_fmaf(pick(n.ly, c), w.iy, w.sy), b1 = __builtin_fmaf(pick(n.hy, c), w.iy, w.sy);
-                const float c0 = __builtin_fmaf(pick(n.lz, c), w.iz, w.sz), c1 = __builtin_fmaf(pick(n.hz, c), w.iz, w.sz);
-                e[c] = fmaxf(fminf(a0, a1), fmaxf(fminf(b0, b1), fmaxf(fminf(c0, c1), tmin)));
-                const float x = fminf(fmaxf(a0, a1), fminf(fmaxf(b0, b1), fminf(fmaxf(c0, c1), tmax)));
+                float x;
+                slab_box<kRobust>(slab_of<kRobust>(w), pick(n.lx, c), pick(n.hx, c), pick(n.ly, c), pick(n.hy, c),
+                                  pick(n.lz, c), pick(n.hz, c), tmin, tmax, e[c], x);
                 const uint32_t cn = pick(n.cnt, c);
                 const bool hit = e[c] <= x && cn != kNode4Empty;
                 leaf_mask |= (hit && cn != 0) ? (1u << c) : 0u;
@@ -787,13 +817,13 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
     __builtin_amdgcn_wave_barrier();
 }
 
+template <bool kRobust = false>
 __device__ __forceinline__ RayWork make_shadow_ray(F3 o, F3 sun) {
     RayWork w;
     w.o = o;
     w.d = normalize(sun - o);                                          // render.hpp:135
-    auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
-    w.ix = safe_inv(w.d.x); w.iy = safe_inv(w.d.y); w.iz = safe_inv(w.d.z);
-    w.sx = (-w.o.x) * w.ix; w.sy = (-w.o.y) * w.iy; w.sz = (-w.o.z) * w.iz;
+    const Slab<kRobust> sl = make_slab<kRobust>(o, w.d);
+    w.ix = sl.ix; w.iy = sl.iy; w.iz = sl.iz; w.sx = sl.sx; w.sy = sl.sy; w.sz = sl.sz;
     return w;
 }
 
@@ -813,7 +843,7 @@ __device__ __forceinline__ void finish_pixel(const KParams& P, uint32_t f, uint3
     }
 }
 
-template <bool kStats>
+template <bool kStats, bool kRobust>
 __global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t pre[kShards + 1];
@@ -850,9 +880,9 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
             const float4 J0 = q[0], J1 = q[1];
             pix = __float_as_uint(J0.x); slot = __float_as_uint(J0.y); hu = J0.z; hv = J0.w;
             f = P.frames > 1 ? pix / frame_pixels : 0;
-            w = make_shadow_ray(F3{J1.x, J1.y, J1.z}, f3(P.cam[f].sun));
+            w = make_shadow_ray<kRobust>(F3{J1.x, J1.y, J1.z}, f3(P.cam[f].sun));
         }
-        steal_traverse<kStats>(P, has_job, w, stk, L, tid, lane, n_pairs, n_tests, overflow);
+        steal_traverse<kStats, kBlock, uint32_t*, kRobust>(P, has_job, w, stk, L, tid, lane, n_pairs, n_tests, overflow);
         if (has_job) {                                                   // shade every pixel together
             const uint32_t rem = pix - f * frame_pixels;
             const uint32_t lr = rem / P.W, i = rem - lr * P.W;
@@ -879,7 +909,7 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
 // own hits with intra-wavefront work stealing (lanes whose pixel missed help the others), then
 // shades.  No shadow-ray queue in HBM, no second launch: the shadow work of early tiles
 // overlaps the primary work of later ones.  Same results as ceres_primary + ceres_shadow.
-template <bool kStats, int kB, typename StkT, int kMinW>
+template <bool kStats, int kB, typename StkT, int kMinW, bool kRobust>
 __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ StealLdsT<kB> L;
@@ -916,7 +946,7 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
     if (active) {
         const F3 view = primary_dir(P, f, i, global_row(P, lr));
-        hit = trace<false, kStats, kB>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
+        hit = trace<false, kStats, kB, StkT, kRobust>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
             P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
@@ -933,7 +963,7 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
             F3 p = tr.p0 * h.u + p1 * h.v + p2 * (1 - h.u - h.v);
             const float scale = -0.00001;
             p = p + normal * scale;
-            w = make_shadow_ray(p, f3(P.cam[f].sun));
+            w = make_shadow_ray<kRobust>(p, f3(P.cam[f].sun));
         }
     }
     const uint32_t n_shadow = __popcll(__ballot(hit));
@@ -941,9 +971,9 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     uint32_t prim_pairs = n_pairs, shadow_iters = 0;
     if (kStats && P.wave_log) t_primary = __builtin_amdgcn_s_memrealtime();
 #if CERES_FUSED_STEAL
-    steal_traverse<kStats, kB>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
+    steal_traverse<kStats, kB, StkT, kRobust>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
 #else
-    L.blocked[tid] = hit && trace_any4<kStats, kB>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
+    L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
 #endif
     uint32_t occluded = 0;
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
@@ -1136,6 +1166,8 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     if (s->f64) return set_error(CERES_EINVAL, "scene is double precision: use ceres_render_f64");
     if (frames == 0 || frames > uint32_t(kMaxFrames))
         return set_error(CERES_EINVAL, "render: %u frames per batch (1..%d)", frames, kMaxFrames);
+    const bool robust = (mode & CERES_MODE_ROBUST) != 0;            // RobustNodeIntersector traversal
+    mode &= ~CERES_MODE_ROBUST;
     if (mode != CERES_MODE_FULL && mode != CERES_MODE_PRIMARY) return set_error(CERES_EINVAL, "render: bad mode %d", mode);
     if (W == 0 || H == 0 || W > 65535u * 16u || H > 0xffffffu) return set_error(CERES_EINVAL, "render: bad size %zux%zu", W, H);
     ceres_tiling t{uint32_t(H), 0, 1};
@@ -1221,23 +1253,33 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             // small scenes (16-bit stacks, LDS for 7+ waves/SIMD) get a 7-wave VGPR budget: +3.7 % C3
             // frames/s with 8 frames in flight; C5-size scenes keep the unconstrained allocation
             constexpr int w16 = CERES_FUSED_MINW16, w32 = CERES_FUSED_MINW32;
-            if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint16_t*, 1>), fgrid, fblock, flds, stream, P);
-            else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, dev::Stk24, w32>), fgrid, fblock, flds, stream, P);
-            else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint32_t*, w32>), fgrid, fblock, flds, stream, P);
-            else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint16_t*, w16>), fgrid, fblock, flds, stream, P);
-            else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, dev::Stk24, w32>), fgrid, fblock, flds, stream, P);
-            else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint32_t*, w32>), fgrid, fblock, flds, stream, P);
+            auto fused = [&](auto rt) {
+                constexpr bool R = decltype(rt)::value;
+                if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint16_t*, 1, R>), fgrid, fblock, flds, stream, P);
+                else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, dev::Stk24, w32, R>), fgrid, fblock, flds, stream, P);
+                else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint32_t*, w32, R>), fgrid, fblock, flds, stream, P);
+                else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint16_t*, w16, R>), fgrid, fblock, flds, stream, P);
+                else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, dev::Stk24, w32, R>), fgrid, fblock, flds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint32_t*, w32, R>), fgrid, fblock, flds, stream, P);
+            };
+            if (robust) fused(std::true_type{});
+            else fused(std::false_type{});
             HIP_TRY(hipGetLastError());
             if (e1) HIP_TRY(hipEventRecord(e1, stream));
             if (e2) HIP_TRY(hipEventRecord(e2, stream));
         } else {
-        if (mode == CERES_MODE_PRIMARY) {
-            if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, true>), grid, block, lds, stream, P);
-            else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, false>), grid, block, lds, stream, P);
-        } else {
-            if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, true>), grid, block, lds, stream, P);
-            else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, false>), grid, block, lds, stream, P);
-        }
+        auto primary = [&](auto rt) {
+            constexpr bool R = decltype(rt)::value;
+            if (mode == CERES_MODE_PRIMARY) {
+                if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, true, R>), grid, block, lds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, false, R>), grid, block, lds, stream, P);
+            } else {
+                if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, true, R>), grid, block, lds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, false, R>), grid, block, lds, stream, P);
+            }
+        };
+        if (robust) primary(std::true_type{});
+        else primary(std::false_type{});
         HIP_TRY(hipGetLastError());
         if (e1) HIP_TRY(hipEventRecord(e1, stream));
         if (mode == CERES_MODE_FULL) {
@@ -1255,9 +1297,11 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
                 HIP_TRY(hipMemsetAsync(s->d_wave_log, 0, waves * 64, stream));
                 P.wave_log = s->d_wave_log;
                 s->last_grid_waves = waves;
-                hipLaunchKernelGGL((dev::CERES_SHADOW_FN<true>), dim3(sgrid), block, slds, stream, P);
+                if (robust) hipLaunchKernelGGL((dev::CERES_SHADOW_FN<true, true>), dim3(sgrid), block, slds, stream, P);
+                else hipLaunchKernelGGL((dev::CERES_SHADOW_FN<true, false>), dim3(sgrid), block, slds, stream, P);
             } else {
-                hipLaunchKernelGGL((dev::CERES_SHADOW_FN<false>), dim3(sgrid), block, slds, stream, P);
+                if (robust) hipLaunchKernelGGL((dev::CERES_SHADOW_FN<false, true>), dim3(sgrid), block, slds, stream, P);
+                else hipLaunchKernelGGL((dev::CERES_SHADOW_FN<false, false>), dim3(sgrid), block, slds, stream, P);
             }
             HIP_TRY(hipGetLastError());
         }

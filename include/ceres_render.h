@@ -43,7 +43,10 @@ typedef enum {
 
 typedef enum {
     CERES_MODE_FULL = 0,     /* primary + shadow + smooth shading (render.hpp:104-153) */
-    CERES_MODE_PRIMARY = 1   /* primary rays only; pixel = |normalize(tri.n)| (render.hpp:123-125) */
+    CERES_MODE_PRIMARY = 1,  /* primary rays only; pixel = |normalize(tri.n)| (render.hpp:123-125) */
+    CERES_MODE_ROBUST = 0x10 /* OR-ed flag: traverse with the library's RobustNodeIntersector
+                                (node_intersectors.hpp:54-79) instead of render()'s FastNodeIntersector;
+                                float scenes only */
 } ceres_mode;
 
 typedef struct ceres_scene ceres_scene;

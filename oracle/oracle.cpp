@@ -249,7 +249,7 @@ inline bool tri_hit(const Tri& tr, V3 o, V3 d, float tmin, float tmax, float* t,
 }
 
 // Closest-hit traversal with statistics; returns true on hit.  Stack overflow sets *ovf.
-bool traverse(const Ctx& cx, V3 o, V3 d, Hit* best, uint64_t* pairs, uint64_t* tests, bool* ovf) {
+bool traverse(const Ctx& cx, V3 o, V3 d, Hit* best, uint64_t* pairs, uint64_t* tests, bool* ovf, bool robust = false) {
     float tmin = 0.0f, tmax = FLT_MAX;                                       // ray.hpp:17-21
     bool have = false;
     auto leaf = [&](const Node& n) {                                         // intersect_leaf :43-63
@@ -270,13 +270,25 @@ bool traverse(const Ctx& cx, V3 o, V3 d, Hit* best, uint64_t* pairs, uint64_t* t
     V3 so = {(-o.x) * inv.x, (-o.y) * inv.y, (-o.z) * inv.z};
     auto rmax = [](float x, float y) { return x > y ? x : y; };              // utilities.hpp:57-67
     auto rmin = [](float x, float y) { return x < y ? x : y; };
+    // RobustNodeIntersector (node_intersectors.hpp:54-79): plain inverse, exit slabs scaled by the
+    // inverse padded by 2 ulps of magnitude (add_ulp_magnitude, utilities.hpp:102-106)
+    auto pad2 = [](float x) { uint32_t u; std::memcpy(&u, &x, 4); u += 2; float r; std::memcpy(&r, &u, 4); return std::isfinite(x) ? r : x; };
+    const V3 rinv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    const V3 pinv = {pad2(rinv.x), pad2(rinv.y), pad2(rinv.z)};
     auto box = [&](const Node& n, float* en, float* ex) {                    // node_intersectors.hpp:35-47
-        float e0 = std::fmaf(n.b[0 + oct[0]], inv.x, so.x);
-        float e1 = std::fmaf(n.b[2 + oct[1]], inv.y, so.y);
-        float e2 = std::fmaf(n.b[4 + oct[2]], inv.z, so.z);
-        float x0 = std::fmaf(n.b[1 - oct[0]], inv.x, so.x);
-        float x1 = std::fmaf(n.b[3 - oct[1]], inv.y, so.y);
-        float x2 = std::fmaf(n.b[5 - oct[2]], inv.z, so.z);
+        float e0, e1, e2, x0, x1, x2;
+        if (robust) {                                                        // (p - o) * inv, :70-73
+            e0 = (n.b[0 + oct[0]] - o.x) * rinv.x; x0 = (n.b[1 - oct[0]] - o.x) * pinv.x;
+            e1 = (n.b[2 + oct[1]] - o.y) * rinv.y; x1 = (n.b[3 - oct[1]] - o.y) * pinv.y;
+            e2 = (n.b[4 + oct[2]] - o.z) * rinv.z; x2 = (n.b[5 - oct[2]] - o.z) * pinv.z;
+        } else {
+            e0 = std::fmaf(n.b[0 + oct[0]], inv.x, so.x);
+            e1 = std::fmaf(n.b[2 + oct[1]], inv.y, so.y);
+            e2 = std::fmaf(n.b[4 + oct[2]], inv.z, so.z);
+            x0 = std::fmaf(n.b[1 - oct[0]], inv.x, so.x);
+            x1 = std::fmaf(n.b[3 - oct[1]], inv.y, so.y);
+            x2 = std::fmaf(n.b[5 - oct[2]], inv.z, so.z);
+        }
         *en = rmax(e0, rmax(e1, rmax(e2, tmin)));
         *ex = rmin(x0, rmin(x1, rmin(x2, tmax)));
     };
@@ -522,7 +534,8 @@ void oracle_camera_basis(const float eye[3], const float dir[3], const float up[
 }
 
 // render() (render.hpp:86-156) over the full framebuffer.
-//   mode 0: primary + shadow + smooth shading; mode 1: primary only, pixel = |normalize(n)|
+//   mode 0: primary + shadow + smooth shading; mode 1: primary only, pixel = |normalize(n)|;
+//   | 0x10: RobustNodeIntersector traversal instead of FastNodeIntersector
 //   pixels: 3*W*H floats (row j=0 at the bottom, render.hpp:107) or null
 //   ppm:    3*W*H bytes of the P6 body (rows top-down, static.cpp:137-145) or null
 //   rec_*:  optional per-pixel records (prim -1 on miss; shadow -1 none / 0 lit / 1 occluded)
@@ -532,6 +545,8 @@ int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const u
                   size_t W, size_t H, float* pixels, uint8_t* ppm, int32_t* rec_prim, float* rec_tuv,
                   int8_t* rec_shadow, uint64_t counts[6], int threads, uint32_t* rec_pairs) {
     if (n_tri == 0 || n_nodes == 0) { g_err = "empty scene"; return -1; }
+    const bool robust = (mode & 0x10) != 0;
+    mode &= 0xf;
     Ctx cx{reinterpret_cast<const Tri*>(tri48), reinterpret_cast<const Node*>(nodes32), prim64};
     const auto* norms = reinterpret_cast<const std::array<V3, 3>*>(norm36);
     const V3 E{eye[0], eye[1], eye[2]}, D{basis[0], basis[1], basis[2]}, IU{basis[3], basis[4], basis[5]},
@@ -552,7 +567,7 @@ int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const u
             V3 view = normalize(add(add(mul(IU, u), mul(IV, v)), D));
             Hit h{}; bool ovf = false;
             const uint64_t pp0 = pp, sp0 = sp_;
-            bool hit = traverse(cx, E, view, &h, &pp, &pt, &ovf);
+            bool hit = traverse(cx, E, view, &h, &pp, &pt, &ovf, robust);
             rays++;
             float c[3] = {0.f, 0.f, 0.f};
             int32_t rp = -1; int8_t rs = -1;
@@ -570,7 +585,7 @@ int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const u
                     p = add(p, mul(normal, scale));
                     V3 sun_line = normalize(sub(S, p));
                     Hit h2{};
-                    bool sh = traverse(cx, p, sun_line, &h2, &sp_, &st, &ovf);   // render.hpp:136-138
+                    bool sh = traverse(cx, p, sun_line, &h2, &sp_, &st, &ovf, robust);   // render.hpp:136-138
                     rays++;
                     if (!sh) { smooth_shading(sun_line, norms[h.prim], view, hu, hv, c); rs = 0; }
                     else { hits++; rs = 1; }

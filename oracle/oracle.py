@@ -183,7 +183,8 @@ def render(scene, cfg, basis=None, want_pixels=True, want_ppm=True, want_records
     _check(L.oracle_render(_ptr(tri, ctypes.c_float), _ptr(nor, ctypes.c_float), tri.shape[0],
                            _ptr(nodes, ctypes.c_uint32), nodes.shape[0], _ptr(prim, ctypes.c_uint64),
                            _ptr(eye, ctypes.c_float), _ptr(basis, ctypes.c_float), _ptr(sun, ctypes.c_float),
-                           1 if cfg["mode"] == "primary" else 0, W, H, _ptr(px, ctypes.c_float),
+                           (1 if cfg["mode"] == "primary" else 0) | (0x10 if cfg.get("robust") else 0), W, H,
+                           _ptr(px, ctypes.c_float),
                            _ptr(ppm, ctypes.c_uint8), _ptr(rp, ctypes.c_int32), _ptr(tuv, ctypes.c_float),
                            _ptr(rs, ctypes.c_int8), _ptr(counts, ctypes.c_uint64), int(threads),
                            _ptr(pairs, ctypes.c_uint32)))

@@ -73,7 +73,7 @@ struct Args {
     size_t W = 1920, H = 1080;
     std::string out, fout, records, dump;
     int reps = 1;
-    bool stats = false, primary_only = false;
+    bool stats = false, primary_only = false, robust = false;
     int proc = 0;  // >0: procedural heightfield with proc x proc vertices instead of an OBJ
     Vector3 orbit_axis{0.f, 1.f, 0.f};
     Scalar orbit_step = 0.f; int orbit_count = 0;   // --orbit: anim.cpp camera/sun rotations
@@ -98,6 +98,7 @@ static bool parse(int argc, char** argv, Args& a) {
         else if (s == "--dump") { need(1); a.dump = argv[++i]; }
         else if (s == "--reps") { need(1); a.reps = std::atoi(argv[++i]); }
         else if (s == "--stats") a.stats = true;
+        else if (s == "--robust") a.robust = true;
         else if (s == "--primary-only") a.primary_only = true;
         else if (s == "--proc") { need(1); a.proc = std::atoi(argv[++i]); }
         else if (s == "--orbit") { need(5); a.orbit_axis = v3(argv + i + 1); a.orbit_step = num(argv[i + 4]); a.orbit_count = std::atoi(argv[i + 5]); i += 5; }
@@ -209,7 +210,7 @@ int main(int argc, char** argv) {
 
     std::pair<int, int> rh{0, 0};
     std::vector<double> times;
-    if (!a.primary_only) {
+    if (!a.primary_only && !a.robust) {
         for (int r = 0; r < std::max(1, a.reps); ++r) {
             auto t0 = std::chrono::high_resolution_clock::now();
             rh = render(camera, a.sun, bvh, triangles.data(), tri_norms.data(), pixels.data(), W, H);   // render.hpp:87
@@ -221,13 +222,17 @@ int main(int argc, char** argv) {
     // Replicated per-pixel loop (render.hpp:105-150) with the reference traverser, used for
     // records / stats / primary-only mode; cross-checked against render()'s framebuffer.
     bvh::ClosestPrimitiveIntersector<Bvh, Triangle, false> intersector(bvh, triangles.data());
-    bvh::SingleRayTraverser<Bvh> traverser(bvh);
-    using Stats = bvh::SingleRayTraverser<Bvh>::Statistics;
-    const bool need_loop = a.stats || !a.records.empty() || a.primary_only;
+    // --robust: the same loop with the library's RobustNodeIntersector (node_intersectors.hpp:
+    // 54-79, T. Ize) in place of render()'s default FastNodeIntersector -- the loop is pinned
+    // to render() itself by loop_vs_render_mismatch == 0 in the default mode.
+    bvh::SingleRayTraverser<Bvh> fast_traverser(bvh);
+    bvh::SingleRayTraverser<Bvh, 64, bvh::RobustNodeIntersector<Bvh>> robust_traverser(bvh);
+    const bool need_loop = a.stats || !a.records.empty() || a.primary_only || a.robust;
     size_t prim_pairs = 0, prim_tests = 0, sh_pairs = 0, sh_tests = 0, n_sh = 0, loop_hits = 0, loop_rays = 0;
     size_t mismatch = 0;
     std::vector<PixelRecord> recs;
-    if (need_loop) {
+    auto replicated_loop = [&](auto& traverser) {
+        using Stats = typename std::decay_t<decltype(traverser)>::Statistics;
         if (!a.records.empty()) recs.resize(W * H);
         std::vector<Scalar> px2(3 * W * H);
         #pragma omp parallel for collapse(2) reduction(+: prim_pairs, prim_tests, sh_pairs, sh_tests, n_sh, loop_hits, loop_rays)
@@ -278,9 +283,13 @@ int main(int argc, char** argv) {
                 if (!recs.empty()) recs[W * j + i] = rec;
             }
         }
-        if (a.primary_only) { pixels = px2; rh = {int(loop_rays), int(loop_hits)}; }
+        if (a.primary_only || a.robust) { pixels = px2; rh = {int(loop_rays), int(loop_hits)}; }
         else mismatch = size_t(std::count_if(pixels.begin(), pixels.end(), [&, k = size_t(0)](Scalar x) mutable {
             uint64_t p = 0, q = 0; Scalar y = px2[k++]; std::memcpy(&p, &x, sizeof x); std::memcpy(&q, &y, sizeof y); return p != q; }));
+    };
+    if (need_loop) {
+        if (a.robust) replicated_loop(robust_traverser);
+        else replicated_loop(fast_traverser);
     }
 
     if (!a.records.empty()) {

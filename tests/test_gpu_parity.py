@@ -69,7 +69,7 @@ def test_frame_matches_reference(gpu, name):
     if hexbits(cam.basis(W, H)) != hexbits(basis):
         import warnings
         warnings.warn("host libm camera basis differs from the fixture; rendering with the pinned basis")
-    mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
+    mode = pkg.cfg_mode(cfg)
     px, rgb, st = scene.render(basis, pinned_sun(meta, cfg), W, H, mode=mode)
     assert (st["rays"], st["hits"]) == (meta["exact"]["rays"], meta["exact"]["hits"])
     body = pkg.ppm(W, H, rgb)
@@ -90,7 +90,7 @@ def test_hit_records_match_reference(gpu, name):
     cfg = configs.CONFIGS[name]
     W, H = cfg["W"], cfg["H"]
     scene, _, _, _ = scene_for(pkg, name)
-    mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
+    mode = pkg.cfg_mode(cfg)
     prim, tuv, sh, st = scene.records(pinned_basis(meta, cfg), pinned_sun(meta, cfg), W, H, mode=mode)
     pix = rec["pixel"].astype(np.int64)
     np.testing.assert_array_equal(prim[pix], rec["prim"])
@@ -123,7 +123,7 @@ def test_traversal_statistics_match_reference(gpu, name):
     meta, _, _ = load_golden(name)
     cfg = configs.CONFIGS[name]
     scene, _, _, _ = scene_for(pkg, name, stats=True)
-    mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
+    mode = pkg.cfg_mode(cfg)
     _, _, st = scene.render(pinned_basis(meta, cfg), cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=False)
     ex = meta["exact"]
     if mode == pkg.MODE_PRIMARY:

@@ -67,7 +67,7 @@ def test_device_scene_renders_reference_frame(gpu, name):
         assert m == meta["n_nodes"]
         a, b = scene.info(), host_scene.info()
         assert (a["depth"], a["stack_entries"], a["n_pairs"]) == (b["depth"], b["stack_entries"], b["n_pairs"])
-        mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
+        mode = pkg.cfg_mode(cfg)
         basis, sun = basis_of(meta, cfg), sun_of(meta, cfg)
         px, rgb, st = scene.render(basis, sun, cfg["W"], cfg["H"], mode=mode)
         hpx, _, _ = host_scene.render(basis, sun, cfg["W"], cfg["H"], mode=mode)

@@ -43,7 +43,7 @@ def main():
     mesh, bvh, cam = first.prepare(cfg)
     bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
     basis = np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
-    mode = first.MODE_PRIMARY if cfg["mode"] == "primary" else first.MODE_FULL
+    mode = first.cfg_mode(cfg)
     scenes = {k: m.Scene(mesh, bvh) for k, m in builds.items()}
     ok = {}
     for k, sc in scenes.items():

@@ -34,7 +34,7 @@ def main():
     torch.cuda.set_device(dev)
     mesh, bvh, cam = pkg.prepare(cfg)
     scene = pkg.Scene(mesh, bvh, device=0)
-    mode = pkg.MODE_PRIMARY if cfg["mode"] == "primary" else pkg.MODE_FULL
+    mode = pkg.cfg_mode(cfg)
     axis, step_deg = pkg.configs.BENCH_ORBIT
     stream = torch.cuda.current_stream(dev)
     out = {"config": name, "W": W, "H": H, "reps": reps, "device": torch.cuda.get_device_name(0), "by_n": {}}
