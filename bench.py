@@ -4,14 +4,16 @@
 Workload (default): C3 = dragon.obj 1920x1080, primary + shadow rays, static.cpp camera
 (static.cpp:38-47,72-73) -- the configuration BASELINE.json's metric is quoted on.
 
-A step renders F frames (F = --frames, default = number of GPUs): the anim.cpp:76-88 orbit of
-the C3 camera + sun about z in 45-degree steps, frame 0 = C3 exactly.  So at N = 1 a step is
-exactly one C3 frame, and at N GPUs a step is N frames -- WEAK scaling, fixed work per GPU.
+A step renders F frames (F = --frames, default = 4 per GPU): the anim.cpp:76-88 orbit of the
+C3 camera + sun about z in 45-degree steps, frame 0 = C3 exactly.  So at N = 1 a step is four
+C3-size frames (0, 45, 90, 135 degrees), and at N GPUs a step is 4N frames -- WEAK scaling,
+fixed work per GPU.
 Every frame's rows are interleaved over the ranks in blocks of --row-block rows (balanced
 load); each rank renders its rows of all F frames with one ceres_render_batch_device launch,
-RGB8 + float framebuffers in HBM, then ONE RCCL collective per step: by default frame f is
-gathered to rank f (all N per-frame gathers as one all-to-all, so no rank's xGMI ingress carries
-the whole step; ceres_assemble_rgb8_packed un-interleaves each rank's frame), or with
+RGB8 + float framebuffers in HBM, then ONE RCCL collective per step: by default each frame is
+gathered to one owner rank (rank q owns 4 of the 4N frames; all the per-frame gathers are one
+all-to-all, so no rank's xGMI ingress carries the whole step; ceres_assemble_rgb8_packed
+un-interleaves a rank's frames), or with
 --collect gather all F frames go to rank 0.  Steps rotate over --streams HIP streams (own
 buffers each): the collective/assembly of step k and the tail of its render overlap later
 steps; the timed region ends when every step's frames are assembled.
@@ -141,14 +143,17 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="dragon_1080")
-    ap.add_argument("--frames", type=int, default=0, help="orbit frames per step (default: number of GPUs)")
+    ap.add_argument("--frames", type=int, default=0,
+                    help="orbit frames per step (default: --frames-per-gpu x number of GPUs)")
+    ap.add_argument("--frames-per-gpu", type=int, default=4,
+                    help="frames of work per GPU per step when --frames is not given (weak scaling)")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
     ap.add_argument("--collect", choices=("exchange", "gather"), default="exchange",
-                    help="N > 1: frame f of a step to rank f in one all-to-all (exchange; needs frames = N) or all "
-                         "frames to rank 0 (gather)")
+                    help="N > 1: every frame of a step to one owner rank in one all-to-all (exchange; frames a "
+                         "multiple of N) or all frames to rank 0 (gather)")
     ap.add_argument("--streams", type=int, default=8,
                     help="HIP streams the steps rotate over (step k on stream k %% S, its own buffers): step k+1 "
                          "fills the tail of step k")
@@ -182,20 +187,26 @@ def main():
             dist.init_process_group(backend, rank=rank, world_size=world)
 
     W, H = cfg["W"], cfg["H"]
-    F = args.frames or world
+    F = args.frames or args.frames_per_gpu * world
     mesh, bvh, cam = pkg.prepare(cfg)
     scene = pkg.Scene(mesh, bvh, device=local_rank)
     axis, step_deg = pkg.configs.BENCH_ORBIT
     b12, s3 = pkg.orbit_cameras(cam, cfg["sun"], W, H, F, axis=axis, step_deg=step_deg, rotate_first=False)
     b12[0] = pinned_basis(meta, cfg, cam)          # frame 0 = C3 (fixture bits)
     s3[0] = np.asarray(cfg["sun"], np.float32)
+    exchange = world > 1 and args.collect == "exchange" and F % world == 0
+    if exchange:
+        # batch order for the all-to-all: rank q owns batch frames q*k .. q*k+k-1, which are orbit
+        # frames q, q + N, q + 2N, ... (batch frame 0 = orbit frame 0 = C3)
+        k = F // world
+        order = np.asarray([m * world + q for q in range(world) for m in range(k)])
+        b12, s3 = b12[order], s3[order]
     mode = pkg.cfg_mode(cfg)
     row_block = args.row_block if world > 1 else H
     tiling = pkg.Tiling(row_block, rank, world)
     S = max(1, args.streams)
-    exchange = world > 1 and args.collect == "exchange" and F == world
-    if exchange:     # frame f -> rank f: each rank's ingress is (N-1)/N of one frame per step
-        gather = D.FrameExchange(W, H, row_block, rank, world, device=dev, slots=max(2, S))
+    if exchange:     # each frame to one owner rank: a rank's ingress is (N-1)/N of its k frames per step
+        gather = D.FrameExchange(W, H, row_block, rank, world, frames=F, device=dev, slots=max(2, S))
     else:            # every frame -> rank 0
         gather = D.BatchGather(W, H, row_block, rank, world, frames=F, device=dev, slots=max(2, S))
     rows = gather.local_rows
@@ -258,12 +269,18 @@ def main():
         sha = hashlib.sha256(body).hexdigest()
         if meta is not None:
             parity = {"frame0_ppm_sha256_matches_reference": sha == meta["ppm_sha256"]["exact"]}
-            if F == 1:
-                parity.update(rays_match=rays_step == meta["exact"]["rays"], hits_match=hits_step == meta["exact"]["hits"])
+            # frame 0's ray / hit counts (render.hpp:155) from a counted whole-frame render
+            c0 = torch.zeros(8, dtype=torch.int64, device=dev)
+            scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=pkg.Tiling(H, 0, 1),
+                                d_counters=c0.data_ptr(), stream=sh)
+            torch.cuda.synchronize(dev)
+            c0 = c0.cpu().numpy()
+            parity.update(rays_match=int(c0[0]) == meta["exact"]["rays"], hits_match=int(c0[1]) == meta["exact"]["hits"])
     if world > 1:
-        # every assembled frame (frame `rank` here with the exchange, all F on rank 0 with the
-        # gather) == the same frame rendered whole on this GPU
-        mine = [(rank, full[0])] if exchange else ([(f, full[f]) for f in range(F)] if rank == 0 else [])
+        # every assembled frame (this rank's k frames with the exchange, all F on rank 0 with
+        # the gather) == the same frame rendered whole on this GPU
+        mine = (list(zip(gather.owned_frames(), full)) if exchange
+                else ([(f, full[f]) for f in range(F)] if rank == 0 else []))
         solo_rgb = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
         same = True
         for f, body in mine:

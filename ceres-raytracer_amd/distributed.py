@@ -163,47 +163,59 @@ def packed_row_permutation(H, row_block, world, frames):
 
 
 class FrameExchange:
-    """Per-rank RGB8 rows of an N-frame batch (N = world) -> frame f's PPM body on rank f.
+    """Per-rank RGB8 rows of an F-frame batch (F = k * world) -> frames [q*k, (q+1)*k) of the
+    batch assembled on rank q.
 
-    The weak-scaling step renders N frames, every frame's rows dealt over the N ranks; gathering
-    all N frames to rank 0 would make rank 0's xGMI ingress (7 links) carry (N-1)/N of every
-    frame of the step.  Instead frame f is gathered to rank f: all N gathers of a step are one
-    RCCL all-to-all (`all_to_all_single`, rank r's rows of frame f -> rank f), each rank
-    receives (N-1)/N of ONE frame over all its links, and un-interleaves it with
-    ceres_assemble_rgb8_packed on a side stream.  Same slot protocol as BatchGather.
+    The weak-scaling step renders F frames, every frame's rows dealt over the N ranks;
+    gathering all F frames to rank 0 would make rank 0's xGMI ingress (7 links) carry
+    (N-1)/N of every frame of the step.  Instead each frame is gathered to ONE owner rank (the
+    batch is ordered so that rank q owns the consecutive batch frames q*k .. q*k+k-1): all
+    those gathers are one RCCL all-to-all (`all_to_all_single`, rank r's rows of rank q's
+    frames -> rank q), each rank receives (N-1)/N of k frames over all its links, and
+    un-interleaves them with ceres_assemble_rgb8_packed on a side stream.  Same slot protocol
+    as BatchGather.
     """
 
-    def __init__(self, W, H, row_block, rank, world, device="cpu", group=None, slots=2):
+    def __init__(self, W, H, row_block, rank, world, frames=None, device="cpu", group=None, slots=2):
         import torch
+        frames = world if frames is None else frames
+        if frames % world:
+            raise ValueError("FrameExchange: frames (%d) must be a multiple of world (%d)" % (frames, world))
         self.W, self.H, self.rank, self.world, self.group = W, H, rank, world, group
-        self.frames, self.row_block, self.slots = world, row_block, slots
+        self.frames, self.row_block, self.slots = frames, row_block, slots
+        self.k = frames // world                     # frames each rank assembles
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.rows = [rank_rows(H, row_block, r, world) for r in range(world)]
         self.local_rows = self.rows[rank]
         self.maxrows = max(self.rows)
         self.row_bytes = 3 * W
-        self.bufs = [torch.zeros((world * self.maxrows, self.row_bytes), dtype=torch.uint8, device=self.device)
+        self.bufs = [torch.zeros((frames * self.maxrows, self.row_bytes), dtype=torch.uint8, device=self.device)
                      for _ in range(slots)]
         self.work = [None] * slots
-        self.is_dst = True                  # every rank assembles one frame
+        self.is_dst = True                  # every rank assembles its k frames
         if world > 1:
-            self.recv = [torch.zeros((H, self.row_bytes), dtype=torch.uint8, device=self.device) for _ in range(slots)]
-            self.full = [torch.empty((1, H, self.row_bytes), dtype=torch.uint8, device=self.device)
+            self.recv = [torch.zeros((self.k * H, self.row_bytes), dtype=torch.uint8, device=self.device)
                          for _ in range(slots)]
-            self.perm = torch.as_tensor(packed_row_permutation(H, row_block, world, 1), device=self.device)
-            self.in_splits = [self.local_rows * self.row_bytes] * world
-            self.out_splits = [n * self.row_bytes for n in self.rows]
+            self.full = [torch.empty((self.k, H, self.row_bytes), dtype=torch.uint8, device=self.device)
+                         for _ in range(slots)]
+            self.perm = torch.as_tensor(packed_row_permutation(H, row_block, world, self.k), device=self.device)
+            self.in_splits = [self.k * self.local_rows * self.row_bytes] * world
+            self.out_splits = [self.k * n * self.row_bytes for n in self.rows]
             if self.cuda:
                 self.side = torch.cuda.Stream(device=self.device)
                 self.assembled = [torch.cuda.Event() for _ in range(slots)]
                 self.reused = [False] * slots
 
+    def owned_frames(self):
+        """Batch frame indices this rank assembles (in the order finish() returns them)."""
+        return list(range(self.rank * self.k, (self.rank + 1) * self.k))
+
     def local_ptr(self, slot=0):
         return self.bufs[slot].data_ptr()
 
     def frame_view(self, slot=0):
-        return self.bufs[slot][: self.H].view(1, self.H, self.row_bytes)
+        return self.bufs[slot][: self.frames * self.H].view(self.frames, self.H, self.row_bytes)
 
     def start(self, slot=0):
         import torch
@@ -212,13 +224,13 @@ class FrameExchange:
             return
         if self.cuda and self.reused[slot]:
             torch.cuda.current_stream(self.device).wait_event(self.assembled[slot])
-        send = self.bufs[slot][: self.world * self.local_rows].view(-1)
+        send = self.bufs[slot][: self.frames * self.local_rows].view(-1)
         self.work[slot] = dist.all_to_all_single(self.recv[slot].view(-1), send, self.out_splits, self.in_splits,
                                                  group=self.group, async_op=True)
 
     def finish(self, slot=0):
-        """Complete `slot`: returns this rank's frame (frame index = rank) as a (1, H, 3W) PPM
-        body (asynchronously, on the side stream for GPUs)."""
+        """Complete `slot`: returns this rank's k frames (batch frames owned_frames()) as
+        (k, H, 3W) PPM bodies (asynchronously, on the side stream for GPUs)."""
         import torch
         if self.world == 1:
             return self.frame_view(slot)
@@ -233,7 +245,7 @@ class FrameExchange:
         import ceres_raytracer_amd as pkg
         with torch.cuda.stream(self.side):
             w.wait()
-            pkg.assemble_rgb8_packed(self.recv[slot].data_ptr(), self.full[slot].data_ptr(), 1, self.W, self.H,
+            pkg.assemble_rgb8_packed(self.recv[slot].data_ptr(), self.full[slot].data_ptr(), self.k, self.W, self.H,
                                      self.row_block, self.world, self.side.cuda_stream)
             self.assembled[slot].record(self.side)
         self.reused[slot] = True

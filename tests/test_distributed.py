@@ -169,7 +169,7 @@ def test_row_map_covers_every_row_once():
                     assert len(rows[r]) == pkg.local_rows(H, pkg.Tiling(rb, r, world))
 
 
-def _exchange_worker(rank, world, port, W, H, row_block, slots, q):
+def _exchange_worker(rank, world, port, W, H, row_block, slots, q, k=1):
     import sys
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from conftest import import_package as ip
@@ -182,8 +182,10 @@ def _exchange_worker(rank, world, port, W, H, row_block, slots, q):
     try:
         rng = np.random.default_rng(11)
         steps = 3 * slots
-        bodies = [rng.integers(0, 256, size=(H, 3 * W), dtype=np.uint8) for _ in range(steps * world)]
-        g = D.FrameExchange(W, H, row_block, rank, world, device="cpu", slots=slots)
+        F = k * world
+        bodies = [rng.integers(0, 256, size=(H, 3 * W), dtype=np.uint8) for _ in range(steps * F)]
+        g = D.FrameExchange(W, H, row_block, rank, world, frames=F, device="cpu", slots=slots)
+        assert g.owned_frames() == list(range(rank * k, rank * k + k))
         rows = D.row_map(H, row_block, world)[rank]
         n = len(rows)
         assert g.local_rows == n
@@ -193,20 +195,21 @@ def _exchange_worker(rank, world, port, W, H, row_block, slots, q):
         def check(slot):
             nonlocal ok
             full = g.finish(slot)
-            k = owner[slot]
-            ok &= bool(np.array_equal(full[0].numpy(), bodies[k * world + rank]))   # frame f = rank
+            st = owner[slot]
+            for m, f in enumerate(g.owned_frames()):  # batch frames rank*k .. rank*k + k - 1
+                ok &= bool(np.array_equal(full[m].numpy(), bodies[st * F + f]))
             owner[slot] = None
 
-        for k in range(steps):
-            slot = k % slots
+        for st in range(steps):
+            slot = st % slots
             if owner[slot] is not None:
                 check(slot)
-            for f in range(world):                   # frame-major, compact (n rows per frame)
-                body = bodies[k * world + f]
+            for f in range(F):                       # frame-major, compact (n rows per frame)
+                body = bodies[st * F + f]
                 for i, j in enumerate(rows):
                     g.bufs[slot][f * n + n - 1 - i] = torch.from_numpy(body[H - 1 - j].copy())
             g.start(slot)
-            owner[slot] = k
+            owner[slot] = st
         for slot in range(slots):
             if owner[slot] is not None:
                 check(slot)
@@ -215,16 +218,18 @@ def _exchange_worker(rank, world, port, W, H, row_block, slots, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,row_block,slots", [(2, 16, 2), (3, 7, 4), (4, 8, 2), (5, 3, 3)])
-def test_frame_exchange_alltoall(world, row_block, slots):
-    """bench.py's default N > 1 collective: frame f of the step's N frames is gathered to rank f
-    (one all-to-all), `slots` steps in flight, gloo on CPU; ragged row counts per rank."""
+@pytest.mark.parametrize("world,row_block,slots,k", [(2, 16, 2, 1), (3, 7, 4, 1), (4, 8, 2, 4), (5, 3, 3, 2),
+                                                     (2, 8, 4, 4)])
+def test_frame_exchange_alltoall(world, row_block, slots, k):
+    """bench.py's default N > 1 collective: each of the step's k*N frames is gathered to its owner
+    rank (one all-to-all; rank q owns batch frames q*k .. q*k+k-1), `slots` steps in flight,
+    gloo on CPU; ragged row counts per rank."""
     import_package()
     W, H = 97, 61
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, W, H, row_block, slots, q)) for r in range(world)]
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, W, H, row_block, slots, q, k)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
