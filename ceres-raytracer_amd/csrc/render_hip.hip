@@ -570,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 #define CERES_STACK24 1          // 24-bit LDS stack entries for scenes with < 2^24 pairs and BVH4 nodes
 #endif
 #ifndef CERES_FUSED_STEAL
-#define CERES_FUSED_STEAL 1      // fused kernel shadow phase: intra-wavefront work stealing (0: one ray per lane)
+#define CERES_FUSED_STEAL 2      // fused shadow phase: 1 work stealing, 0 one ray per lane, 2 stealing for one-frame launches only
 #endif
 #ifndef CERES_FUSED_WG
 #define CERES_FUSED_WG 64        // fused kernel workgroup: 64 (8x8 tile, default) or 256 (16x16 tile)
@@ -909,7 +909,7 @@ __global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
 // own hits with intra-wavefront work stealing (lanes whose pixel missed help the others), then
 // shades.  No shadow-ray queue in HBM, no second launch: the shadow work of early tiles
 // overlaps the primary work of later ones.  Same results as ceres_primary + ceres_shadow.
-template <bool kStats, int kB, typename StkT, int kMinW, bool kRobust>
+template <bool kStats, int kB, typename StkT, int kMinW, bool kRobust, bool kSteal>
 __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ StealLdsT<kB> L;
@@ -970,11 +970,13 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     uint64_t t_primary = 0;
     uint32_t prim_pairs = n_pairs, shadow_iters = 0;
     if (kStats && P.wave_log) t_primary = __builtin_amdgcn_s_memrealtime();
-#if CERES_FUSED_STEAL
-    steal_traverse<kStats, kB, StkT, kRobust>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
-#else
-    L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
-#endif
+    // shadow phase: intra-wavefront work stealing shortens a frame's longest tiles (a one-frame
+    // launch is tail-bound); a multi-frame batch is throughput-bound, and there one ray per lane
+    // spends fewer instructions per node (the steal bookkeeping runs every iteration)
+    if constexpr (kSteal)
+        steal_traverse<kStats, kB, StkT, kRobust>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
+    else
+        L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
     uint32_t occluded = 0;
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
     if (kStats && P.wave_log) {
@@ -1253,17 +1255,23 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             // small scenes (16-bit stacks, LDS for 7+ waves/SIMD) get a 7-wave VGPR budget: +3.7 % C3
             // frames/s with 8 frames in flight; C5-size scenes keep the unconstrained allocation
             constexpr int w16 = CERES_FUSED_MINW16, w32 = CERES_FUSED_MINW32;
-            auto fused = [&](auto rt) {
-                constexpr bool R = decltype(rt)::value;
-                if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint16_t*, 1, R>), fgrid, fblock, flds, stream, P);
-                else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, dev::Stk24, w32, R>), fgrid, fblock, flds, stream, P);
-                else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint32_t*, w32, R>), fgrid, fblock, flds, stream, P);
-                else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint16_t*, w16, R>), fgrid, fblock, flds, stream, P);
-                else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, dev::Stk24, w32, R>), fgrid, fblock, flds, stream, P);
-                else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint32_t*, w32, R>), fgrid, fblock, flds, stream, P);
+            auto fused = [&](auto rt, auto st) {
+                constexpr bool R = decltype(rt)::value, T = decltype(st)::value;
+                if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint16_t*, 1, R, T>), fgrid, fblock, flds, stream, P);
+                else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
+                else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);
+                else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint16_t*, w16, R, T>), fgrid, fblock, flds, stream, P);
+                else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);
             };
-            if (robust) fused(std::true_type{});
-            else fused(std::false_type{});
+            // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
+            const bool steal = CERES_FUSED_STEAL == 1 || (CERES_FUSED_STEAL == 2 && frames == 1);
+            auto fused_s = [&](auto rt) {
+                if (steal) fused(rt, std::true_type{});
+                else fused(rt, std::false_type{});
+            };
+            if (robust) fused_s(std::true_type{});
+            else fused_s(std::false_type{});
             HIP_TRY(hipGetLastError());
             if (e1) HIP_TRY(hipEventRecord(e1, stream));
             if (e2) HIP_TRY(hipEventRecord(e2, stream));

@@ -64,6 +64,14 @@ def main():
         rgb = [torch.empty(3 * W * H, dtype=torch.uint8, device="cuda") for _ in range(n_streams)]
         b12 = basis[None, :].astype(np.float32)
         s3 = np.asarray(cfg["sun"], np.float32)[None, :]
+        nb = int(os.environ.get("AB_BATCH", "1"))      # frames per launch (bench.py's --frames-per-gpu)
+        if nb > 1:
+            axis, step_deg = first.configs.BENCH_ORBIT
+            b12, s3 = first.orbit_cameras(cam, cfg["sun"], W, H, nb, axis=axis, step_deg=step_deg, rotate_first=False)
+            b12[0] = basis
+            s3[0] = np.asarray(cfg["sun"], np.float32)
+            px = [torch.empty(nb * 3 * W * H, dtype=torch.float32, device="cuda") for _ in range(n_streams)]
+            rgb = [torch.empty(nb * 3 * W * H, dtype=torch.uint8, device="cuda") for _ in range(n_streams)]
         for _ in range(rounds):
             for k, sc in scenes.items():
                 torch.cuda.synchronize()
@@ -73,7 +81,7 @@ def main():
                     sc.render_batch_device(b12, s3, W, H, mode=mode, d_pixels=px[i].data_ptr() if want_px else 0,
                                            d_rgb8=rgb[i].data_ptr(), stream=strs[i].cuda_stream)
                 torch.cuda.synchronize()
-                res[k].append((time.perf_counter() - t0) * 1e3 / per)
+                res[k].append((time.perf_counter() - t0) * 1e3 / (per * nb))
     for _ in range(0 if n_streams else rounds):
         for k, sc in scenes.items():
             _, _, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=want_px, want_rgb8=True)
