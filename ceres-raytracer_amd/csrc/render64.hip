@@ -35,7 +35,11 @@
 namespace ceres {
 namespace dev64 {
 
-constexpr int kBlock = 256;
+#ifndef CERES64_WG
+#define CERES64_WG 64            // workgroup: 64 = one 8x8 tile (a long tile pins only its own LDS), 256 = 16x16
+#endif
+constexpr int kBlock = CERES64_WG;
+constexpr uint32_t kTile = kBlock == 256 ? 16u : 8u;
 
 struct D3 { double x, y, z; };
 __device__ __forceinline__ D3 operator+(D3 a, D3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
@@ -204,14 +208,15 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
     return x;
 }
 
-// grid (ceil(W/16), ceil(H/16)); each wavefront an 8x8 tile of its workgroup's 16x16 pixels
+// grid (ceil(W/kTile), ceil(H/kTile)); each wavefront an 8x8 tile (of its workgroup's 16x16
+// pixels when kBlock = 256)
 template <int kMode>
 __global__ __launch_bounds__(kBlock) void ceres_render64(const KParams64 P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     uint32_t* stk = lds + tid;
-    const uint32_t i = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t j = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const uint32_t i = blockIdx.x * kTile + (kBlock == 256 ? (wave & 1u) * 8u : 0u) + (lane & 7u);
+    const uint32_t j = blockIdx.y * kTile + (kBlock == 256 ? (wave >> 1) * 8u : 0u) + (lane >> 3);
     const bool valid = i < P.W && j < P.H;
     bool overflow = false;
     uint32_t n_hit = 0, n_shadow = 0, n_occ = 0;
@@ -295,7 +300,7 @@ int render64(ceres_scene* s, const double basis12[12], const double sun[3], int 
     if (!s || !basis12 || !sun) return set_error(CERES_EINVAL, "ceres_render_f64: null argument");
     if (!s->f64) return set_error(CERES_EINVAL, "scene is single precision: use ceres_render_f32");
     if (mode != CERES_MODE_FULL && mode != CERES_MODE_PRIMARY) return set_error(CERES_EINVAL, "bad mode %d", mode);
-    if (W == 0 || H == 0 || W > 65535u * 16u || H > 65535u * 16u) return set_error(CERES_EINVAL, "bad frame size %zux%zu", W, H);
+    if (W == 0 || H == 0 || W > 65535u * kTile || H > 65535u * kTile) return set_error(CERES_EINVAL, "bad frame size %zux%zu", W, H);
     HIP64_TRY(hipSetDevice(s->device));
     KParams64 P{};
     std::memcpy(P.cam.eye, basis12, 3 * sizeof(double));
@@ -314,7 +319,7 @@ int render64(ceres_scene* s, const double basis12[12], const double sun[3], int 
     HIP64_TRY(hipEventCreate(&e1));
     HIP64_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, s->stream));
     s->shards_dirty = true;
-    const dim3 grid((unsigned(W) + 15) / 16, (unsigned(H) + 15) / 16), block(kBlock);
+    const dim3 grid((unsigned(W) + kTile - 1) / kTile, (unsigned(H) + kTile - 1) / kTile), block(kBlock);
     const size_t lds = size_t(s->stack_entries) * kBlock * 4;
     HIP64_TRY(hipEventRecord(e0, s->stream));
     if (mode == CERES_MODE_PRIMARY) hipLaunchKernelGGL(ceres_render64<CERES_MODE_PRIMARY>, grid, block, lds, s->stream, P);
