@@ -1089,7 +1089,9 @@ void ceres::scene_release(ceres_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     dfree(s->d_pairs64); dfree(s->d_tris64); dfree(s->d_norms64);
-    dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_order); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
+    for (auto& o : s->orders) dfree(o.d);
+    s->orders.clear();
+    dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
     for (auto e : s->ev_used) (void)hipEventDestroy(e);
@@ -1126,14 +1128,18 @@ constexpr uint32_t kFusedWG = CERES_FUSED_WG;
 
 // Centre-first order of a batch's tile x tile tiles for the fused kernel: ascending distance of the
 // tile centre (global pixel coordinates) from the image centre, frames interleaved.  Cached
-// on the scene per (W, H, tiling, frames).
+// on the scene per (W, H, tiling, frames, tile) -- up to 8 orders, least recently used evicted
+// after a device synchronise (a launch in flight may still read it).
 int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, size_t rows, uint32_t frames,
-                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream) {
-    const uint64_t key = (uint64_t(W) << 44) ^ (uint64_t(H) << 24) ^ (uint64_t(t.row_block) << 12) ^
-                         (uint64_t(t.rank) << 36) ^ (uint64_t(t.world) << 52) ^ (uint64_t(frames) << 5) ^ rows ^
-                         (uint64_t(tile) << 60);
+                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out) {
+    for (auto& o : s->orders)
+        if (o.W == W && o.H == H && o.row_block == t.row_block && o.rank == t.rank && o.world == t.world &&
+            o.frames == frames && o.tile == tile) {
+            o.used = ++s->order_clock;
+            *out = o.d;
+            return CERES_OK;
+        }
     const size_t n = size_t(bx) * by * frames;
-    if (key == s->order_key && s->d_order && n <= s->order_cap) return CERES_OK;
     std::vector<std::pair<double, uint32_t>> k(n);
     const double cx = 0.5 * double(W), cy = 0.5 * double(H);
     for (uint32_t f = 0; f < frames; ++f)
@@ -1149,14 +1155,24 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     std::stable_sort(k.begin(), k.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
     std::vector<uint32_t> order(n);
     for (size_t q = 0; q < n; ++q) order[q] = k[q].second;
-    if (n > s->order_cap) {
-        dfree(s->d_order);
-        HIP_TRY(hipMalloc(&s->d_order, n * sizeof(uint32_t)));
-        s->order_cap = n;
+    if (s->orders.size() >= 8) {
+        auto lru = std::min_element(s->orders.begin(), s->orders.end(),
+                                    [](const auto& a, const auto& b) { return a.used < b.used; });
+        HIP_TRY(hipDeviceSynchronize());
+        dfree(lru->d);
+        s->orders.erase(lru);
     }
-    HIP_TRY(hipMemcpyAsync(s->d_order, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    s->order_key = key;
+    ceres_scene::TileOrder o;
+    o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile;
+    HIP_TRY(hipMalloc(&o.d, n * sizeof(uint32_t)));
+    if (hipMemcpyAsync(o.d, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess) {
+        dfree(o.d);
+        return set_error(CERES_EHIP, "tile order upload failed");
+    }
+    o.used = ++s->order_clock;
+    s->orders.push_back(o);
+    *out = o.d;
     return CERES_OK;
 }
 
@@ -1218,8 +1234,9 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     // fused kernel tiles: kFusedWG = 256 -> 16x16 per workgroup, 64 -> 8x8
     constexpr uint32_t ftile = kFusedWG == 256 ? 16 : 8;
     const uint32_t fbx = uint32_t((W + ftile - 1) / ftile), fby = uint32_t((rows + ftile - 1) / ftile);
+    const uint32_t* tile_order = nullptr;
     if (CERES_FUSED && mode == CERES_MODE_FULL && rows)
-        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream)) return rc;
+        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order)) return rc;
     // The shards must start at zero when they are read back (counters) or hold the two-pass
     // shadow queue; the fused kernel without counters only adds to them, so its steady-state
     // frames skip the memset (ceres_finalize re-zeroes them after every counted render).
@@ -1237,7 +1254,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             const bool st16 = stw == 2;
             P.lds_entries = uint32_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries));
             const size_t flds = size_t(P.lds_entries) * kFusedWG * stw;
-            P.tile_order = s->d_order;
+            P.tile_order = tile_order;
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
             const dim3 fgrid(fbx * fby * frames), fblock(kFusedWG);

@@ -20,9 +20,16 @@ struct ceres_scene {
     size_t n_nodes4 = 0;
     SiblingPair* d_pairs = nullptr;
     Node4* d_nodes4 = nullptr;
-    uint32_t* d_order = nullptr;          // fused kernel tile order, for order_key
-    size_t order_cap = 0;
-    uint64_t order_key = ~0ull;
+    // fused-kernel tile orders, one per (frame size, tiling, batch, tile), never rewritten while
+    // cached: launches on different streams may read different orders concurrently
+    struct TileOrder {
+        size_t W = 0, H = 0;
+        uint32_t row_block = 0, rank = 0, world = 0, frames = 0, tile = 0;
+        uint32_t* d = nullptr;
+        uint64_t used = 0;
+    };
+    std::vector<TileOrder> orders;
+    uint64_t order_clock = 0;
     Tri48* d_tris = nullptr;
     uint32_t* d_orig = nullptr;
     float* d_norms = nullptr;

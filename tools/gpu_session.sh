@@ -7,4 +7,4 @@ step() { local t=$1; shift; local name=$1; shift; timeout -k 10 "$t" "$@" > "gpu
 step 400 smoke python -c "import __graft_entry__ as g; g.smoke()"
 step 900 pytest_gpu python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread
 step 400 bench python bench.py
-step 400 bench_f4 python bench.py --steps 50 --warmup 5 --frames 4 --no-cpu-baseline --no-roofline
+step 400 bench_f1 python bench.py --steps 200 --warmup 10 --frames 1 --no-cpu-baseline --no-roofline
