@@ -174,7 +174,8 @@ int ceres_render_f32(ceres_scene* scene, const float basis12[12], const float su
 
 /* Device-resident variant for benchmarks and multi-GPU drivers: all output pointers are
  * DEVICE pointers on the scene's device, work is enqueued on `stream` (a hipStream_t, NULL =
- * default stream) and NOT synchronised.  Outputs cover only this rank's rows (ceres_tiling):
+ * default stream) and NOT synchronised.  Launches of one scene may be in flight on several
+ * streams at once (bench.py does) as long as only one of them at a time passes d_counters.  Outputs cover only this rank's rows (ceres_tiling):
  * d_pixels = 3*W*local_rows floats (local row-major, local row 0 first) or NULL;
  * d_rgb8 = 3*W*local_rows bytes with local row k stored at position local_rows-1-k (so for
  * world = 1 it is exactly the PPM body) or NULL.  d_counters (8 x u64, zeroed by this call)
