@@ -437,3 +437,39 @@ def test_cli_gpus_splits_frame(gpu, tmp_path):
     assert "on 3 HIP ranks" in r.stdout
     assert "Rays: %d\tHits: %d" % (meta["exact"]["rays"], meta["exact"]["hits"]) in r.stdout
     assert out.read_bytes() == ppm["exact"]
+
+
+def test_concurrent_streams_render_identical_frames(gpu):
+    """bench.py's pattern: launches of one scene in flight on several HIP streams at once, with
+    different batch shapes (1 and 3 frames, full frame and a row tiling) so their tile orders
+    differ -- every output equals the same render done alone."""
+    import torch
+    pkg = gpu
+    name = "dragon_333x217"
+    meta, _, _ = load_golden(name)
+    cfg = configs.CONFIGS[name]
+    scene = scene_for(pkg, name)[0]
+    W, H = cfg["W"], cfg["H"]
+    cam = scene_for(pkg, name)[1]
+    b3, s3 = pkg.orbit_cameras(cam, cfg["sun"], W, H, 3, axis=(0.0, 0.0, 1.0), step_deg=45.0, rotate_first=False)
+    b3[0] = pinned_basis(meta, cfg)
+    s3[0] = pinned_sun(meta, cfg)
+    jobs = [(b3[:1], s3[:1], pkg.Tiling(H, 0, 1)), (b3, s3, pkg.Tiling(H, 0, 1)), (b3, s3, pkg.Tiling(8, 1, 3)),
+            (b3[:1], s3[:1], pkg.Tiling(5, 0, 2))]
+    outs, refs = [], []
+    for b, s, t in jobs:
+        rows = pkg.local_rows(H, t)
+        outs.append(torch.zeros(len(b) * 3 * W * rows, dtype=torch.uint8, device="cuda"))
+        ref = torch.zeros_like(outs[-1])
+        scene.render_batch_device(b, s, W, H, tiling=t, d_rgb8=ref.data_ptr())
+        torch.cuda.synchronize()
+        refs.append(ref.cpu())
+    streams = [torch.cuda.Stream() for _ in jobs]
+    for rep in range(4):
+        for (b, s, t), o, st in zip(jobs, outs, streams):
+            with torch.cuda.stream(st):
+                o.zero_()
+            scene.render_batch_device(b, s, W, H, tiling=t, d_rgb8=o.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        for o, r in zip(outs, refs):
+            assert torch.equal(o.cpu(), r)
