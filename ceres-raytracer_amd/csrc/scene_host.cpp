@@ -81,7 +81,7 @@ struct MeshBuilder {
         *tri = static_cast<S*>(std::malloc(std::max<size_t>(1, nt * sizeof(TriT<S>))));
         *norm = static_cast<S*>(std::malloc(std::max<size_t>(1, nt * 9 * sizeof(S))));
         if (!*tri || !*norm) { std::free(*tri); std::free(*norm); *tri = *norm = nullptr; return set_error(CERES_ENOMEM, "out of host memory"); }
-        std::memcpy(*tri, tris.data(), nt * sizeof(TriT<S>));
+        if (nt) std::memcpy(*tri, tris.data(), nt * sizeof(TriT<S>));   // (an empty mesh has no data())
         S* o = *norm;
         for (size_t t = 0; t < nt; ++t)
             for (int k = 0; k < 3; ++k) {
@@ -576,6 +576,8 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
             if (ents[c].count) {
                 rec.first[c] = ents[c].first;
             } else {
+                if (out.size() > pairs.size() || ents[c].first >= pairs.size())   // a tree has fewer records than pairs
+                    return set_error(CERES_EINVAL, "build_shadow_bvh4: sibling pairs do not form a tree");
                 rec.first[c] = uint32_t(out.size());
                 out.emplace_back();
                 st.push_back({ents[c].first, rec.first[c], acc});
