@@ -473,3 +473,31 @@ def test_concurrent_streams_render_identical_frames(gpu):
         torch.cuda.synchronize()
         for o, r in zip(outs, refs):
             assert torch.equal(o.cpu(), r)
+
+
+@pytest.mark.parametrize("name", ["quad_65x49_robust", "bunny_97x61_primary_robust", "dragon_orbit3_333x217"])
+def test_cli_modes_write_reference_ppm(gpu, tmp_path, name):
+    """./render with --robust / --primary-only / --orbit (configs.cli_args) writes the
+    reference's PPM byte for byte."""
+    pkg = gpu
+    meta, _, ppm = load_golden(name)
+    out = tmp_path / "out.ppm"
+    r = subprocess.run([pkg.CLI_PATH] + configs.cli_args(configs.CONFIGS[name]) + ["-o", str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert out.read_bytes() == ppm["exact"]
+
+
+def test_robust_mode_rejected_for_double_scenes(gpu):
+    pkg = gpu
+    name = "dragon_333x217"
+    meta, _, _ = load_golden(name)
+    cfg = configs.CONFIGS[name]
+    mesh, bvh, cam = pkg.prepare(cfg, f64=True)
+    sc = pkg.Scene(mesh, bvh, device=0)
+    try:
+        with pytest.raises(pkg.CeresError):
+            sc.render(cam.basis(cfg["W"], cfg["H"]), np.asarray(cfg["sun"], np.float64), cfg["W"], cfg["H"],
+                      mode=pkg.MODE_FULL | pkg.MODE_ROBUST)
+    finally:
+        sc.close()
