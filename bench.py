@@ -4,10 +4,11 @@
 Workload (default): C3 = dragon.obj 1920x1080, primary + shadow rays, static.cpp camera
 (static.cpp:38-47,72-73) -- the configuration BASELINE.json's metric is quoted on.
 
-A step renders F frames (F = --frames, default = 4 per GPU): the anim.cpp:76-88 orbit of the
-C3 camera + sun about z in 45-degree steps, frame 0 = C3 exactly.  So at N = 1 a step is four
-C3-size frames (0, 45, 90, 135 degrees), and at N GPUs a step is 4N frames -- WEAK scaling,
-fixed work per GPU.
+A step renders F frames (F = --frames, default = 4 per GPU): views of the anim.cpp:76-88 orbit
+of the C3 camera + sun about z, frame 0 = C3 exactly.  At N = 1 a step is four C3-size frames
+(0, 45, 90, 135 degrees); at N GPUs it is 4N distinct frames over the same half orbit, 45/N
+degrees apart (step_views) -- WEAK scaling, four frames' work per GPU from the same arc at
+every N.
 Every frame's rows are interleaved over the ranks in blocks of --row-block rows (balanced
 load); each rank renders its rows of all F frames with one ceres_render_batch_device launch,
 RGB8 + float framebuffers in HBM, then ONE RCCL collective per step: by default each frame is
@@ -74,6 +75,28 @@ def pinned_basis(meta, cfg, cam):
         return cam.basis(cfg["W"], cfg["H"])
     bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
     return np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
+
+
+def step_views(pkg, cfg, meta, cam, F, V):
+    """Cameras (basis12 [F,12], sun3 [F,3]) of one bench step of F frames: V orbit views
+    (BENCH_ORBIT: v x 45 degrees about z, v = 0 is C3 with the fixture's basis bits) when F <= V;
+    for F = V N (N GPUs) the SAME arc sampled N times finer, frame f at f x 45 / N degrees.  So
+    every GPU's share of a step covers the same half orbit at every N (views differ in cost),
+    and all F views are distinct (near-copies of one view in one launch run slower:
+    tools/partition_probe.py)."""
+    W, H = cfg["W"], cfg["H"]
+    axis, step_deg = pkg.configs.BENCH_ORBIT
+    V = max(1, min(F, V))
+    b12, s3 = pkg.orbit_cameras(cam, cfg["sun"], W, H, V, axis=axis, step_deg=step_deg, rotate_first=False)
+    if F > V:
+        b12, s3 = np.zeros((F, 12), np.float32), np.zeros((F, 3), np.float32)
+        for f in range(1, F):
+            b, s = pkg.orbit_cameras(cam, cfg["sun"], W, H, 2, axis=axis, step_deg=f * float(step_deg) * V / F,
+                                     rotate_first=False)
+            b12[f], s3[f] = b[1], s[1]
+    b12[0] = pinned_basis(meta, cfg, cam)          # frame 0 = C3 (fixture bits)
+    s3[0] = np.asarray(cfg["sun"], np.float32)
+    return b12, s3
 
 
 def cpu_baseline(cfg_name, cfg, rays_per_frame, budget_s=3.0):
@@ -190,10 +213,8 @@ def main():
     F = args.frames or args.frames_per_gpu * world
     mesh, bvh, cam = pkg.prepare(cfg)
     scene = pkg.Scene(mesh, bvh, device=local_rank)
-    axis, step_deg = pkg.configs.BENCH_ORBIT
-    b12, s3 = pkg.orbit_cameras(cam, cfg["sun"], W, H, F, axis=axis, step_deg=step_deg, rotate_first=False)
-    b12[0] = pinned_basis(meta, cfg, cam)          # frame 0 = C3 (fixture bits)
-    s3[0] = np.asarray(cfg["sun"], np.float32)
+    # explicit --frames: F distinct orbit views spread over the ranks; default: --frames-per-gpu views
+    b12, s3 = step_views(pkg, cfg, meta, cam, F, max(1, F // world) if args.frames else args.frames_per_gpu)
     exchange = world > 1 and args.collect == "exchange" and F % world == 0
     if exchange:
         # batch order for the all-to-all: rank q owns batch frames q*k .. q*k+k-1, which are orbit

@@ -569,6 +569,9 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 #ifndef CERES_STACK24
 #define CERES_STACK24 1          // 24-bit LDS stack entries for scenes with < 2^24 pairs and BVH4 nodes
 #endif
+#ifndef CERES_TILE_XCD_MIX
+#define CERES_TILE_XCD_MIX 1     // deal every frame of a batch to every XCD (tile order rotated per run of 8)
+#endif
 #ifndef CERES_FUSED_STEAL
 #define CERES_FUSED_STEAL 2      // fused shadow phase: 1 work stealing, 0 one ray per lane, 2 stealing for one-frame launches only
 #endif
@@ -1155,6 +1158,16 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     std::stable_sort(k.begin(), k.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
     std::vector<uint32_t> order(n);
     for (size_t q = 0; q < n; ++q) order[q] = k[q].second;
+#if CERES_TILE_XCD_MIX
+    // Workgroups b and b + 8 share an XCD (MI355X_MICROARCH.md: blocks are dealt round-robin
+    // over the 8 XCDs).  Equal-distance tiles of the F frames are adjacent in the order, so with
+    // F a divisor or multiple of 8 every XCD would get the same frames for the whole launch and
+    // the XCD holding the costliest view would set the launch's length.  Rotating each run of 8
+    // by its index deals every frame to every XCD.  (One frame: left as is -- the rotation only
+    // scatters neighbouring tiles over more L2s, +8 MB of DRAM reads per C3 frame.)
+    for (size_t b0 = 0; frames > 1 && b0 + 8 <= n; b0 += 8)
+        std::rotate(order.begin() + b0, order.begin() + b0 + (b0 / 8) % 8, order.begin() + b0 + 8);
+#endif
     if (s->orders.size() >= 8) {
         auto lru = std::min_element(s->orders.begin(), s->orders.end(),
                                     [](const auto& a, const auto& b) { return a.used < b.used; });

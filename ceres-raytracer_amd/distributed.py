@@ -8,8 +8,9 @@ every rank renders its rows of all F frames with ONE ceres_render_batch_device l
 into a compact RGB8 buffer (frame-major, local row k of a frame at position n - 1 - k), and
 ONE collective per step -- a gather of those buffers to rank 0 -- brings all F frames there,
 where ceres_assemble_rgb8 un-interleaves them into F PPM bodies (BatchGather), or -- the
-bench's default for F = N -- frame f is gathered to rank f, all N gathers as one all-to-all
-(FrameExchange), so no single rank's ingress carries the whole step.  Both are
+bench's default, F = k N -- each frame is gathered to one owner rank (k frames per rank), all
+those gathers as one all-to-all (FrameExchange), so no single rank's ingress carries the whole
+step.  Both are
 multi-buffered: the gather (RCCL stream) and assembly (side stream) of step k overlap the
 render of step k + 1.  The scene is replicated (uploaded per device, outside the timed
 region).  The reference has no distributed code (render.hpp:104 is an OpenMP loop).
