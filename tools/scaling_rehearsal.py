@@ -10,7 +10,7 @@ the predicted device time of a step, serialised (tail-bound) and in the bench's 
 (launches rotated over 8 streams, wall time per launch); the RCCL collective is NOT modelled (one GPU has no xGMI
 peer) -- it is pipelined behind the next step's render in bench.py (distributed.BatchGather).
 
-    python tools/scaling_rehearsal.py [config] [reps] [frames per GPU] > gpurun_out/scaling_rehearsal.json
+    python tools/scaling_rehearsal.py [config] [reps] [frames per GPU] [row block] > gpurun_out/scaling_rehearsal.json
 """
 import json
 import os
@@ -27,9 +27,12 @@ def main():
     import torch
     from bench import import_package, load_golden, step_views
     pkg = import_package()
+    if os.environ.get("CERES_LIB"):                               # A/B: another build of the library
+        pkg.LIB_PATH = os.path.abspath(os.environ["CERES_LIB"])
     name = sys.argv[1] if len(sys.argv) > 1 else "dragon_1080"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     k = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    rb = int(sys.argv[4]) if len(sys.argv) > 4 else 8            # bench.py --row-block
     cfg = pkg.configs.CONFIGS[name]
     meta = load_golden(name)
     W, H = cfg["W"], cfg["H"]
@@ -46,8 +49,9 @@ def main():
     for N in (1, 2, 4, 8):
         F = k * N
         b12, s3 = step_views(pkg, cfg, meta, cam, F, k)      # the same arc at every N, as bench.py
-        row_block = 8 if N > 1 else H
+        row_block = rb if N > 1 else H
         per_rank = []
+        rank_rays = []
         rays = 0
         maxrows = max(pkg.local_rows(H, pkg.Tiling(row_block, r, N)) for r in range(N))
         px = torch.empty(F * 3 * W * maxrows, dtype=torch.float32, device=dev)
@@ -63,7 +67,8 @@ def main():
             scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=til, d_pixels=px.data_ptr(),
                                       d_rgb8=rgb.data_ptr(), d_counters=counters.data_ptr(), stream=stream.cuda_stream)
             torch.cuda.synchronize(dev)
-            rays += int(counters[0].item())
+            rank_rays.append(int(counters[0].item()))
+            rays += rank_rays[-1]
             for _ in range(5):
                 scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=til, d_pixels=px.data_ptr(),
                                           d_rgb8=rgb.data_ptr(), stream=stream.cuda_stream)
@@ -105,7 +110,7 @@ def main():
         if base is None:
             base, base_p = mrays, mrays_p
         del spx, srgb
-        out["by_n"][N] = {"frames_per_step": F, "rays_per_step": rays, "rank_ms": [round(x, 5) for x in per_rank],
+        out["by_n"][N] = {"frames_per_step": F, "rays_per_step": rays, "rank_rays": rank_rays, "row_block": row_block, "rank_ms": [round(x, 5) for x in per_rank],
                           "slowest_rank_ms": round(step_ms, 5), "mean_rank_ms": round(float(np.mean(per_rank)), 5),
                           "assemble_ms_rank0": round(asm_ms, 5),
                           "gather_bytes_to_rank0": (N - 1) * F * maxrows * 3 * W,
