@@ -572,6 +572,9 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 #ifndef CERES_TILE_XCD_WEDGE
 #define CERES_TILE_XCD_WEDGE 0   // XCD group w renders angular wedge w of every frame (L2 locality)
 #endif
+#ifndef CERES_TILE_SHUFFLE_WINDOW
+#define CERES_TILE_SHUFFLE_WINDOW 64   // tiles per shuffled window of the centre-first order
+#endif
 #ifndef CERES_TILE_XCD_MIX
 #define CERES_TILE_XCD_MIX 3     // tile order vs XCDs: 3 shuffle windows of 64 (default), 2 the same for batches only,
                                  // 1 rotate runs of 8 for batches, 0 plain centre-first
@@ -1199,8 +1202,8 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     // (Mode 2: batches only; 3: always.)
     if (CERES_TILE_XCD_MIX == 3 || frames > 1) {
         uint64_t st = 0x9e3779b97f4a7c15ull;
-        for (size_t b0 = 0; b0 < n; b0 += 64) {
-            const size_t len = std::min<size_t>(64, n - b0);
+        for (size_t b0 = 0; b0 < n; b0 += CERES_TILE_SHUFFLE_WINDOW) {
+            const size_t len = std::min<size_t>(CERES_TILE_SHUFFLE_WINDOW, n - b0);
             for (size_t q = len - 1; q > 0; --q) {
                 st = st * 6364136223846793005ull + 1442695040888963407ull;
                 std::swap(order[b0 + q], order[b0 + size_t((st >> 33) % (q + 1))]);
