@@ -4,15 +4,15 @@
 Workload (default): C3 = dragon.obj 1920x1080, primary + shadow rays, static.cpp camera
 (static.cpp:38-47,72-73) -- the configuration BASELINE.json's metric is quoted on.
 
-A step renders F frames (F = --frames, default = 4 per GPU): views of the anim.cpp:76-88 orbit
-of the C3 camera + sun about z, frame 0 = C3 exactly.  At N = 1 a step is four C3-size frames
-(0, 45, 90, 135 degrees); at N GPUs it is 4N distinct frames over the same half orbit, 45/N
-degrees apart (step_views) -- WEAK scaling, four frames' work per GPU from the same arc at
-every N.
+A step renders F frames (F = --frames, default = 8 per GPU): views of the anim.cpp:76-88 orbit
+of the C3 camera + sun about z, frame 0 = C3 exactly.  At N = 1 a step is eight C3-size frames
+(the full orbit in 45-degree steps); at N GPUs it is 8N distinct frames over the same orbit,
+45/N degrees apart (step_views) -- WEAK scaling, eight frames' work per GPU from the same orbit
+at every N.
 Every frame's rows are interleaved over the ranks in blocks of --row-block rows (balanced
 load); each rank renders its rows of all F frames with one ceres_render_batch_device launch,
 RGB8 + float framebuffers in HBM, then ONE RCCL collective per step: by default each frame is
-gathered to one owner rank (rank q owns 4 of the 4N frames; all the per-frame gathers are one
+gathered to one owner rank (rank q owns 8 of the 8N frames; all the per-frame gathers are one
 all-to-all, so no rank's xGMI ingress carries the whole step; ceres_assemble_rgb8_packed
 un-interleaves a rank's frames), or with
 --collect gather all F frames go to rank 0.  Steps rotate over --streams HIP streams (own
@@ -81,7 +81,7 @@ def step_views(pkg, cfg, meta, cam, F, V):
     """Cameras (basis12 [F,12], sun3 [F,3]) of one bench step of F frames: V orbit views
     (BENCH_ORBIT: v x 45 degrees about z, v = 0 is C3 with the fixture's basis bits) when F <= V;
     for F = V N (N GPUs) the SAME arc sampled N times finer, frame f at f x 45 / N degrees.  So
-    every GPU's share of a step covers the same half orbit at every N (views differ in cost),
+    every GPU's share of a step covers the same arc at every N (views differ in cost),
     and all F views are distinct (near-copies of one view in one launch run slower:
     tools/partition_probe.py)."""
     W, H = cfg["W"], cfg["H"]
@@ -168,7 +168,7 @@ def main():
     ap.add_argument("--config", default="dragon_1080")
     ap.add_argument("--frames", type=int, default=0,
                     help="orbit frames per step (default: --frames-per-gpu x number of GPUs)")
-    ap.add_argument("--frames-per-gpu", type=int, default=4,
+    ap.add_argument("--frames-per-gpu", type=int, default=8,
                     help="frames of work per GPU per step when --frames is not given (weak scaling)")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -92,7 +92,7 @@ struct alignas(128) Shard {
 };
 static_assert(sizeof(Shard) == 128, "Shard");
 
-constexpr int kMaxFrames = 32;  // frames per batch launch (KParams stays well inside the 4 KB kernarg limit)
+constexpr int kMaxFrames = 64;  // frames per batch launch (KParams, cameras inline, stays inside the 4 KB kernarg limit)
 struct FrameCam {              // one frame of a batch: eye + the render.hpp:91-97 basis + its sun
     float eye[3], dir[3], iu[3], iv[3], sun[3];
 };
@@ -126,6 +126,7 @@ struct KParams {
     // diagnostic (stats scenes only): 8 x u64 per wavefront of the shadow kernel
     unsigned long long* wave_log;
 };
+static_assert(sizeof(KParams) <= 4096, "KParams must fit the 4 KB kernel-argument limit");
 
 // device: reference BVH in HBM -> GPU layout (scene_device.hip); buffers hipMalloc'd
 struct DeviceLayout {

@@ -183,7 +183,7 @@ int ceres_render_f32(ceres_scene* scene, const float basis12[12], const float su
 int ceres_render_device(ceres_scene* scene, const float basis12[12], const float sun[3], int mode,
                         size_t width, size_t height, const ceres_tiling* tiling,
                         float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, void* stream);
-/* A batch of `frames` (1..32) frames of one scene in ONE launch pair -- the render() call
+/* A batch of `frames` (1..64) frames of one scene in ONE launch pair -- the render() call
  * that anim.cpp:93-110 makes once per orbit frame, batched.  basis12 = frames x 12 floats
  * (eye, dir, iu, iv per frame), sun3 = frames x 3 floats.  Frame f of the batch occupies
  * d_pixels[f*3*W*local_rows ...] / d_rgb8[f*3*W*local_rows ...], each laid out exactly as

@@ -268,11 +268,35 @@ def test_assemble_packed_kernel_matches_permutation(gpu, W, H, row_block, world,
     assert torch.equal(out, ref)
 
 
+def test_batch_of_64_frames_matches_single_frames(gpu):
+    """The largest batch (64 frames, cameras inline in the kernel arguments): every frame's PPM
+    body == a one-frame render of the same camera, whole frames and one rank of a 3-way split."""
+    import torch
+    pkg = gpu
+    name = "dragon_333x217"
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    scene, _, _, _ = scene_for(pkg, name)
+    cam0 = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    b12, s3 = pkg.orbit_cameras(cam0, cfg["sun"], W, H, 64, axis=configs.BENCH_ORBIT[0], step_deg=5.625,
+                                rotate_first=False)
+    st = torch.cuda.current_stream().cuda_stream
+    for til in (pkg.Tiling(H, 0, 1), pkg.Tiling(8, 2, 3)):
+        rows = pkg.local_rows(H, til)
+        rgb = torch.zeros((64, rows, 3 * W), dtype=torch.uint8, device="cuda")
+        scene.render_batch_device(b12, s3, W, H, tiling=til, d_rgb8=rgb.data_ptr(), stream=st)
+        one = torch.zeros((rows, 3 * W), dtype=torch.uint8, device="cuda")
+        for f in (0, 1, 31, 32, 33, 62, 63):
+            scene.render_device(b12[f], s3[f], W, H, tiling=til, d_rgb8=one.data_ptr(), stream=st)
+            torch.cuda.synchronize()
+            assert torch.equal(rgb[f], one), f"frame {f}, tiling {til}"
+
+
 def test_batch_rejects_bad_frame_counts(gpu):
     pkg = gpu
     scene, _, _, _ = scene_for(pkg, "tri1")
     with pytest.raises(pkg.CeresError):
-        scene.render_batch_device(np.zeros((33, 12), np.float32), np.zeros((33, 3), np.float32), 8, 8)
+        scene.render_batch_device(np.zeros((65, 12), np.float32), np.zeros((65, 3), np.float32), 8, 8)
     with pytest.raises(pkg.CeresError):
         scene.render_batch_device(np.zeros((2, 12), np.float32), np.zeros((3, 3), np.float32), 8, 8)
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Weak-scaling rehearsal on ONE MI355X: the per-rank work of bench.py at N = 1, 2, 4, 8 GPUs.
 
-At N GPUs a bench step is F = k*N orbit frames (k = frames per GPU, bench.py's default 4), each frame's rows dealt in blocks of 8 over the
+At N GPUs a bench step is F = k*N orbit frames (k = frames per GPU, bench.py's default 8), each frame's rows dealt in blocks of 8 over the
 N ranks; rank r renders its rows of all F frames with one ceres_render_batch_device launch,
 and rank 0 un-interleaves the gathered buffers with ceres_assemble_rgb8.  This tool runs,
 on the one GPU it has, exactly the launch every rank would run (Tiling(8, r, N)) and the
@@ -31,7 +31,7 @@ def main():
         pkg.LIB_PATH = os.path.abspath(os.environ["CERES_LIB"])
     name = sys.argv[1] if len(sys.argv) > 1 else "dragon_1080"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
-    k = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    k = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     rb = int(sys.argv[4]) if len(sys.argv) > 4 else 8            # bench.py --row-block
     cfg = pkg.configs.CONFIGS[name]
     meta = load_golden(name)

@@ -13,5 +13,5 @@ for c in ${CONFIGS:-bunny_1080_primary bunny_1080 dragon_1080 dragon_4096 proc_c
   step 400 bench_$c python bench.py --config $c --steps $steps --warmup 5
 done
 for c in ${REHEARSE:-dragon_1080 bunny_1080 dragon_4096}; do
-  step 300 rehearsal_$c python tools/scaling_rehearsal.py $c 20 ${FPG:-4}
+  step 300 rehearsal_$c python tools/scaling_rehearsal.py $c 20 ${FPG:-8}
 done
