@@ -67,6 +67,8 @@ struct KParams64 {
     int32_t* rec_prim;       // optional per-pixel records, pixel = j*W + i
     double* rec_tuv;
     int8_t* rec_shadow;
+    const uint32_t* tile_order;  // block -> tile, centre first and XCD-balanced (frame_tile_order)
+    uint32_t tiles_x;
 };
 
 struct TriD { D3 p0, e1, e2, n; };
@@ -208,15 +210,18 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
     return x;
 }
 
-// grid (ceil(W/kTile), ceil(H/kTile)); each wavefront an 8x8 tile (of its workgroup's 16x16
+// 1-D grid over the frame's kTile x kTile tiles in tile_order (as the float path: expensive tiles
+// first, every XCD an unbiased share); each wavefront an 8x8 tile (of its workgroup's 16x16
 // pixels when kBlock = 256)
 template <int kMode>
 __global__ __launch_bounds__(kBlock) void ceres_render64(const KParams64 P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     uint32_t* stk = lds + tid;
-    const uint32_t i = blockIdx.x * kTile + (kBlock == 256 ? (wave & 1u) * 8u : 0u) + (lane & 7u);
-    const uint32_t j = blockIdx.y * kTile + (kBlock == 256 ? (wave >> 1) * 8u : 0u) + (lane >> 3);
+    const uint32_t t = __builtin_amdgcn_readfirstlane(P.tile_order[blockIdx.x]);
+    const uint32_t tby = t / P.tiles_x, tbx = t - tby * P.tiles_x;
+    const uint32_t i = tbx * kTile + (kBlock == 256 ? (wave & 1u) * 8u : 0u) + (lane & 7u);
+    const uint32_t j = tby * kTile + (kBlock == 256 ? (wave >> 1) * 8u : 0u) + (lane >> 3);
     const bool valid = i < P.W && j < P.H;
     bool overflow = false;
     uint32_t n_hit = 0, n_shadow = 0, n_occ = 0;
@@ -268,7 +273,7 @@ __global__ __launch_bounds__(kBlock) void ceres_render64(const KParams64 P) {
         }
     }
     const uint32_t wh = wave_sum(n_hit + n_occ), ws = wave_sum(n_shadow);
-    const uint32_t shard = (blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave;
+    const uint32_t shard = blockIdx.x * (kBlock / 64) + wave;
     if (lane == 0) {
         Shard& sh = P.shards[shard % kShards];
         if (ws) atomicAdd(&sh.queued, ws);
@@ -319,7 +324,10 @@ int render64(ceres_scene* s, const double basis12[12], const double sun[3], int 
     HIP64_TRY(hipEventCreate(&e1));
     HIP64_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, s->stream));
     s->shards_dirty = true;
-    const dim3 grid((unsigned(W) + kTile - 1) / kTile, (unsigned(H) + kTile - 1) / kTile), block(kBlock);
+    const uint32_t tx = (uint32_t(W) + kTile - 1) / kTile, ty = (uint32_t(H) + kTile - 1) / kTile;
+    if (int rc = frame_tile_order(s, W, H, kTile, s->stream, &P.tile_order)) return rc;
+    P.tiles_x = tx;
+    const dim3 grid(tx * ty), block(kBlock);
     const size_t lds = size_t(s->stack_entries) * kBlock * 4;
     HIP64_TRY(hipEventRecord(e0, s->stream));
     if (mode == CERES_MODE_PRIMARY) hipLaunchKernelGGL(ceres_render64<CERES_MODE_PRIMARY>, grid, block, lds, s->stream, P);

@@ -1415,6 +1415,14 @@ void fill_stats(ceres_stats* st, const uint64_t c[8], double ms) {
 
 }  // namespace
 
+namespace ceres {
+int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out) {
+    const ceres_tiling t{uint32_t(H), 0, 1};
+    return ensure_tile_order(s, W, H, t, H, 1, uint32_t((W + tile - 1) / tile), uint32_t((H + tile - 1) / tile), tile,
+                             stream, out);
+}
+}  // namespace ceres
+
 extern "C" {
 
 const char* ceres_last_error(void) { return error_buffer(); }

@@ -59,4 +59,6 @@ struct ceres_scene {
 
 namespace ceres {
 void scene_release(ceres_scene* s);          // frees every device buffer and the stream (render_hip.hip)
+// centre-first, XCD-balanced order of one whole frame's tile x tile tiles (render_hip.hip)
+int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out);
 }
