@@ -1099,7 +1099,10 @@ void ceres::scene_release(ceres_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     dfree(s->d_pairs64); dfree(s->d_tris64); dfree(s->d_norms64);
-    for (auto& o : s->orders) dfree(o.d);
+    for (auto& o : s->orders) {
+        dfree(o.d);
+        for (auto& u : o.uses) (void)hipEventDestroy(u.second);
+    }
     s->orders.clear();
     dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
@@ -1138,8 +1141,10 @@ constexpr uint32_t kFusedWG = CERES_FUSED_WG;
 
 // Centre-first order of a batch's tile x tile tiles for the fused kernel: ascending distance of the
 // tile centre (global pixel coordinates) from the image centre, frames interleaved.  Cached
-// on the scene per (W, H, tiling, frames, tile) -- up to 8 orders, least recently used evicted
-// after a device synchronise (a launch in flight may still read it).
+// on the scene per (W, H, tiling, frames, tile) -- up to kMaxTileOrders orders; the least
+// recently used one is evicted once the launches that read it have ended (its per-stream
+// events, mark_tile_order), and its buffer is reused when large enough, so eviction stalls
+// neither the other streams nor the device.
 int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, size_t rows, uint32_t frames,
                       uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out) {
     for (auto& o : s->orders)
@@ -1220,16 +1225,23 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     for (size_t b0 = 0; frames > 1 && b0 + 8 <= n; b0 += 8)
         std::rotate(order.begin() + b0, order.begin() + b0 + (b0 / 8) % 8, order.begin() + b0 + 8);
 #endif
-    if (s->orders.size() >= 8) {
+    ceres_scene::TileOrder o;
+    if (s->orders.size() >= ceres::kMaxTileOrders) {
         auto lru = std::min_element(s->orders.begin(), s->orders.end(),
                                     [](const auto& a, const auto& b) { return a.used < b.used; });
-        HIP_TRY(hipDeviceSynchronize());
-        dfree(lru->d);
+        for (auto& u : lru->uses) {                                  // launches that read it have ended
+            HIP_TRY(hipEventSynchronize(u.second));
+            (void)hipEventDestroy(u.second);
+        }
+        o.d = lru->d; o.cap = lru->cap;
         s->orders.erase(lru);
+        if (o.cap < n) { dfree(o.d); o.cap = 0; }
     }
-    ceres_scene::TileOrder o;
     o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile;
-    HIP_TRY(hipMalloc(&o.d, n * sizeof(uint32_t)));
+    if (!o.d) {
+        HIP_TRY(hipMalloc(&o.d, n * sizeof(uint32_t)));
+        o.cap = n;
+    }
     if (hipMemcpyAsync(o.d, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess) {
         dfree(o.d);
@@ -1265,7 +1277,11 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     HIP_TRY(hipSetDevice(s->device));
     const size_t nwaves = size_t(bx) * by * frames * (dev::kBlock / 64);
     const uint32_t cap = uint32_t(((nwaves + kShards - 1) / kShards) * 64);   // <= 64 jobs per wavefront
-    if (int rc = ensure_workspace(s, size_t(cap) * kShards, 0, false, false)) return rc;
+    // only the two-pass path (ceres_primary -> shadow kernel) queues shadow jobs in HBM; the fused
+    // kernel and primary-only mode never touch them
+    const bool two_pass = !CERES_FUSED && mode == CERES_MODE_FULL;
+    if (two_pass)
+        if (int rc = ensure_workspace(s, size_t(cap) * kShards, 0, false, false)) return rc;
 
     KParams P{};
     for (uint32_t f = 0; f < frames; ++f) {
@@ -1355,6 +1371,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             if (robust) fused_s(std::true_type{});
             else fused_s(std::false_type{});
             HIP_TRY(hipGetLastError());
+            if (int rc = ceres::mark_tile_order(s, tile_order, stream)) return rc;
             if (e1) HIP_TRY(hipEventRecord(e1, stream));
             if (e2) HIP_TRY(hipEventRecord(e2, stream));
         } else {
@@ -1416,6 +1433,24 @@ void fill_stats(ceres_stats* st, const uint64_t c[8], double ms) {
 }  // namespace
 
 namespace ceres {
+int mark_tile_order(ceres_scene* s, const uint32_t* d, hipStream_t stream) {
+    for (auto& o : s->orders) {
+        if (o.d != d) continue;
+        hipEvent_t* ev = nullptr;
+        for (auto& u : o.uses)
+            if (u.first == stream) ev = &u.second;     // stream order: the latest record covers earlier ones
+        if (!ev) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            o.uses.push_back({stream, e});
+            ev = &o.uses.back().second;
+        }
+        HIP_TRY(hipEventRecord(*ev, stream));
+        return CERES_OK;
+    }
+    return set_error(CERES_EINVAL, "tile order not cached");
+}
+
 int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out) {
     const ceres_tiling t{uint32_t(H), 0, 1};
     return ensure_tile_order(s, W, H, t, H, 1, uint32_t((W + tile - 1) / tile), uint32_t((H + tile - 1) / tile), tile,

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "ceres_types.hpp"
@@ -21,12 +22,16 @@ struct ceres_scene {
     SiblingPair* d_pairs = nullptr;
     Node4* d_nodes4 = nullptr;
     // fused-kernel tile orders, one per (frame size, tiling, batch, tile), never rewritten while
-    // cached: launches on different streams may read different orders concurrently
+    // a launch that reads them may be in flight: launches on different streams may read different
+    // orders concurrently.  `uses` holds one event per stream that launched with the order,
+    // recorded after its latest such launch; evicting the order waits on those events only.
     struct TileOrder {
         size_t W = 0, H = 0;
         uint32_t row_block = 0, rank = 0, world = 0, frames = 0, tile = 0;
         uint32_t* d = nullptr;
+        size_t cap = 0;                // entries allocated at d
         uint64_t used = 0;
+        std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
     };
     std::vector<TileOrder> orders;
     uint64_t order_clock = 0;
@@ -61,4 +66,7 @@ namespace ceres {
 void scene_release(ceres_scene* s);          // frees every device buffer and the stream (render_hip.hip)
 // centre-first, XCD-balanced order of one whole frame's tile x tile tiles (render_hip.hip)
 int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out);
+// records, after a launch on `stream` that reads tile order `d`, the event eviction waits on
+int mark_tile_order(ceres_scene* s, const uint32_t* d, hipStream_t stream);
+constexpr size_t kMaxTileOrders = 16;         // cached orders per scene before LRU eviction
 }

@@ -499,6 +499,72 @@ def test_concurrent_streams_render_identical_frames(gpu):
             assert torch.equal(o.cpu(), r)
 
 
+def test_tile_order_eviction_under_concurrent_streams(gpu):
+    """More distinct batch shapes than the scene caches tile orders for (kMaxTileOrders = 16,
+    scene_internal.hpp), launched round-robin on four streams and repeated, so least-recently-used
+    orders are evicted and their buffers reused while other streams' launches are in flight --
+    every output still equals the same render done alone."""
+    import torch
+    pkg = gpu
+    name = "dragon_333x217"
+    meta, _, _ = load_golden(name)
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    mesh, bvh, cam = pkg.prepare(cfg)
+    scene = pkg.Scene(mesh, bvh, device=0)
+    b4, s4 = pkg.orbit_cameras(cam, cfg["sun"], W, H, 4, axis=(0.0, 0.0, 1.0), step_deg=30.0, rotate_first=False)
+    b4[0] = pinned_basis(meta, cfg)
+    s4[0] = pinned_sun(meta, cfg)
+    jobs = []
+    for nf in (1, 2, 3, 4):
+        for t in (pkg.Tiling(H, 0, 1), pkg.Tiling(8, 0, 2), pkg.Tiling(8, 1, 2), pkg.Tiling(5, 2, 3),
+                  pkg.Tiling(16, 0, 4)):
+            jobs.append((b4[:nf], s4[:nf], t))
+    assert len(jobs) == 20
+    refs = []
+    for b, s, t in jobs:
+        ref = torch.zeros(len(b) * 3 * W * pkg.local_rows(H, t), dtype=torch.uint8, device="cuda")
+        scene.render_batch_device(b, s, W, H, tiling=t, d_rgb8=ref.data_ptr())
+        torch.cuda.synchronize()
+        refs.append(ref.cpu())
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    outs = [torch.zeros_like(r, device="cuda") for r in refs]
+    for rep in range(3):
+        order = list(range(len(jobs))) if rep % 2 == 0 else list(reversed(range(len(jobs))))
+        for q, j in enumerate(order):
+            b, s, t = jobs[j]
+            st = streams[q % 4]
+            with torch.cuda.stream(st):
+                outs[j].zero_()
+            scene.render_batch_device(b, s, W, H, tiling=t, d_rgb8=outs[j].data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        for j, (o, r) in enumerate(zip(outs, refs)):
+            assert torch.equal(o.cpu(), r), f"rep {rep} job {j}"
+    scene.close()
+
+
+def test_fused_batch_allocates_no_shadow_queue(gpu):
+    """The fused kernel keeps shadow rays on chip: a 64-frame batch must not allocate the
+    two-pass path's HBM shadow-job queue (32 B x 64 per wavefront: ~150 MB here)."""
+    import torch
+    pkg = gpu
+    name = "dragon_333x217"
+    meta, _, _ = load_golden(name)
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    mesh, bvh, cam = pkg.prepare(cfg)
+    scene = pkg.Scene(mesh, bvh, device=0)
+    b, s = pkg.orbit_cameras(cam, cfg["sun"], W, H, 64, axis=(0.0, 0.0, 1.0), step_deg=5.0, rotate_first=False)
+    out = torch.zeros(64 * 3 * W * H, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    scene.render_batch_device(b, s, W, H, d_rgb8=out.data_ptr())
+    torch.cuda.synchronize()
+    grown = free0 - torch.cuda.mem_get_info()[0]
+    scene.close()
+    assert grown < 32 << 20, f"device memory grew by {grown / 2**20:.1f} MiB for one fused batch"
+
+
 @pytest.mark.parametrize("name", ["quad_65x49_robust", "bunny_97x61_primary_robust", "dragon_orbit3_333x217"])
 def test_cli_modes_write_reference_ppm(gpu, tmp_path, name):
     """./render with --robust / --primary-only / --orbit (configs.cli_args) writes the
