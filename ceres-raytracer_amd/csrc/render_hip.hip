@@ -48,6 +48,18 @@
 #ifndef CERES_PREFETCH_NEXT
 #define CERES_PREFETCH_NEXT 1 // trace(): issue the next record's load before the step's triangle tests
 #endif
+#ifndef CERES_SCALAR_UNIFORM
+#define CERES_SCALAR_UNIFORM 1 // wave-uniform record fetches through the scalar cache (see uniform_id)
+#endif
+#ifndef CERES_SU_PAIR
+#define CERES_SU_PAIR 0                       // ... of primary BVH2 sibling pairs (A/B: C3 -0.6 %, bunny +6 %)
+#endif
+#ifndef CERES_SU_TRI
+#define CERES_SU_TRI CERES_SCALAR_UNIFORM     // ... of leaf triangles
+#endif
+#ifndef CERES_SU_NODE4
+#define CERES_SU_NODE4 CERES_SCALAR_UNIFORM   // ... of shadow BVH4 nodes
+#endif
 
 namespace ceres {
 
@@ -69,11 +81,48 @@ __device__ __forceinline__ F3 cross(F3 a, F3 b) { return {a.y * b.z - a.z * b.y,
 __device__ __forceinline__ F3 normalize(F3 v) { float inv = 1.0f / sqrtf(dot(v, v)); return v * inv; }
 __device__ __forceinline__ F3 f3(const float* p) { return {p[0], p[1], p[2]}; }
 
+// Wave-uniform fetches.  The fused kernel is bound by the vector-memory return path (PMC of an
+// 8-frame C3 batch: TD busy 79 %, TA 70 % of cycles), which delivers every active lane's 16 B
+// per dwordx4 even when all lanes read the same record -- and in half the primary BVH2 steps
+// they do (coherent 8x8 tiles; tools/diag_uniform.py: C3 49 %, bunny 64 %, dragon 4096^2 65 %
+// of wave-steps; shadow BVH4 steps 33-51 %, leaf triangles 48-77 %).  Such a record is read
+// once through the scalar cache instead (s_load into SGPRs: no TA/TD traffic) and broadcast.
+// uniform_id: true and r = the id when every active lane of the wavefront holds the same id.
+__device__ __forceinline__ bool uniform_id(uint32_t id, uint32_t& r) {
+    r = __builtin_amdgcn_readfirstlane(id);
+    return __ballot(id != r) == 0;
+}
+typedef float F4v __attribute__((ext_vector_type(4)));
+typedef uint32_t U4v __attribute__((ext_vector_type(4)));
+// 16-B piece i of a read-only record through the constant address space: s_load_dwordx*
+// (the address must be wave-uniform; the scene is never written while a kernel runs)
+__device__ __forceinline__ float4 sload_f4(const void* p, int i) {
+    const F4v v = ((const __attribute__((address_space(4))) F4v*)(p))[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 sload_u4(const void* p, int i) {
+    const U4v v = ((const __attribute__((address_space(4))) U4v*)(p))[i];
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 struct TriV { F3 p0, e1, e2, n; };
 __device__ __forceinline__ TriV load_tri(const Tri48* t) {
     const float4* q = reinterpret_cast<const float4*>(t);
     const float4 a = q[0], b = q[1], c = q[2];
     return {{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, c.x}, {c.y, c.z, c.w}};
+}
+// the same record through the scalar cache (t wave-uniform)
+__device__ __forceinline__ TriV load_tri_s(const Tri48* t) {
+    const float4 a = sload_f4(t, 0), b = sload_f4(t, 1), c = sload_f4(t, 2);
+    return {{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, c.x}, {c.y, c.z, c.w}};
+}
+// triangle `idx` for the active lanes: one scalar fetch when they all test the same triangle
+__device__ __forceinline__ TriV load_tri_u(const Tri48* tris, uint32_t idx) {
+#if CERES_SU_TRI
+    uint32_t r;
+    if (uniform_id(idx, r)) return load_tri_s(tris + r);
+#endif
+    return load_tri(tris + idx);
 }
 
 // Correctly rounded 1/x (IEEE division, as the reference's `1 / dot(n, d)`), fast path: one
@@ -106,6 +155,35 @@ struct Stk24 {
     };
     __device__ __forceinline__ Ref operator[](uint32_t i) const { return {lo + i, hi + i}; }
 };
+
+// Diagnostic build only (make variant DEFS=-DCERES_DIAG_UNIFORM=1, tools/diag_uniform.py): per
+// wave-step of a loop, how many distinct records the wave's active lanes fetch.  g_diag[base..+3]
+// += steps, steps with one record for all active lanes, distinct records, active lanes.
+#ifndef CERES_DIAG_UNIFORM
+#define CERES_DIAG_UNIFORM 0
+#endif
+#if CERES_DIAG_UNIFORM
+__device__ unsigned long long g_diag[16];
+__device__ __forceinline__ void diag_step(uint32_t id, int base) {
+    const unsigned long long m = __ballot(1);
+    uint32_t distinct = 0;
+    unsigned long long rest = m;
+    while (rest) {
+        const uint32_t f = __builtin_amdgcn_readlane(id, __builtin_ctzll(rest));
+        rest &= ~__ballot(id == f);
+        ++distinct;
+    }
+    if (__lane_id() == uint32_t(__builtin_ctzll(m))) {
+        atomicAdd(&g_diag[base], 1ull);
+        atomicAdd(&g_diag[base + 1], distinct == 1 ? 1ull : 0ull);
+        atomicAdd(&g_diag[base + 2], (unsigned long long)distinct);
+        atomicAdd(&g_diag[base + 3], (unsigned long long)__popcll(m));
+    }
+}
+#define CERES_DIAG(id, base) diag_step((id), (base))
+#else
+#define CERES_DIAG(id, base) ((void)0)
+#endif
 
 // Per-ray hit; closest hit keeps the LAST accepted hit with t <= tmax (intersect_leaf :54-60).
 struct Hit { uint32_t slot; float t, u, v; };
@@ -229,8 +307,11 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         const float4* q = reinterpret_cast<const float4*>(P.pairs);  // pair of the root's children (:81)
         float4 A = q[0], B = q[1], C = q[2];
         uint4 L = reinterpret_cast<const uint4*>(q)[3];
+        uint32_t rec = 0;
+        (void)rec;
         while (true) {                                                // :82-123
             if (kStats) ++n_pairs;
+            if (!kAnyHit) CERES_DIAG(rec, 0);
             const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];
             float le, lx, re, rx;
             slab_box<kRobust>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
@@ -249,23 +330,51 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
             if (hit_l && L.x) { k = L.y; k_end = L.y + L.x; }
             if (hit_r && L.z) { k2 = L.w; k2_end = L.w + L.z; }
             if (kStats) n_tests += (k_end - k) + (k2_end - k2);
-            float4 nA{}, nB{}, nC{};
-            uint4 nL{};
+            float4 nA, nB, nC;                                        // undefined for done lanes
+            uint4 nL;
+#if CERES_SU_PAIR
+            // one scalar fetch when every live lane continues with the same record (the data
+            // are moved into the vector registers at the top of the next step, after the leaves)
+            float4 sA, sB, sC;                                        // undefined unless suni
+            uint4 sL;
+            bool suni = false;
+            const unsigned long long live = __ballot(!done);
+            if (live) {
+                const uint32_t rn = __builtin_amdgcn_readlane(nxt, __builtin_ctzll(live));
+                suni = __ballot(!done && nxt != rn) == 0;
+                if (suni) {
+                    const SiblingPair* nq = P.pairs + rn;
+                    sA = sload_f4(nq, 0); sB = sload_f4(nq, 1); sC = sload_f4(nq, 2); sL = sload_u4(nq, 3);
+                }
+            }
+            if (!suni && !done) {
+                const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
+                nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
+            }
+#else
             if (!done) {
                 const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
                 nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
             }
+#endif
             while (k < k_end || k2 < k2_end) {
                 const uint32_t idx = k < k_end ? k++ : k2++;
+                if (!kAnyHit) CERES_DIAG(idx, 4);
                 float t, u, v;
-                if (tri_test(load_tri(P.tris + idx), o, d, tmin, tmax, t, u, v)) {
+                if (tri_test(load_tri_u(P.tris, idx), o, d, tmin, tmax, t, u, v)) {
                     best = {idx, t, u, v}; have = true;
                     if (kAnyHit) return true;
                     tmax = t;
                 }
             }
             if (done) break;
+#if CERES_SU_PAIR
+            if (suni) { A = sA; B = sB; C = sC; L = sL; }
+            else { A = nA; B = nB; C = nC; L = nL; }
+#else
             A = nA; B = nB; C = nC; L = nL;
+#endif
+            rec = nxt;
         }
         return have;
     }
@@ -348,6 +457,18 @@ __device__ __forceinline__ N4 load_n4(const Node4* n) {
     const uint4* u = reinterpret_cast<const uint4*>(n);
     return {q[0], q[1], q[2], q[3], q[4], q[5], u[6], u[7]};
 }
+// node `cur` for the active lanes: one scalar fetch when they all visit the same node
+__device__ __forceinline__ N4 load_n4_u(const Node4* nodes, uint32_t cur) {
+#if CERES_SU_NODE4
+    uint32_t r;
+    if (uniform_id(cur, r)) {
+        const Node4* q = nodes + r;
+        return {sload_f4(q, 0), sload_f4(q, 1), sload_f4(q, 2), sload_f4(q, 3), sload_f4(q, 4), sload_f4(q, 5),
+                sload_u4(q, 6), sload_u4(q, 7)};
+    }
+#endif
+    return load_n4(nodes + cur);
+}
 __device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 __device__ __forceinline__ uint32_t pick(uint4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 
@@ -363,10 +484,22 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
     uint32_t sp = 0, cur = 0;
     while (true) {
         if (kStats) ++n_pairs;
-        const float4* q = reinterpret_cast<const float4*>(P.nodes4 + cur);
-        const float4 LX = q[0], HX = q[1], LY = q[2], HY = q[3], LZ = q[4], HZ = q[5];
-        const uint4 CNT = reinterpret_cast<const uint4*>(q)[6];
-        const uint4 FST = reinterpret_cast<const uint4*>(q)[7];
+        CERES_DIAG(cur, 8);
+        float4 LX, HX, LY, HY, LZ, HZ;
+        uint4 CNT, FST;
+#if CERES_SU_NODE4
+        uint32_t rc;
+        if (uniform_id(cur, rc)) {
+            const Node4* q = P.nodes4 + rc;
+            LX = sload_f4(q, 0); HX = sload_f4(q, 1); LY = sload_f4(q, 2); HY = sload_f4(q, 3);
+            LZ = sload_f4(q, 4); HZ = sload_f4(q, 5); CNT = sload_u4(q, 6); FST = sload_u4(q, 7);
+        } else
+#endif
+        {
+            const float4* q = reinterpret_cast<const float4*>(P.nodes4 + cur);
+            LX = q[0]; HX = q[1]; LY = q[2]; HY = q[3]; LZ = q[4]; HZ = q[5];
+            CNT = reinterpret_cast<const uint4*>(q)[6]; FST = reinterpret_cast<const uint4*>(q)[7];
+        }
         float e[4], x[4];
         const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
         const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
@@ -391,8 +524,9 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
                 k_end = k + (c == 0 ? cnt[0] : c == 1 ? cnt[1] : c == 2 ? cnt[2] : cnt[3]);
                 if (kStats) n_tests += k_end - k;
             }
+            CERES_DIAG(k, 12);
             float t, u, v;
-            if (tri_test(load_tri(P.tris + k), o, d, tmin, tmax, t, u, v)) return true;
+            if (tri_test(load_tri_u(P.tris, k), o, d, tmin, tmax, t, u, v)) return true;
             ++k;
         }
         if (inner_mask) {
@@ -733,7 +867,7 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
         if (active && L.blocked[owner]) active = false;                 // another piece found an occluder
         if (active) {
             if (kStats) ++n_pairs;
-            const N4 n = load_n4(P.nodes4 + cur);
+            const N4 n = load_n4_u(P.nodes4, cur);
             float e[4];
             uint32_t leaf_mask = 0, inner_mask = 0;
 #pragma unroll
@@ -758,7 +892,7 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
                     if (kStats) n_tests += k_end - k;
                 }
                 float t, u, v;
-                if (tri_test(load_tri(P.tris + k), w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
+                if (tri_test(load_tri_u(P.tris, k), w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
                 ++k;
             }
             if (found) {
@@ -1459,6 +1593,15 @@ int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStrea
 }  // namespace ceres
 
 extern "C" {
+
+#if CERES_DIAG_UNIFORM
+int ceres_diag_read(uint64_t* out) {            // diagnostic builds only: read and zero g_diag
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(ceres::dev::g_diag), sizeof(uint64_t) * 16));
+    static const uint64_t zero[16] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(ceres::dev::g_diag), zero, sizeof(zero)));
+    return CERES_OK;
+}
+#endif
 
 const char* ceres_last_error(void) { return error_buffer(); }
 const char* ceres_version(void) { return "ceres-mi355x 0.2 (gfx950)"; }
