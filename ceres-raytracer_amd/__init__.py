@@ -22,7 +22,8 @@ import sys
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libceres_hip.so")
+# CERES_LIB: an A/B build of the same library (tools/ab.py, `make variant`); default the in-tree one
+LIB_PATH = os.environ.get("CERES_LIB") or os.path.join(_PKG, "libceres_hip.so")
 CLI_PATH = os.path.join(_PKG, "render")
 
 if _PKG not in sys.path:

@@ -51,11 +51,26 @@
 #ifndef CERES_SCALAR_UNIFORM
 #define CERES_SCALAR_UNIFORM 1 // wave-uniform record fetches through the scalar cache (see uniform_id)
 #endif
+#ifndef CERES_TILES_PER_WAVE
+#define CERES_TILES_PER_WAVE 4                // fused kernel, batches: consecutive tile-order entries per
+#endif                                        // wavefront (A/B, 8-frame batches x 8 streams: 2 -1..-3 %, 4 -3..-4 %)
+#ifndef CERES_TILE_CLUSTER
+#define CERES_TILE_CLUSTER 0                  // batches: each wavefront's tiles form a 2x2 cluster (A/B: +3..5 %, not kept)
+#endif
+#ifndef CERES_NT_STORE
+#define CERES_NT_STORE 0                      // non-temporal framebuffer stores
+#endif
+#ifndef CERES_FUSED_SHADOW_BVH2
+#define CERES_FUSED_SHADOW_BVH2 0             // batch shadow rays over the BVH2 (trace<true>) instead of the BVH4
+#endif
 #ifndef CERES_SU_PAIR
 #define CERES_SU_PAIR 0                       // ... of primary BVH2 sibling pairs (A/B: C3 -0.6 %, bunny +6 %)
 #endif
 #ifndef CERES_SU_TRI
 #define CERES_SU_TRI CERES_SCALAR_UNIFORM     // ... of leaf triangles
+#endif
+#ifndef CERES_SU_TRI2
+#define CERES_SU_TRI2 0                       // ... and of leaf triangles two distinct ones among the lanes
 #endif
 #ifndef CERES_SU_NODE4
 #define CERES_SU_NODE4 CERES_SCALAR_UNIFORM   // ... of shadow BVH4 nodes
@@ -121,6 +136,17 @@ __device__ __forceinline__ TriV load_tri_u(const Tri48* tris, uint32_t idx) {
 #if CERES_SU_TRI
     uint32_t r;
     if (uniform_id(idx, r)) return load_tri_s(tris + r);
+#if CERES_SU_TRI2
+    // two distinct triangles among the active lanes: two scalar fetches and a per-lane select
+    const unsigned long long rest = __ballot(idx != r);
+    const uint32_t r1 = __builtin_amdgcn_readlane(idx, __builtin_ctzll(rest));
+    if (__ballot(idx != r && idx != r1) == 0) {
+        const TriV a = load_tri_s(tris + r), b = load_tri_s(tris + r1);
+        const bool first = idx == r;
+        auto sel = [first](F3 x, F3 y) { return F3{first ? x.x : y.x, first ? x.y : y.y, first ? x.z : y.z}; };
+        return {sel(a.p0, b.p0), sel(a.e1, b.e1), sel(a.e2, b.e2), sel(a.n, b.n)};
+    }
+#endif
 #endif
     return load_tri(tris + idx);
 }
@@ -304,6 +330,37 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         // Same steps, software-pipelined: the next record (near child or stack top) follows from
         // this step's box tests alone (the leaf hits only lower tmax for LATER steps, :89-121),
         // so its load is issued before this step's triangle tests and overlaps them.
+#if CERES_SU_PAIR
+        // Two copies of the step: one on a record the whole wavefront shares, read through the
+        // scalar cache into SGPRs (sA..sL, used by the box tests as scalar operands -- no TA/TD
+        // traffic, no copies), one on a per-lane record in VGPRs (vA..vL).  The next step's
+        // record is fetched the same way, chosen by whether every live lane continues with it.
+        float4 sA, sB, sC, vA, vB, vC;
+        uint4 sL, vL;
+        {
+            const SiblingPair* q0 = P.pairs;                                 // root's children (:81)
+            sA = sload_f4(q0, 0); sB = sload_f4(q0, 1); sC = sload_f4(q0, 2); sL = sload_u4(q0, 3);
+        }
+        bool uni = true;
+        while (true) {                                                // :82-123
+            if (kStats) ++n_pairs;
+            const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];
+            float le, lx, re, rx;
+            uint4 L;
+            // (the empty asm markers keep the compiler from merging the two copies into one
+            // with per-operand selects, which would cost 32 VALU per step)
+            if (uni) {                                                // SGPR operands
+                slab_box<kRobust>(sl, sA.x, sA.y, sA.z, sA.w, sB.x, sB.y, tmin, tmax, le, lx);
+                slab_box<kRobust>(sl, sB.z, sB.w, sC.x, sC.y, sC.z, sC.w, tmin, tmax, re, rx);
+                L = sL;
+                asm volatile("; uniform pair" ::);
+            } else {
+                slab_box<kRobust>(sl, vA.x, vA.y, vA.z, vA.w, vB.x, vB.y, tmin, tmax, le, lx);
+                slab_box<kRobust>(sl, vB.z, vB.w, vC.x, vC.y, vC.z, vC.w, tmin, tmax, re, rx);
+                L = vL;
+                asm volatile("; per-lane pair" ::);
+            }
+#else
         const float4* q = reinterpret_cast<const float4*>(P.pairs);  // pair of the root's children (:81)
         float4 A = q[0], B = q[1], C = q[2];
         uint4 L = reinterpret_cast<const uint4*>(q)[3];
@@ -316,6 +373,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
             float le, lx, re, rx;
             slab_box<kRobust>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
             slab_box<kRobust>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
+#endif
             const bool hit_l = le <= lx, hit_r = re <= rx;
             const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
             const bool both = go_l && go_r, none = !go_l && !go_r;
@@ -330,28 +388,25 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
             if (hit_l && L.x) { k = L.y; k_end = L.y + L.x; }
             if (hit_r && L.z) { k2 = L.w; k2_end = L.w + L.z; }
             if (kStats) n_tests += (k_end - k) + (k2_end - k2);
-            float4 nA, nB, nC;                                        // undefined for done lanes
-            uint4 nL;
 #if CERES_SU_PAIR
-            // one scalar fetch when every live lane continues with the same record (the data
-            // are moved into the vector registers at the top of the next step, after the leaves)
-            float4 sA, sB, sC;                                        // undefined unless suni
-            uint4 sL;
-            bool suni = false;
+            bool un = false;
             const unsigned long long live = __ballot(!done);
             if (live) {
                 const uint32_t rn = __builtin_amdgcn_readlane(nxt, __builtin_ctzll(live));
-                suni = __ballot(!done && nxt != rn) == 0;
-                if (suni) {
+                un = __ballot(!done && nxt != rn) == 0;
+                if (un) {
                     const SiblingPair* nq = P.pairs + rn;
                     sA = sload_f4(nq, 0); sB = sload_f4(nq, 1); sC = sload_f4(nq, 2); sL = sload_u4(nq, 3);
                 }
             }
-            if (!suni && !done) {
+            if (!un && !done) {
                 const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
-                nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
+                vA = nq[0]; vB = nq[1]; vC = nq[2]; vL = reinterpret_cast<const uint4*>(nq)[3];
             }
+            uni = un;
 #else
+            float4 nA, nB, nC;                                        // undefined for done lanes
+            uint4 nL;
             if (!done) {
                 const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
                 nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
@@ -368,13 +423,10 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
                 }
             }
             if (done) break;
-#if CERES_SU_PAIR
-            if (suni) { A = sA; B = sB; C = sC; L = sL; }
-            else { A = nA; B = nB; C = nC; L = nL; }
-#else
+#if !CERES_SU_PAIR
             A = nA; B = nB; C = nC; L = nL;
-#endif
             rec = nxt;
+#endif
         }
         return have;
     }
@@ -568,6 +620,18 @@ __device__ __forceinline__ uint8_t quantize(float x) {               // static.c
 __device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32_t lr, uint32_t i, float c0, float c1,
                                             float c2) {
     const size_t frame_base = size_t(f) * P.local_rows;
+#if CERES_NT_STORE
+    // A/B: streaming (non-temporal) framebuffer stores, so they do not evict the scene from L2
+    if (P.pixels) {
+        float* q = P.pixels + 3 * ((frame_base + lr) * P.W + i);
+        __builtin_nontemporal_store(c0, q); __builtin_nontemporal_store(c1, q + 1); __builtin_nontemporal_store(c2, q + 2);
+    }
+    if (P.rgb8) {
+        uint8_t* q = P.rgb8 + 3 * ((frame_base + (P.local_rows - 1 - lr)) * P.W + i);
+        __builtin_nontemporal_store(quantize(c0), q); __builtin_nontemporal_store(quantize(c1), q + 1);
+        __builtin_nontemporal_store(quantize(c2), q + 2);
+    }
+#else
     if (P.pixels) {
         float* q = P.pixels + 3 * ((frame_base + lr) * P.W + i);
         q[0] = c0; q[1] = c1; q[2] = c2;
@@ -576,6 +640,7 @@ __device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32
         uint8_t* q = P.rgb8 + 3 * ((frame_base + (P.local_rows - 1 - lr)) * P.W + i);
         q[0] = quantize(c0); q[1] = quantize(c1); q[2] = quantize(c2);
     }
+#endif
 }
 
 __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t lr) {
@@ -1072,8 +1137,19 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     // kB = 64: one 8x8 tile per single-wavefront workgroup, so a long tile holds only its own
     // LDS and wave slot, never three finished siblings' (LDS is released per workgroup).
     constexpr uint32_t kTile = kB == 256 ? 16 : 8;
-    const uint32_t t = __builtin_amdgcn_readfirstlane(P.tile_order[blockIdx.x]);
+    // kTPW consecutive entries of the order per wavefront in batches (throughput: fewer, longer
+    // wavefronts -- the background tiles' short waves are mostly launch and first-fetch latency);
+    // one per wavefront for single frames (latency: their longest tiles set the frame time) and
+    // in stats builds (the wave log is per tile)
+    constexpr uint32_t kTPW = (kStats || kB != 64 || kSteal) ? 1 : CERES_TILES_PER_WAVE;
     const uint32_t per_frame = P.tiles_x * P.row_blocks_per_frame;
+    const uint32_t n_tiles = per_frame * P.frames;
+    uint32_t n_shadow = 0, occluded = 0, n_pairs = 0, n_tests = 0;
+    bool overflow = false;
+    for (uint32_t q = 0; q < kTPW; ++q) {
+    const uint32_t slot_q = blockIdx.x * kTPW + q;
+    if (kTPW > 1 && slot_q >= n_tiles) break;
+    const uint32_t t = __builtin_amdgcn_readfirstlane(P.tile_order[slot_q]);
     const uint32_t f = t / per_frame;
     const uint32_t rem = t - f * per_frame;
     const uint32_t by = rem / P.tiles_x, bx = rem - by * P.tiles_x;
@@ -1083,8 +1159,6 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;
     bool hit = false;
     Hit h{0, 0.f, 0.f, 0.f};
-    uint32_t n_pairs = 0, n_tests = 0;
-    bool overflow = false;
     RayWork w{};
     uint64_t t_start = 0;
     if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
@@ -1110,7 +1184,8 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
             w = make_shadow_ray<kRobust>(p, f3(P.cam[f].sun));
         }
     }
-    const uint32_t n_shadow = __popcll(__ballot(hit));
+    const uint32_t n_shadow_t = __popcll(__ballot(hit));
+    n_shadow += n_shadow_t;
     uint64_t t_primary = 0;
     uint32_t prim_pairs = n_pairs, shadow_iters = 0;
     if (kStats && P.wave_log) t_primary = __builtin_amdgcn_s_memrealtime();
@@ -1120,8 +1195,15 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     if constexpr (kSteal)
         steal_traverse<kStats, kB, StkT, kRobust>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
     else
+    {
+#if CERES_FUSED_SHADOW_BVH2
+        // A/B: any-hit over the reference BVH2 with the pipelined step of trace()
+        Hit h2{0, 0.f, 0.f, 0.f};
+        L.blocked[tid] = hit && trace<true, kStats, kB, StkT, kRobust>(P, w.o, w.d, stk, h2, n_pairs, n_tests, overflow) ? 1u : 0u;
+#else
         L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
-    uint32_t occluded = 0;
+#endif
+    }
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
@@ -1133,8 +1215,9 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
         if (lane == 0) {
             unsigned long long* wl = P.wave_log + 8 * size_t(blockIdx.x * (kB / 64) + wave);
             wl[0] = t_start; wl[1] = t_primary; wl[2] = t_end; wl[3] = mx; wl[4] = shadow_iters;
-            wl[5] = n_shadow; wl[6] = sp; wl[7] = ss;
+            wl[5] = n_shadow_t; wl[6] = sp; wl[7] = ss;
         }
+    }
     }
     const uint32_t wo = wave_sum(occluded);
     const uint32_t wave_id = blockIdx.x * (kB / 64) + wave;
@@ -1273,6 +1356,38 @@ int ensure_workspace(ceres_scene* s, size_t jobs, size_t px, bool want_px, bool 
 
 constexpr uint32_t kFusedWG = CERES_FUSED_WG;
 
+// Caches `order` on the scene under its key (see ensure_tile_order) and uploads it.
+int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, uint32_t frames, uint32_t tile,
+                      uint32_t cluster, const std::vector<uint32_t>& order, hipStream_t stream, const uint32_t** out) {
+    const size_t n = order.size();
+    ceres_scene::TileOrder o;
+    if (s->orders.size() >= ceres::kMaxTileOrders) {
+        auto lru = std::min_element(s->orders.begin(), s->orders.end(),
+                                    [](const auto& a, const auto& b) { return a.used < b.used; });
+        for (auto& u : lru->uses) {                                  // launches that read it have ended
+            HIP_TRY(hipEventSynchronize(u.second));
+            (void)hipEventDestroy(u.second);
+        }
+        o.d = lru->d; o.cap = lru->cap;
+        s->orders.erase(lru);
+        if (o.cap < n) { dfree(o.d); o.cap = 0; }
+    }
+    o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile; o.cluster = cluster;
+    if (!o.d) {
+        HIP_TRY(hipMalloc(&o.d, n * sizeof(uint32_t)));
+        o.cap = n;
+    }
+    if (hipMemcpyAsync(o.d, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess) {
+        dfree(o.d);
+        return set_error(CERES_EHIP, "tile order upload failed");
+    }
+    o.used = ++s->order_clock;
+    s->orders.push_back(o);
+    *out = o.d;
+    return CERES_OK;
+}
+
 // Centre-first order of a batch's tile x tile tiles for the fused kernel: ascending distance of the
 // tile centre (global pixel coordinates) from the image centre, frames interleaved.  Cached
 // on the scene per (W, H, tiling, frames, tile) -- up to kMaxTileOrders orders; the least
@@ -1280,17 +1395,58 @@ constexpr uint32_t kFusedWG = CERES_FUSED_WG;
 // events, mark_tile_order), and its buffer is reused when large enough, so eviction stalls
 // neither the other streams nor the device.
 int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, size_t rows, uint32_t frames,
-                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out) {
+                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out,
+                      uint32_t cluster = 1) {
     for (auto& o : s->orders)
         if (o.W == W && o.H == H && o.row_block == t.row_block && o.rank == t.rank && o.world == t.world &&
-            o.frames == frames && o.tile == tile) {
+            o.frames == frames && o.tile == tile && o.cluster == cluster) {
             o.used = ++s->order_clock;
             *out = o.d;
             return CERES_OK;
         }
     const size_t n = size_t(bx) * by * frames;
-    std::vector<std::pair<double, uint32_t>> k(n);
     const double cx = 0.5 * double(W), cy = 0.5 * double(H);
+    if (cluster > 1) {
+        // Batches (several tiles per wavefront, kTPW): the order is built over clusters of
+        // cluster x cluster tiles, each expanded into its tiles consecutively, so the tiles one
+        // wavefront renders in turn are neighbours and share their BVH nodes and triangles in
+        // the CU's vector L1 (the loads' tail latency is set by L1 misses).  Clusters are
+        // centre-first and shuffled in windows for the XCD balance, as tiles are below.
+        const uint32_t cbx = (bx + cluster - 1) / cluster, cby = (by + cluster - 1) / cluster;
+        const size_t nc = size_t(cbx) * cby * frames;
+        std::vector<std::pair<double, uint32_t>> kc(nc);
+        const uint32_t span = cluster * tile;
+        for (uint32_t f = 0; f < frames; ++f)
+            for (uint32_t y = 0; y < cby; ++y) {
+                const size_t lr = std::min<size_t>(size_t(y) * span + span / 2, rows - 1);
+                const size_t j = ((lr / t.row_block) * t.world + t.rank) * t.row_block + lr % t.row_block;
+                for (uint32_t x = 0; x < cbx; ++x) {
+                    const double dx = double(x) * span + span / 2 - cx, dy = double(j) - cy;
+                    const uint32_t id = (f * cby + y) * cbx + x;
+                    kc[id] = {dx * dx + dy * dy, id};
+                }
+            }
+        std::stable_sort(kc.begin(), kc.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+        uint64_t st = 0x9e3779b97f4a7c15ull;
+        const size_t win = std::max<size_t>(1, CERES_TILE_SHUFFLE_WINDOW / (cluster * cluster));
+        for (size_t b0 = 0; b0 < nc; b0 += win) {
+            const size_t len = std::min<size_t>(win, nc - b0);
+            for (size_t q = len - 1; q > 0; --q) {
+                st = st * 6364136223846793005ull + 1442695040888963407ull;
+                std::swap(kc[b0 + q], kc[b0 + size_t((st >> 33) % (q + 1))]);
+            }
+        }
+        std::vector<uint32_t> order;
+        order.reserve(n);
+        for (const auto& c : kc) {
+            const uint32_t f = c.second / (cbx * cby), r = c.second % (cbx * cby);
+            const uint32_t y0 = (r / cbx) * cluster, x0 = (r % cbx) * cluster;
+            for (uint32_t y = y0; y < std::min(y0 + cluster, by); ++y)
+                for (uint32_t x = x0; x < std::min(x0 + cluster, bx); ++x) order.push_back((f * by + y) * bx + x);
+        }
+        return upload_tile_order(s, W, H, t, frames, tile, cluster, order, stream, out);
+    }
+    std::vector<std::pair<double, uint32_t>> k(n);
     for (uint32_t f = 0; f < frames; ++f)
         for (uint32_t y = 0; y < by; ++y) {
             const size_t lr = std::min<size_t>(size_t(y) * tile + tile / 2, rows - 1);
@@ -1359,32 +1515,7 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     for (size_t b0 = 0; frames > 1 && b0 + 8 <= n; b0 += 8)
         std::rotate(order.begin() + b0, order.begin() + b0 + (b0 / 8) % 8, order.begin() + b0 + 8);
 #endif
-    ceres_scene::TileOrder o;
-    if (s->orders.size() >= ceres::kMaxTileOrders) {
-        auto lru = std::min_element(s->orders.begin(), s->orders.end(),
-                                    [](const auto& a, const auto& b) { return a.used < b.used; });
-        for (auto& u : lru->uses) {                                  // launches that read it have ended
-            HIP_TRY(hipEventSynchronize(u.second));
-            (void)hipEventDestroy(u.second);
-        }
-        o.d = lru->d; o.cap = lru->cap;
-        s->orders.erase(lru);
-        if (o.cap < n) { dfree(o.d); o.cap = 0; }
-    }
-    o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile;
-    if (!o.d) {
-        HIP_TRY(hipMalloc(&o.d, n * sizeof(uint32_t)));
-        o.cap = n;
-    }
-    if (hipMemcpyAsync(o.d, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, stream) != hipSuccess ||
-        hipStreamSynchronize(stream) != hipSuccess) {
-        dfree(o.d);
-        return set_error(CERES_EHIP, "tile order upload failed");
-    }
-    o.used = ++s->order_clock;
-    s->orders.push_back(o);
-    *out = o.d;
-    return CERES_OK;
+    return upload_tile_order(s, W, H, t, frames, tile, 1, order, stream, out);
 }
 
 // One batch: `frames` cameras (basis12 = frames x {eye, dir, iu, iv}) and suns (frames x 3).
@@ -1450,8 +1581,12 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     constexpr uint32_t ftile = kFusedWG == 256 ? 16 : 8;
     const uint32_t fbx = uint32_t((W + ftile - 1) / ftile), fby = uint32_t((rows + ftile - 1) / ftile);
     const uint32_t* tile_order = nullptr;
+    // batches render CERES_TILES_PER_WAVE consecutive tiles per wavefront: 2x2 clusters of them
+    const bool clustered = CERES_FUSED_WG == 64 && CERES_TILES_PER_WAVE == 4 && CERES_TILE_CLUSTER &&
+                           !(s->flags & CERES_SCENE_STATS) && !(CERES_FUSED_STEAL == 1 || (CERES_FUSED_STEAL == 2 && frames == 1));
     if (CERES_FUSED && mode == CERES_MODE_FULL && rows)
-        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order)) return rc;
+        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order, clustered ? 2 : 1))
+            return rc;
     // The shards must start at zero when they are read back (counters) or hold the two-pass
     // shadow queue; the fused kernel without counters only adds to them, so its steady-state
     // frames skip the memset (ceres_finalize re-zeroes them after every counted render).
@@ -1472,7 +1607,11 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             P.tile_order = tile_order;
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
-            const dim3 fgrid(fbx * fby * frames), fblock(kFusedWG);
+            // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
+            const bool steal = CERES_FUSED_STEAL == 1 || (CERES_FUSED_STEAL == 2 && frames == 1);
+            const uint32_t tpw = (kFusedWG == 64 && !stats && !steal) ? CERES_TILES_PER_WAVE : 1;   // = kTPW
+            const uint32_t n_tiles = fbx * fby * frames;
+            const dim3 fgrid((n_tiles + tpw - 1) / tpw), fblock(kFusedWG);
             if (stats) {                                             // per-wave diagnostic timeline
                 const size_t waves = size_t(fbx) * fby * frames * (kFusedWG / 64);
                 if (s->wave_log_waves < waves) {
@@ -1496,8 +1635,6 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
                 else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
                 else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);
             };
-            // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
-            const bool steal = CERES_FUSED_STEAL == 1 || (CERES_FUSED_STEAL == 2 && frames == 1);
             auto fused_s = [&](auto rt) {
                 if (steal) fused(rt, std::true_type{});
                 else fused(rt, std::false_type{});

@@ -27,7 +27,7 @@ struct ceres_scene {
     // recorded after its latest such launch; evicting the order waits on those events only.
     struct TileOrder {
         size_t W = 0, H = 0;
-        uint32_t row_block = 0, rank = 0, world = 0, frames = 0, tile = 0;
+        uint32_t row_block = 0, rank = 0, world = 0, frames = 0, tile = 0, cluster = 1;
         uint32_t* d = nullptr;
         size_t cap = 0;                // entries allocated at d
         uint64_t used = 0;
