@@ -177,6 +177,8 @@ def main():
     ap.add_argument("--collect", choices=("exchange", "gather"), default="exchange",
                     help="N > 1: every frame of a step to one owner rank in one all-to-all (exchange; frames a "
                          "multiple of N) or all frames to rank 0 (gather)")
+    ap.add_argument("--prime-s", type=float, default=0.3,
+                    help="untimed setup: seconds of steps before the W warmup steps (GPU clock ramp)")
     ap.add_argument("--streams", type=int, default=8,
                     help="HIP streams the steps rotate over (step k on stream k %% S, its own buffers): step k+1 "
                          "fills the tail of step k")
@@ -322,10 +324,22 @@ def main():
         if rank == 0 and parity is not None:
             parity["all_frames_match_one_gpu_render"] = bool(flag.item())
 
-    # setup (untimed, before the W warmup steps): one step on every stream and collective slot,
-    # so no stream's first launch lands in the timed region when W < S
+    # setup (untimed, before the W warmup steps): steps over every stream and collective slot for
+    # at least --prime-s seconds, so no stream's first launch lands in the timed region when
+    # W < S and the GPU has left its idle clock state (measured: K = 20 after W = 5 from a cold
+    # start ran 6 % below the same K after W = 200; after this priming they agree)
+    t_prime = time.perf_counter()
     for k in range(slots):
         step(k)
+    drain()
+    torch.cuda.synchronize(dev)
+    per_step = max((time.perf_counter() - t_prime) / slots, 1e-5)
+    # the same number of steps on every rank (each step is a collective)
+    more = torch.tensor([min(20000, max(0, int(args.prime_s / per_step) - slots))], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(more, op=dist.ReduceOp.MAX)
+    for k in range(int(more.item())):
+        step(slots + k)
     drain()
     torch.cuda.synchronize(dev)
     for k in range(args.warmup):

@@ -57,6 +57,18 @@
 #ifndef CERES_TILE_CLUSTER
 #define CERES_TILE_CLUSTER 0                  // batches: each wavefront's tiles form a 2x2 cluster (A/B: +3..5 %, not kept)
 #endif
+#ifndef CERES_FOOTPRINT_PAD
+#define CERES_FOOTPRINT_PAD 0                 // diagnostic: pad the pair records to 2x their footprint
+#endif
+#ifndef CERES_DIAG_EXTRA_LOAD
+#define CERES_DIAG_EXTRA_LOAD 0               // diagnostic: an extra vector load per primary step
+#endif
+#ifndef CERES_DIAG_EXTRA_VALU
+#define CERES_DIAG_EXTRA_VALU 0               // diagnostic: N extra dependent VALU per primary step
+#endif
+#ifndef CERES_LANE_QUADS
+#define CERES_LANE_QUADS 0                    // fused kernel: quads of lanes are 2x2 pixel blocks (else 4x1)
+#endif
 #ifndef CERES_NT_STORE
 #define CERES_NT_STORE 0                      // non-temporal framebuffer stores
 #endif
@@ -189,17 +201,46 @@ struct Stk24 {
 #define CERES_DIAG_UNIFORM 0
 #endif
 #if CERES_DIAG_UNIFORM
-__device__ unsigned long long g_diag[16];
-__device__ __forceinline__ void diag_step(uint32_t id, int base) {
-    const unsigned long long m = __ballot(1);
+__device__ unsigned long long g_diag[34];
+__device__ const uint32_t* g_diag_parent;     // pair index -> pair index of its parent (host-built)
+__device__ __forceinline__ uint32_t count_distinct(uint32_t id) {
     uint32_t distinct = 0;
-    unsigned long long rest = m;
+    unsigned long long rest = __ballot(1);
     while (rest) {
         const uint32_t f = __builtin_amdgcn_readlane(id, __builtin_ctzll(rest));
         rest &= ~__ballot(id == f);
         ++distinct;
     }
+    return distinct;
+}
+__device__ __forceinline__ void diag_step(uint32_t id, int base) {
+    const unsigned long long m = __ballot(1);
+    const uint32_t distinct = count_distinct(id);
+    if (base == 0) {
+        // primary BVH2 records: distinct 128-B lines now (two 64-B records per line, DFS order)
+        // and with sibling records paired in one line (distinct parents)
+        const uint32_t lines = count_distinct(id >> 1);
+        const uint32_t parents = count_distinct(id == 0 ? 0xffffffffu : g_diag_parent[id]);
+        if (__lane_id() == uint32_t(__builtin_ctzll(m))) {
+            atomicAdd(&g_diag[32], (unsigned long long)lines);
+            atomicAdd(&g_diag[33], (unsigned long long)parents);
+        }
+    }
+    // quads of lanes (4k..4k+3): active quads, quads whose active lanes share one record, and
+    // wave-steps where every active quad does (g_diag[16 + base / 4 * 4 ..])
+    const uint32_t q0 = __shfl(id, __lane_id() & ~3u, 64), q1 = __shfl(id, (__lane_id() & ~3u) + 1, 64);
+    const uint32_t q2 = __shfl(id, (__lane_id() & ~3u) + 2, 64), q3 = __shfl(id, (__lane_id() & ~3u) + 3, 64);
+    const unsigned long long qa = m >> (__lane_id() & ~3u) & 0xfull;
+    const bool quni = (!(qa & 1) || q0 == id) && (!(qa & 2) || q1 == id) && (!(qa & 4) || q2 == id) && (!(qa & 8) || q3 == id);
+    const unsigned long long qbad = __ballot(!quni);
+    uint32_t nq = 0, nqu = 0;
+    for (int k = 0; k < 16; ++k) {
+        if (m >> (4 * k) & 0xfull) { ++nq; if (!(qbad >> (4 * k) & 0xfull)) ++nqu; }
+    }
     if (__lane_id() == uint32_t(__builtin_ctzll(m))) {
+        atomicAdd(&g_diag[16 + base], (unsigned long long)nq);
+        atomicAdd(&g_diag[16 + base + 1], (unsigned long long)nqu);
+        atomicAdd(&g_diag[16 + base + 2], qbad == 0 ? 1ull : 0ull);
         atomicAdd(&g_diag[base], 1ull);
         atomicAdd(&g_diag[base + 1], distinct == 1 ? 1ull : 0ull);
         atomicAdd(&g_diag[base + 2], (unsigned long long)distinct);
@@ -325,6 +366,13 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     }
     const Slab<kRobust> sl = make_slab<kRobust>(o, d);
     uint32_t sp = 0;
+#if CERES_DIAG_EXTRA_LOAD || CERES_DIAG_EXTRA_VALU
+    float diag_sink = 0.f;
+    struct SinkGuard {                                // keeps the diagnostic work alive
+        float& v; const KParams& P;
+        __device__ ~SinkGuard() { if (P.frames == 0xffffffffu) P.pixels[0] = v; }
+    } guard{diag_sink, P};
+#endif
 #if CERES_PREFETCH_NEXT
     if (!(kStats && ss)) {
         // Same steps, software-pipelined: the next record (near child or stack top) follows from
@@ -407,10 +455,29 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
 #else
             float4 nA, nB, nC;                                        // undefined for done lanes
             uint4 nL;
+#if CERES_DIAG_EXTRA_LOAD >= 2
+            float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
             if (!done) {
                 const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
                 nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
+#if CERES_DIAG_EXTRA_LOAD
+                // diagnostic A/B: one more dwordx4 per step (TA/TD sensitivity)
+#if CERES_DIAG_EXTRA_LOAD == 1                                  // 4 x dword
+                const volatile float* xq = reinterpret_cast<const volatile float*>(nq + 1 + (nxt & 1));
+                diag_sink += xq[0] + xq[1] + xq[2] + xq[3];
+#elif CERES_DIAG_EXTRA_LOAD == 2                                // 1 x dwordx4, consumed after the leaves
+                xv = reinterpret_cast<const float4*>(P.tris + nxt)[0];   // nxt < n_pairs < n_tri
+#else                                                             // the same by a quarter of the lanes
+                if ((__lane_id() & 3) == 0) xv = reinterpret_cast<const float4*>(P.tris + nxt)[0];
+#endif
+#endif
             }
+#endif
+#if CERES_DIAG_EXTRA_VALU
+            // diagnostic A/B: a chain of dependent VALU per step (issue sensitivity)
+#pragma unroll
+            for (int z = 0; z < CERES_DIAG_EXTRA_VALU; ++z) diag_sink = __builtin_fmaf(diag_sink, 0.999f, le);
 #endif
             while (k < k_end || k2 < k2_end) {
                 const uint32_t idx = k < k_end ? k++ : k2++;
@@ -422,6 +489,9 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
                     tmax = t;
                 }
             }
+#if CERES_DIAG_EXTRA_LOAD >= 2
+            diag_sink += xv.x + xv.y + xv.z + xv.w;
+#endif
             if (done) break;
 #if !CERES_SU_PAIR
             A = nA; B = nB; C = nC; L = nL;
@@ -1153,8 +1223,14 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     const uint32_t f = t / per_frame;
     const uint32_t rem = t - f * per_frame;
     const uint32_t by = rem / P.tiles_x, bx = rem - by * P.tiles_x;
-    const uint32_t i = bx * kTile + (kB == 256 ? (wave & 1) * 8 : 0) + (lane & 7);
-    const uint32_t lr = by * kTile + (kB == 256 ? (wave >> 1) * 8 : 0) + (lane >> 3);
+#if CERES_LANE_QUADS
+    // lane -> pixel with every quad of lanes (4k..4k+3) a 2x2 pixel block
+    const uint32_t lx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4), ly = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
+#else
+    const uint32_t lx = lane & 7, ly = lane >> 3;
+#endif
+    const uint32_t i = bx * kTile + (kB == 256 ? (wave & 1) * 8 : 0) + lx;
+    const uint32_t lr = by * kTile + (kB == 256 ? (wave >> 1) * 8 : 0) + ly;
     const bool active = i < P.W && lr < P.local_rows;
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;
     bool hit = false;
@@ -1733,8 +1809,8 @@ extern "C" {
 
 #if CERES_DIAG_UNIFORM
 int ceres_diag_read(uint64_t* out) {            // diagnostic builds only: read and zero g_diag
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(ceres::dev::g_diag), sizeof(uint64_t) * 16));
-    static const uint64_t zero[16] = {};
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(ceres::dev::g_diag), sizeof(uint64_t) * 34));
+    static const uint64_t zero[34] = {};
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(ceres::dev::g_diag), zero, sizeof(zero)));
     return CERES_OK;
 }
@@ -1776,8 +1852,35 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     uint32_t stack4 = 0, not_collapsed = 0;
     if (!rlc && build_shadow_bvh4(pairs, nodes4, stack4, not_collapsed)) return nullptr;
     if (nodes4.empty()) nodes4.emplace_back();
+#if CERES_FOOTPRINT_PAD
+    {   // diagnostic A/B only: every pair record followed by an unused one (2x the primary BVH's
+        // cache footprint, same traversal) -- how sensitive is the kernel to L1/L2 capacity?
+        std::vector<SiblingPair> padded(2 * pairs.size());
+        for (size_t q = 0; q < pairs.size(); ++q) {
+            SiblingPair r = pairs[q];
+            if (r.lcount == 0) r.lfirst *= 2;
+            if (r.rcount == 0) r.rfirst *= 2;
+            padded[2 * q] = r;
+            padded[2 * q + 1] = r;
+        }
+        pairs.swap(padded);
+    }
+#endif
     auto* s = new (std::nothrow) ceres_scene;
     if (!s) { set_error(CERES_ENOMEM, "out of host memory"); return nullptr; }
+#if CERES_DIAG_UNIFORM
+    {
+        std::vector<uint32_t> parent(pairs.size(), 0);
+        for (size_t q = 0; q < pairs.size(); ++q) {
+            if (pairs[q].lcount == 0) parent[pairs[q].lfirst] = uint32_t(q);
+            if (pairs[q].rcount == 0) parent[pairs[q].rfirst] = uint32_t(q);
+        }
+        uint32_t* d = nullptr;
+        if (hipMalloc(&d, parent.size() * 4) == hipSuccess &&
+            hipMemcpy(d, parent.data(), parent.size() * 4, hipMemcpyHostToDevice) == hipSuccess)
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(ceres::dev::g_diag_parent), &d, sizeof(d));
+    }
+#endif
     s->n_nodes4 = nodes4.size();
     s->shadow_stack_entries = std::max<uint32_t>(1, stack4);
     s->device = device; s->flags = flags; s->n_tri = n_tri; s->n_pairs = pairs.size();

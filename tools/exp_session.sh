@@ -1,12 +1,10 @@
 set -u; cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-V=ceres-raytracer_amd/variants
-L=${LIBS:-"ceres-raytracer_amd/libceres_hip.so $V/libceres_hip_tpw2.so $V/libceres_hip_tpw4.so"}
-summ() { grep -v amdgpu.ids $1 | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['config'], '$2', {k[12:-3]: v['median_ms'] for k, v in d['results'].items()}, all(v['parity'] for v in d['results'].values()))"; }
-for c in ${CONFIGS:-dragon_1080 bunny_1080}; do
-  if [ "${SOLO:-1}" = 1 ]; then
-  timeout -k 10 300 python tools/ab.py $c ${ROUNDS:-20} $L > gpurun_out/abs_$c.log 2>&1 || { tail -5 gpurun_out/abs_$c.log; exit 3; }
-  summ gpurun_out/abs_$c.log solo
-  fi
-  AB_STREAMS=8 AB_BATCH=8 AB_FRAMES=64 timeout -k 10 300 python tools/ab.py $c ${ROUNDS:-8} $L > gpurun_out/ab_$c.log 2>&1 || { tail -5 gpurun_out/ab_$c.log; exit 3; }
-  summ gpurun_out/ab_$c.log batch8x8
+run() { timeout -k 10 200 python bench.py --no-cpu-baseline --no-roofline "$@" > gpurun_out/e.log 2>&1 || { tail -3 gpurun_out/e.log; exit 3; }; python -c "import json,sys; d=json.loads(open('gpurun_out/e.log').read().strip().splitlines()[-1]); print(sys.argv[1:], d['value'], d['ms_per_step'])" "$@"; }
+for r in 1 2; do
+run --steps 20 --warmup 5
+run --steps 20 --warmup 200
+run --steps 20 --warmup 5 --frames-per-gpu 16
+run --steps 20 --warmup 5 --frames-per-gpu 32
+run --steps 200 --warmup 20
+run --steps 200 --warmup 20 --frames-per-gpu 16
 done
