@@ -25,7 +25,7 @@ Scene upload, OBJ load and BVH build are outside the timed region, as in the ref
 Also reported (rank 0):
   roofline      dominant kernel's algorithmic bytes per launch (pinned reference statistics,
                 SURVEY.md §8(d): 64 B per node-pair visit + 56 B per triangle test) / its mean
-                device duration from HIP events on the launch stream, vs 8 TB/s HBM peak, for
+                device duration from HIP events around back-to-back launches on their stream, vs 8 TB/s HBM peak, for
                 one full C3 frame on one GPU; traffic = rocprofv3 --pmc FETCH_SIZE (gfx950 x2
                 correction) per launch from profiles/pmc_summary.json.
   cpu_baseline  the REFERENCE hot path (oracle/_ref/ref_render, reference CMake flags) timed
@@ -370,22 +370,39 @@ def main():
         solo = pkg.Tiling(H, 0, 1)
         solo_rgb = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
         solo_px = torch.empty(3 * W * H, dtype=torch.float32, device=dev)
-        scene.set_timing(True)
         n_t = max(10, min(args.steps, 200))
+        for _ in range(3):                            # the solo frame's tile order, warm
+            scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
+                                d_rgb8=solo_rgb.data_ptr(), stream=sh)
+        # n_t back-to-back launches between two HIP events on their stream: mean launch duration
+        # (per-launch event pairs would add each launch's dispatch latency, ~13 us here)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fused = "ceres_fused" in pkg.lib().ceres_kernel_names().decode()
+        p_ms = s_ms = 0.0
+        if not fused and mode == pkg.MODE_FULL:       # two-pass build: per-launch primary / shadow split
+            scene.set_timing(True)
+            for _ in range(n_t):
+                scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
+                                    d_rgb8=solo_rgb.data_ptr(), stream=sh)
+            p_ms, s_ms, _ = scene.read_timing()
+            scene.set_timing(False)
+        ev0.record(stream)
         for _ in range(n_t):
             scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
                                 d_rgb8=solo_rgb.data_ptr(), stream=sh)
-        p_ms, s_ms, n = scene.read_timing()
-        scene.set_timing(False)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        mean_ms = ev0.elapsed_time(ev1) / n_t
         ex = meta["exact"]
         b_p = 64 * ex["primary_pairs"] + 56 * ex["primary_tests"]
         b_s = 64 * ex["shadow_pairs"] + 56 * ex["shadow_tests"]
-        if mode == pkg.MODE_FULL and s_ms == 0.0:     # one fused kernel per frame
-            kern = {"ceres_fused": (p_ms / n, b_p + b_s)}
-        else:
-            kern = {"ceres_primary": (p_ms / n, b_p)}
-            if mode == pkg.MODE_FULL:
-                kern["ceres_shadow"] = (s_ms / n, b_s)
+        if mode == pkg.MODE_FULL and fused:           # one fused kernel per frame
+            kern = {"ceres_fused": (mean_ms, b_p + b_s)}
+        elif mode != pkg.MODE_FULL:                   # primary-only: one kernel
+            kern = {"ceres_primary": (mean_ms, b_p)}
+        else:                                         # two-pass build: split by the per-launch events
+            kern = {"ceres_primary": (mean_ms * p_ms / (p_ms + s_ms), b_p),
+                    "ceres_shadow": (mean_ms * s_ms / (p_ms + s_ms), b_s)}
         name = max(kern, key=lambda k: kern[k][0])
         ms, nbytes = kern[name]
         achieved = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0

@@ -333,7 +333,6 @@ int render64(ceres_scene* s, const double basis12[12], const double sun[3], int 
     if (mode == CERES_MODE_PRIMARY) hipLaunchKernelGGL(ceres_render64<CERES_MODE_PRIMARY>, grid, block, lds, s->stream, P);
     else hipLaunchKernelGGL(ceres_render64<CERES_MODE_FULL>, grid, block, lds, s->stream, P);
     HIP64_TRY(hipGetLastError());
-    if (int rc = mark_tile_order(s, P.tile_order, s->stream)) return rc;
     HIP64_TRY(hipEventRecord(e1, s->stream));
     std::vector<Shard> sh(kShards);
     HIP64_TRY(hipMemcpyAsync(sh.data(), s->d_shards, sizeof(Shard) * kShards, hipMemcpyDeviceToHost, s->stream));

@@ -1392,11 +1392,9 @@ void ceres::scene_release(ceres_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     dfree(s->d_pairs64); dfree(s->d_tris64); dfree(s->d_norms64);
-    for (auto& o : s->orders) {
-        dfree(o.d);
-        for (auto& u : o.uses) (void)hipEventDestroy(u.second);
-    }
-    s->orders.clear();
+    for (auto& o : s->orders) dfree(o.d);
+    for (auto& d : s->retired) dfree(d);
+    s->orders.clear(); s->retired.clear(); s->retired_bytes = 0;
     dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
@@ -1440,13 +1438,15 @@ int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     if (s->orders.size() >= ceres::kMaxTileOrders) {
         auto lru = std::min_element(s->orders.begin(), s->orders.end(),
                                     [](const auto& a, const auto& b) { return a.used < b.used; });
-        for (auto& u : lru->uses) {                                  // launches that read it have ended
-            HIP_TRY(hipEventSynchronize(u.second));
-            (void)hipEventDestroy(u.second);
-        }
-        o.d = lru->d; o.cap = lru->cap;
+        s->retired.push_back(lru->d);                                // a launch may still read it
+        s->retired_bytes += lru->cap * sizeof(uint32_t);
         s->orders.erase(lru);
-        if (o.cap < n) { dfree(o.d); o.cap = 0; }
+        if (s->retired_bytes > ceres::kRetiredBytes) {
+            HIP_TRY(hipDeviceSynchronize());
+            for (auto& d : s->retired) dfree(d);
+            s->retired.clear();
+            s->retired_bytes = 0;
+        }
     }
     o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile; o.cluster = cluster;
     if (!o.d) {
@@ -1466,10 +1466,9 @@ int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
 
 // Centre-first order of a batch's tile x tile tiles for the fused kernel: ascending distance of the
 // tile centre (global pixel coordinates) from the image centre, frames interleaved.  Cached
-// on the scene per (W, H, tiling, frames, tile) -- up to kMaxTileOrders orders; the least
-// recently used one is evicted once the launches that read it have ended (its per-stream
-// events, mark_tile_order), and its buffer is reused when large enough, so eviction stalls
-// neither the other streams nor the device.
+// on the scene per (W, H, tiling, frames, tile, cluster) -- up to kMaxTileOrders orders; the
+// least recently used one is retired (freed later, see ceres_scene::retired), so eviction
+// neither rewrites an order a launch in flight reads nor stalls the streams.
 int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, size_t rows, uint32_t frames,
                       uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out,
                       uint32_t cluster = 1) {
@@ -1718,7 +1717,6 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             if (robust) fused_s(std::true_type{});
             else fused_s(std::false_type{});
             HIP_TRY(hipGetLastError());
-            if (int rc = ceres::mark_tile_order(s, tile_order, stream)) return rc;
             if (e1) HIP_TRY(hipEventRecord(e1, stream));
             if (e2) HIP_TRY(hipEventRecord(e2, stream));
         } else {
@@ -1780,24 +1778,6 @@ void fill_stats(ceres_stats* st, const uint64_t c[8], double ms) {
 }  // namespace
 
 namespace ceres {
-int mark_tile_order(ceres_scene* s, const uint32_t* d, hipStream_t stream) {
-    for (auto& o : s->orders) {
-        if (o.d != d) continue;
-        hipEvent_t* ev = nullptr;
-        for (auto& u : o.uses)
-            if (u.first == stream) ev = &u.second;     // stream order: the latest record covers earlier ones
-        if (!ev) {
-            hipEvent_t e;
-            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            o.uses.push_back({stream, e});
-            ev = &o.uses.back().second;
-        }
-        HIP_TRY(hipEventRecord(*ev, stream));
-        return CERES_OK;
-    }
-    return set_error(CERES_EINVAL, "tile order not cached");
-}
-
 int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out) {
     const ceres_tiling t{uint32_t(H), 0, 1};
     return ensure_tile_order(s, W, H, t, H, 1, uint32_t((W + tile - 1) / tile), uint32_t((H + tile - 1) / tile), tile,

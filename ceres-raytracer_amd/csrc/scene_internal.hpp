@@ -21,19 +21,21 @@ struct ceres_scene {
     size_t n_nodes4 = 0;
     SiblingPair* d_pairs = nullptr;
     Node4* d_nodes4 = nullptr;
-    // fused-kernel tile orders, one per (frame size, tiling, batch, tile), never rewritten while
-    // a launch that reads them may be in flight: launches on different streams may read different
-    // orders concurrently.  `uses` holds one event per stream that launched with the order,
-    // recorded after its latest such launch; evicting the order waits on those events only.
+    // fused-kernel tile orders, one per (frame size, tiling, batch, tile), never rewritten or
+    // freed while a launch that reads them may be in flight (launches on different streams may
+    // read different orders concurrently): an evicted order's buffer goes to `retired` and is
+    // freed only once retired buffers exceed kRetiredBytes, after one device synchronise -- no
+    // per-launch events, and no stall while the working set of shapes fits the cache.
     struct TileOrder {
         size_t W = 0, H = 0;
         uint32_t row_block = 0, rank = 0, world = 0, frames = 0, tile = 0, cluster = 1;
         uint32_t* d = nullptr;
         size_t cap = 0;                // entries allocated at d
         uint64_t used = 0;
-        std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
     };
     std::vector<TileOrder> orders;
+    std::vector<uint32_t*> retired;
+    size_t retired_bytes = 0;
     uint64_t order_clock = 0;
     Tri48* d_tris = nullptr;
     uint32_t* d_orig = nullptr;
@@ -66,7 +68,6 @@ namespace ceres {
 void scene_release(ceres_scene* s);          // frees every device buffer and the stream (render_hip.hip)
 // centre-first, XCD-balanced order of one whole frame's tile x tile tiles (render_hip.hip)
 int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out);
-// records, after a launch on `stream` that reads tile order `d`, the event eviction waits on
-int mark_tile_order(ceres_scene* s, const uint32_t* d, hipStream_t stream);
 constexpr size_t kMaxTileOrders = 16;         // cached orders per scene before LRU eviction
+constexpr size_t kRetiredBytes = 64u << 20;   // evicted orders kept until they exceed this
 }
