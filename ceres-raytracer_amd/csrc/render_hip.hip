@@ -69,6 +69,9 @@
 #ifndef CERES_LANE_QUADS
 #define CERES_LANE_QUADS 0                    // fused kernel: quads of lanes are 2x2 pixel blocks (else 4x1)
 #endif
+#ifndef CERES_TRI_FIRST
+#define CERES_TRI_FIRST 0                     // trace(): first leaf triangle fetched before the next record (+12 VGPRs: spills, 2x slower)
+#endif
 #ifndef CERES_NT_STORE
 #define CERES_NT_STORE 0                      // non-temporal framebuffer stores
 #endif
@@ -453,6 +456,18 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
             }
             uni = un;
 #else
+#if CERES_TRI_FIRST
+            // The first leaf triangle's fetch goes out before the next record's: vmcnt retires in
+            // issue order, so the first test then waits for its triangle only, not for the
+            // prefetch as well.
+            const bool any_leaf = k < k_end || k2 < k2_end;
+            TriV tr0;
+            uint32_t idx0 = 0;
+            if (any_leaf) {
+                idx0 = k < k_end ? k++ : k2++;
+                tr0 = load_tri_u(P.tris, idx0);
+            }
+#endif
             float4 nA, nB, nC;                                        // undefined for done lanes
             uint4 nL;
 #if CERES_DIAG_EXTRA_LOAD >= 2
@@ -478,6 +493,17 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
             // diagnostic A/B: a chain of dependent VALU per step (issue sensitivity)
 #pragma unroll
             for (int z = 0; z < CERES_DIAG_EXTRA_VALU; ++z) diag_sink = __builtin_fmaf(diag_sink, 0.999f, le);
+#endif
+#if CERES_TRI_FIRST
+            if (any_leaf) {
+                if (!kAnyHit) CERES_DIAG(idx0, 4);
+                float t, u, v;
+                if (tri_test(tr0, o, d, tmin, tmax, t, u, v)) {
+                    best = {idx0, t, u, v}; have = true;
+                    if (kAnyHit) return true;
+                    tmax = t;
+                }
+            }
 #endif
             while (k < k_end || k2 < k2_end) {
                 const uint32_t idx = k < k_end ? k++ : k2++;
@@ -827,7 +853,7 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 }
 
 #ifndef CERES_FUSED_MINW16
-#define CERES_FUSED_MINW16 7     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes
+#define CERES_FUSED_MINW16 7     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes (round 2: 6 waves / 80 VGPRs: C3 bench -1 %, 4096^2 batches -4 %)
 #endif
 #ifndef CERES_FUSED_MINW32
 #define CERES_FUSED_MINW32 1     // ... and 32-bit-stack scenes (1 = no constraint)
