@@ -69,6 +69,9 @@
 #ifndef CERES_LANE_QUADS
 #define CERES_LANE_QUADS 0                    // fused kernel: quads of lanes are 2x2 pixel blocks (else 4x1)
 #endif
+#ifndef CERES_SU_ROOT
+#define CERES_SU_ROOT 0                       // trace(): the root record through the scalar cache (A/B: -1..+2 %, noise)
+#endif
 #ifndef CERES_TRI_FIRST
 #define CERES_TRI_FIRST 0                     // trace(): first leaf triangle fetched before the next record (+12 VGPRs: spills, 2x slower)
 #endif
@@ -412,9 +415,16 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
                 asm volatile("; per-lane pair" ::);
             }
 #else
+#if CERES_SU_ROOT
+        // the root's children (:81): the same record for every ray, read through the scalar
+        // cache (its latency is exposed: nothing else is in flight yet)
+        float4 A = sload_f4(P.pairs, 0), B = sload_f4(P.pairs, 1), C = sload_f4(P.pairs, 2);
+        uint4 L = sload_u4(P.pairs, 3);
+#else
         const float4* q = reinterpret_cast<const float4*>(P.pairs);  // pair of the root's children (:81)
         float4 A = q[0], B = q[1], C = q[2];
         uint4 L = reinterpret_cast<const uint4*>(q)[3];
+#endif
         uint32_t rec = 0;
         (void)rec;
         while (true) {                                                // :82-123
