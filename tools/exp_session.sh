@@ -1,4 +1,9 @@
 set -u; cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-make -C tools/probes 2>/dev/null >/dev/null || true
-timeout -k 10 300 python tools/bvh_bench.py --config proc_c5 --reps 5 --host-reps 0 > gpurun_out/bvh.log 2>&1; echo bvh rc=$?; tail -1 gpurun_out/bvh.log | cut -c1-400
-timeout -k 10 400 python tools/pipeline_bench.py proc_c5 > gpurun_out/pipe.log 2>&1; echo pipe rc=$?; tail -1 gpurun_out/pipe.log | cut -c1-600
+run() { timeout -k 10 200 python bench.py --no-cpu-baseline --no-roofline "$@" > gpurun_out/e.log 2>&1 || { tail -3 gpurun_out/e.log; exit 3; }; python -c "import json,sys; d=json.loads(open('gpurun_out/e.log').read().strip().splitlines()[-1]); print(sys.argv[1:], d['value'], d['ms_per_step'])" "$@"; }
+for r in 1 2; do
+run --steps 20 --warmup 5
+run --steps 20 --warmup 5 --frames-per-gpu 16
+run --steps 20 --warmup 5 --streams 4
+run --steps 20 --warmup 5 --streams 16
+run --steps 20 --warmup 5 --frames-per-gpu 4 --streams 16
+done
