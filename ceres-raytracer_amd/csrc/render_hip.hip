@@ -52,7 +52,7 @@
 #define CERES_SCALAR_UNIFORM 1 // wave-uniform record fetches through the scalar cache (see uniform_id)
 #endif
 #ifndef CERES_TILES_PER_WAVE
-#define CERES_TILES_PER_WAVE 4                // fused kernel, batches: consecutive tile-order entries per
+#define CERES_TILES_PER_WAVE 4                // fused kernel, batches: consecutive tile-order entries (1 or 4) per
 #endif                                        // wavefront (A/B, 8-frame batches x 8 streams: 2 -1..-3 %, 4 -3..-4 %)
 #ifndef CERES_TILE_CLUSTER
 #define CERES_TILE_CLUSTER 0                  // batches: each wavefront's tiles form a 2x2 cluster (A/B: +3..5 %, not kept)
@@ -132,6 +132,9 @@ typedef uint32_t U4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 sload_f4(const void* p, int i) {
     const F4v v = ((const __attribute__((address_space(4))) F4v*)(p))[i];
     return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t sload_u32(const void* p) {
+    return *((const __attribute__((address_space(4))) uint32_t*)(p));
 }
 __device__ __forceinline__ uint4 sload_u4(const void* p, int i) {
     const U4v v = ((const __attribute__((address_space(4))) U4v*)(p))[i];
@@ -1252,10 +1255,17 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     const uint32_t n_tiles = per_frame * P.frames;
     uint32_t n_shadow = 0, occluded = 0, n_pairs = 0, n_tests = 0;
     bool overflow = false;
+    // this wavefront's tile-order entries, read once through the scalar cache (a vector load of a
+    // uniform address would put a full vector-memory round trip in front of every tile; the order
+    // buffer is padded to a multiple of 4 entries)
+    static_assert(kTPW == 1 || kTPW == 4, "CERES_TILES_PER_WAVE must be 1 or 4");
+    uint4 tiles4;
+    if constexpr (kTPW == 4) tiles4 = sload_u4(P.tile_order + 4 * size_t(blockIdx.x), 0);
+    else tiles4.x = sload_u32(P.tile_order + blockIdx.x);
     for (uint32_t q = 0; q < kTPW; ++q) {
     const uint32_t slot_q = blockIdx.x * kTPW + q;
     if (kTPW > 1 && slot_q >= n_tiles) break;
-    const uint32_t t = __builtin_amdgcn_readfirstlane(P.tile_order[slot_q]);
+    const uint32_t t = kTPW == 1 ? tiles4.x : q == 0 ? tiles4.x : q == 1 ? tiles4.y : q == 2 ? tiles4.z : tiles4.w;
     const uint32_t f = t / per_frame;
     const uint32_t rem = t - f * per_frame;
     const uint32_t by = rem / P.tiles_x, bx = rem - by * P.tiles_x;
@@ -1485,11 +1495,15 @@ int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
         }
     }
     o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile; o.cluster = cluster;
+    // padded to a multiple of 4 entries (zeros): the fused kernel reads its tile-order entries
+    // four at a time through the scalar cache
+    const size_t padded = (n + 3) / 4 * 4;
     if (!o.d) {
-        HIP_TRY(hipMalloc(&o.d, n * sizeof(uint32_t)));
-        o.cap = n;
+        HIP_TRY(hipMalloc(&o.d, padded * sizeof(uint32_t)));
+        o.cap = padded;
     }
-    if (hipMemcpyAsync(o.d, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, stream) != hipSuccess ||
+    if ((padded > n && hipMemsetAsync(o.d + n, 0, (padded - n) * sizeof(uint32_t), stream) != hipSuccess) ||
+        hipMemcpyAsync(o.d, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess) {
         dfree(o.d);
         return set_error(CERES_EHIP, "tile order upload failed");
