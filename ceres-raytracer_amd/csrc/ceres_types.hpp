@@ -58,16 +58,25 @@ struct alignas(16) SiblingPair64 {
 };
 static_assert(sizeof(SiblingPair64) == 112, "SiblingPair64");
 
-// Shadow-ray BVH4 record (build_shadow_bvh4, scene_host.cpp): 4 child boxes as SoA float4
-// rows, then per-child count (0 inner -> first = Node4 index; kNode4Empty unused slot;
-// else leaf of `count` triangles from leaf slot `first`).  128 B = one L2 line.
+// Shadow-ray BVH4 record (build_shadow_bvh4, scene_host.cpp; k_nodes4, scene_device.hip): 4 child
+// boxes as SoA float4 rows, then one packed word per child: first << 5 | count (count 0: inner,
+// first = Node4 index; 1..31: leaf of `count` triangles from leaf slot `first`), kNode4Empty for
+// an unused slot.  One word per child keeps a traversal step at 7 vector loads instead of 8 (the
+// kernel pays per load instruction).  128 B = one L2 line; the last 16 B are unused.
 constexpr uint32_t kNode4Empty = 0xffffffffu;
+constexpr uint32_t kNode4CountBits = 5;
+constexpr uint32_t kNode4MaxCount = (1u << kNode4CountBits) - 1;             // 31
+constexpr uint32_t kNode4MaxFirst = (1u << (32 - kNode4CountBits)) - 2;      // keeps clear of kNode4Empty
 struct alignas(128) Node4 {
     float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
-    uint32_t count[4];
-    uint32_t first[4];
+    uint32_t child[4];
+    uint32_t unused[4];
 };
 static_assert(sizeof(Node4) == 128, "Node4");
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint32_t node4_child(uint32_t count, uint32_t first) { return first << kNode4CountBits | count; }
 
 struct ShadowJob {             // one queued shadow ray (render.hpp:127-136), 32 B
     uint32_t pixel;            // batch pixel index = (frame * local_rows + local_row) * W + i

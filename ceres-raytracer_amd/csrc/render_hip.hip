@@ -612,12 +612,14 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
 // same fma/min/max restatement as trace(), the triangles of every passing leaf, then descend
 // into the nearest passing inner child and push the others.  The order only changes how soon
 // an occluder is found, never whether one is.
-struct N4 { float4 lx, hx, ly, hy, lz, hz; uint4 cnt, fst; };
+struct N4 { float4 lx, hx, ly, hy, lz, hz; uint4 ch; };   // ch: packed child words (Node4::child)
 __device__ __forceinline__ N4 load_n4(const Node4* n) {
     const float4* q = reinterpret_cast<const float4*>(n);
     const uint4* u = reinterpret_cast<const uint4*>(n);
-    return {q[0], q[1], q[2], q[3], q[4], q[5], u[6], u[7]};
+    return {q[0], q[1], q[2], q[3], q[4], q[5], u[6]};
 }
+__device__ __forceinline__ uint32_t n4_count(uint32_t w) { return w & kNode4MaxCount; }
+__device__ __forceinline__ uint32_t n4_first(uint32_t w) { return w >> kNode4CountBits; }
 // node `cur` for the active lanes: one scalar fetch when they all visit the same node
 __device__ __forceinline__ N4 load_n4_u(const Node4* nodes, uint32_t cur) {
 #if CERES_SU_NODE4
@@ -625,7 +627,7 @@ __device__ __forceinline__ N4 load_n4_u(const Node4* nodes, uint32_t cur) {
     if (uniform_id(cur, r)) {
         const Node4* q = nodes + r;
         return {sload_f4(q, 0), sload_f4(q, 1), sload_f4(q, 2), sload_f4(q, 3), sload_f4(q, 4), sload_f4(q, 5),
-                sload_u4(q, 6), sload_u4(q, 7)};
+                sload_u4(q, 6)};
     }
 #endif
     return load_n4(nodes + cur);
@@ -647,30 +649,32 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
         if (kStats) ++n_pairs;
         CERES_DIAG(cur, 8);
         float4 LX, HX, LY, HY, LZ, HZ;
-        uint4 CNT, FST;
+        uint4 CH;
 #if CERES_SU_NODE4
         uint32_t rc;
         if (uniform_id(cur, rc)) {
             const Node4* q = P.nodes4 + rc;
             LX = sload_f4(q, 0); HX = sload_f4(q, 1); LY = sload_f4(q, 2); HY = sload_f4(q, 3);
-            LZ = sload_f4(q, 4); HZ = sload_f4(q, 5); CNT = sload_u4(q, 6); FST = sload_u4(q, 7);
+            LZ = sload_f4(q, 4); HZ = sload_f4(q, 5); CH = sload_u4(q, 6);
         } else
 #endif
         {
             const float4* q = reinterpret_cast<const float4*>(P.nodes4 + cur);
             LX = q[0]; HX = q[1]; LY = q[2]; HY = q[3]; LZ = q[4]; HZ = q[5];
-            CNT = reinterpret_cast<const uint4*>(q)[6]; FST = reinterpret_cast<const uint4*>(q)[7];
+            CH = reinterpret_cast<const uint4*>(q)[6];
         }
         float e[4], x[4];
         const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
         const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
         const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
-        const uint32_t cnt[4] = {CNT.x, CNT.y, CNT.z, CNT.w}, fst[4] = {FST.x, FST.y, FST.z, FST.w};
+        const uint32_t chw[4] = {CH.x, CH.y, CH.z, CH.w};
+        const uint32_t cnt[4] = {n4_count(CH.x), n4_count(CH.y), n4_count(CH.z), n4_count(CH.w)};
+        const uint32_t fst[4] = {n4_first(CH.x), n4_first(CH.y), n4_first(CH.z), n4_first(CH.w)};
         uint32_t leaf_mask = 0, inner_mask = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             slab_box<kRobust>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e[c], x[c]);
-            const bool hit = e[c] <= x[c] && cnt[c] != kNode4Empty;
+            const bool hit = e[c] <= x[c] && chw[c] != kNode4Empty;
             leaf_mask |= (hit && cnt[c] != 0) ? (1u << c) : 0u;
             inner_mask |= (hit && cnt[c] == 0) ? (1u << c) : 0u;
         }
@@ -1049,8 +1053,8 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
                 float x;
                 slab_box<kRobust>(slab_of<kRobust>(w), pick(n.lx, c), pick(n.hx, c), pick(n.ly, c), pick(n.hy, c),
                                   pick(n.lz, c), pick(n.hz, c), tmin, tmax, e[c], x);
-                const uint32_t cn = pick(n.cnt, c);
-                const bool hit = e[c] <= x && cn != kNode4Empty;
+                const uint32_t w = pick(n.ch, c), cn = n4_count(w);
+                const bool hit = e[c] <= x && w != kNode4Empty;
                 leaf_mask |= (hit && cn != 0) ? (1u << c) : 0u;
                 inner_mask |= (hit && cn == 0) ? (1u << c) : 0u;
             }
@@ -1061,8 +1065,8 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
                     if (!leaf_mask) break;
                     const uint32_t c = __builtin_ctz(leaf_mask);
                     leaf_mask &= leaf_mask - 1;
-                    k = pick(n.fst, c);
-                    k_end = k + pick(n.cnt, c);
+                    k = n4_first(pick(n.ch, c));
+                    k_end = k + n4_count(pick(n.ch, c));
                     if (kStats) n_tests += k_end - k;
                 }
                 float t, u, v;
@@ -1083,11 +1087,11 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
                 while (rest) {
                     const uint32_t c = __builtin_ctz(rest);
                     rest &= rest - 1;
-                    stk[top * kS] = pick(n.fst, c);
+                    stk[top * kS] = n4_first(pick(n.ch, c));
                     top = top + 1 == cap ? 0 : top + 1;
                     ++cnt;
                 }
-                cur = pick(n.fst, best);
+                cur = n4_first(pick(n.ch, best));
             } else if (cnt) {
                 top = (top == 0 ? cap : top) - 1;
                 cur = stk[top * kS];

@@ -32,7 +32,7 @@ namespace scenedev {
 
 using namespace devscan;
 
-enum : uint32_t { kErrRange = 1, kErrLeaf = 2, kErrShared = 4, kErrPrim = 8 };
+enum : uint32_t { kErrRange = 1, kErrLeaf = 2, kErrShared = 4, kErrPrim = 8, kErrNode4 = 16 };
 
 __device__ __forceinline__ bool inside(const float* c, const float* p) {          // build_shadow_bvh4 `inside`
     return c[0] >= p[0] && c[1] <= p[1] && c[2] >= p[2] && c[3] <= p[3] && c[4] >= p[4] && c[5] <= p[5];
@@ -139,7 +139,8 @@ __global__ void __launch_bounds__(256) k_pairs(const RefNode* __restrict__ nodes
 
 // one Node4 per BVH4 head (build_shadow_bvh4's record)
 __global__ void __launch_bounds__(256) k_nodes4(const RefNode* __restrict__ nodes, uint32_t n_nodes, const uint32_t* __restrict__ f4,
-                                                const uint32_t* __restrict__ node4_of, Node4* __restrict__ out) {
+                                                const uint32_t* __restrict__ node4_of, Node4* __restrict__ out,
+                                                uint32_t* __restrict__ err) {
     const uint32_t x = blockIdx.x * 256u + threadIdx.x;
     if (x >= n_nodes || !f4[x]) return;
     struct Entry { uint32_t node; };
@@ -160,16 +161,18 @@ __global__ void __launch_bounds__(256) k_nodes4(const RefNode* __restrict__ node
     for (int q = 0; q < 4; ++q) {
         if (q >= n) {
             r.lo_x[q] = r.hi_x[q] = r.lo_y[q] = r.hi_y[q] = r.lo_z[q] = r.hi_z[q] = 0.f;
-            r.count[q] = kNode4Empty; r.first[q] = 0;
+            r.child[q] = kNode4Empty;
             continue;
         }
         const RefNode& e = nodes[ent[q]];
         r.lo_x[q] = e.bounds[0]; r.hi_x[q] = e.bounds[1];
         r.lo_y[q] = e.bounds[2]; r.hi_y[q] = e.bounds[3];
         r.lo_z[q] = e.bounds[4]; r.hi_z[q] = e.bounds[5];
-        r.count[q] = e.primitive_count;
-        r.first[q] = e.primitive_count ? e.first_child_or_primitive : node4_of[ent[q]];
+        const uint32_t first = e.primitive_count ? e.first_child_or_primitive : node4_of[ent[q]];
+        if (e.primitive_count > kNode4MaxCount || first > kNode4MaxFirst) atomicOr(err, uint32_t(kErrNode4));
+        r.child[q] = node4_child(e.primitive_count, first);
     }
+    for (int q = 0; q < 4; ++q) r.unused[q] = 0;
     out[node4_of[x]] = r;
 }
 
@@ -269,13 +272,19 @@ int relayout_device(const Tri48* d_tris, uint32_t n_tri, const RefNode* d_nodes,
             SD_TRY(hipMalloc(&out.pairs, size_t(np) * sizeof(SiblingPair)));
             SD_TRY(hipMalloc(&out.nodes4, size_t(out.n_nodes4) * sizeof(Node4)));
             hipLaunchKernelGGL(k_pairs, dim3((n_nodes + 255) / 256), dim3(256), 0, stream, d_nodes, n_nodes, inner, pair_of, out.pairs);
-            hipLaunchKernelGGL(k_nodes4, dim3((n_nodes + 255) / 256), dim3(256), 0, stream, d_nodes, n_nodes, f4, node4_of, out.nodes4);
+            hipLaunchKernelGGL(k_nodes4, dim3((n_nodes + 255) / 256), dim3(256), 0, stream, d_nodes, n_nodes, f4, node4_of, out.nodes4,
+                               ctr + 2);
             SD_TRY(hipGetLastError());
         }
         uint32_t perr = 0;
         SD_TRY(hipMemcpyAsync(&perr, ctr + 2, 4, hipMemcpyDeviceToHost, stream));
         SD_TRY(hipStreamSynchronize(stream));
         if (perr & kErrPrim) { rc = set_error(CERES_EINVAL, "primitive index out of range"); goto done; }
+        if (perr & kErrNode4) {
+            rc = set_error(CERES_EUNSUPPORTED, "shadow BVH4: a leaf of more than %u triangles or an index above 2^27",
+                           kNode4MaxCount);
+            goto done;
+        }
     }
 #undef SD_TRY
 done:

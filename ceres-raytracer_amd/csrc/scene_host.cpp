@@ -568,19 +568,23 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
         stack_bound = std::max(stack_bound, acc);
         Node4 rec{};
         for (int c = 0; c < 4; ++c) {
-            if (c >= n) { rec.count[c] = kNode4Empty; rec.first[c] = 0; continue; }
+            if (c >= n) { rec.child[c] = kNode4Empty; continue; }
             rec.lo_x[c] = ents[c].box[0]; rec.hi_x[c] = ents[c].box[1];
             rec.lo_y[c] = ents[c].box[2]; rec.hi_y[c] = ents[c].box[3];
             rec.lo_z[c] = ents[c].box[4]; rec.hi_z[c] = ents[c].box[5];
-            rec.count[c] = ents[c].count;
             if (ents[c].count) {
-                rec.first[c] = ents[c].first;
+                if (ents[c].count > kNode4MaxCount || ents[c].first > kNode4MaxFirst)
+                    return set_error(CERES_EUNSUPPORTED, "shadow BVH4: leaf of %u triangles at slot %u (at most %u "
+                                     "triangles per leaf, slots below 2^27)", ents[c].count, ents[c].first, kNode4MaxCount);
+                rec.child[c] = node4_child(ents[c].count, ents[c].first);
             } else {
                 if (out.size() > pairs.size() || ents[c].first >= pairs.size())   // a tree has fewer records than pairs
                     return set_error(CERES_EINVAL, "build_shadow_bvh4: sibling pairs do not form a tree");
-                rec.first[c] = uint32_t(out.size());
+                if (out.size() > kNode4MaxFirst) return set_error(CERES_EUNSUPPORTED, "shadow BVH4: more than 2^27 records");
+                const uint32_t idx = uint32_t(out.size());
+                rec.child[c] = node4_child(0, idx);
                 out.emplace_back();
-                st.push_back({ents[c].first, rec.first[c], acc});
+                st.push_back({ents[c].first, idx, acc});
             }
         }
         out[it.node4] = rec;
