@@ -870,7 +870,7 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 }
 
 #ifndef CERES_FUSED_MINW16
-#define CERES_FUSED_MINW16 7     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes (round 2: 6 waves / 80 VGPRs: C3 bench -1 %, 4096^2 batches -4 %)
+#define CERES_FUSED_MINW16 6     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes (no-SLP build: 6 waves / 80 VGPRs beat 7 / 72 with spills: bench +0.7 %)
 #endif
 #ifndef CERES_FUSED_MINW32
 #define CERES_FUSED_MINW32 1     // ... and 32-bit-stack scenes (1 = no constraint)
