@@ -4,15 +4,15 @@
 Workload (default): C3 = dragon.obj 1920x1080, primary + shadow rays, static.cpp camera
 (static.cpp:38-47,72-73) -- the configuration BASELINE.json's metric is quoted on.
 
-A step renders F frames (F = --frames, default = 8 per GPU): views of the anim.cpp:76-88 orbit
-of the C3 camera + sun about z, frame 0 = C3 exactly.  At N = 1 a step is eight C3-size frames
-(the full orbit in 45-degree steps); at N GPUs it is 8N distinct frames over the same orbit,
-45/N degrees apart (step_views) -- WEAK scaling, eight frames' work per GPU from the same orbit
-at every N.
+A step renders F frames (F = --frames, default = 16 per GPU): views of the anim.cpp:76-88 orbit
+of the C3 camera + sun about z, frame 0 = C3 exactly.  At N = 1 a step is sixteen C3-size frames
+(the full orbit in 22.5-degree steps); at N GPUs it is 16N distinct frames over the same orbit,
+22.5/N degrees apart (step_views) -- WEAK scaling, sixteen frames' work per GPU from the same
+orbit at every N (one batch launch per 64 frames).
 Every frame's rows are interleaved over the ranks in blocks of --row-block rows (balanced
 load); each rank renders its rows of all F frames with one ceres_render_batch_device launch,
 RGB8 + float framebuffers in HBM, then ONE RCCL collective per step: by default each frame is
-gathered to one owner rank (rank q owns 8 of the 8N frames; all the per-frame gathers are one
+gathered to one owner rank (rank q owns 16 of the 16N frames; all the per-frame gathers are one
 all-to-all, so no rank's xGMI ingress carries the whole step; ceres_assemble_rgb8_packed
 un-interleaves a rank's frames), or with
 --collect gather all F frames go to rank 0.  Steps rotate over --streams HIP streams (own
@@ -168,7 +168,7 @@ def main():
     ap.add_argument("--config", default="dragon_1080")
     ap.add_argument("--frames", type=int, default=0,
                     help="orbit frames per step (default: --frames-per-gpu x number of GPUs)")
-    ap.add_argument("--frames-per-gpu", type=int, default=8,
+    ap.add_argument("--frames-per-gpu", type=int, default=16,
                     help="frames of work per GPU per step when --frames is not given (weak scaling)")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -216,7 +216,9 @@ def main():
     mesh, bvh, cam = pkg.prepare(cfg)
     scene = pkg.Scene(mesh, bvh, device=local_rank)
     # explicit --frames: F distinct orbit views spread over the ranks; default: --frames-per-gpu views
-    b12, s3 = step_views(pkg, cfg, meta, cam, F, max(1, F // world) if args.frames else args.frames_per_gpu)
+    # the orbit is 8 views 45 degrees apart (BENCH_ORBIT, a full turn); a step of F frames samples
+    # it F / 8 times finer (frame f at f x 360 / F degrees), at every N
+    b12, s3 = step_views(pkg, cfg, meta, cam, F, max(1, F // world) if args.frames else min(8, F))
     exchange = world > 1 and args.collect == "exchange" and F % world == 0
     if exchange:
         # batch order for the all-to-all: rank q owns batch frames q*k .. q*k+k-1, which are orbit
@@ -245,11 +247,24 @@ def main():
     slots = max(2, S)
     pending = [False] * slots
 
+    MAXF = 64                                    # frames per ceres_render_batch_device launch (kMaxFrames)
+    chunk_counters = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range((F + MAXF - 1) // MAXF)]
+
     def render(slot, st, with_counters=False):
+        # one launch per (at most) 64 frames of the step; frame f's rows at f * 3 * W * rows
         px = d_px[slot % S]
-        scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=tiling,
-                                  d_pixels=0 if px is None else px.data_ptr(), d_rgb8=gather.local_ptr(slot),
-                                  d_counters=counters.data_ptr() if with_counters else 0, stream=st.cuda_stream)
+        fb = 3 * W * max(rows, 1)
+        for c, f0 in enumerate(range(0, F, MAXF)):
+            f1 = min(F, f0 + MAXF)
+            scene.render_batch_device(b12[f0:f1], s3[f0:f1], W, H, mode=mode, tiling=tiling,
+                                      d_pixels=0 if px is None else px.data_ptr() + 4 * fb * f0,
+                                      d_rgb8=gather.local_ptr(slot) + fb * f0,
+                                      d_counters=chunk_counters[c].data_ptr() if with_counters else 0,
+                                      stream=st.cuda_stream)
+        if with_counters:
+            with torch.cuda.stream(st):
+                cs = torch.stack(chunk_counters)
+                counters.copy_(torch.cat([cs[:, :6].sum(0), cs[:, 6:7].max(0).values, cs[:, 7:].sum(0)]))
 
     def step(k):
         slot = k % slots
