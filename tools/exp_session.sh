@@ -1,9 +1,3 @@
 set -u; cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-run() { timeout -k 10 200 python bench.py --no-cpu-baseline --no-roofline "$@" > gpurun_out/e.log 2>&1 || { tail -3 gpurun_out/e.log; exit 3; }; python -c "import json,sys; d=json.loads(open('gpurun_out/e.log').read().strip().splitlines()[-1]); print(sys.argv[1:], d['value'], d['ms_per_step'])" "$@"; }
-for r in 1 2; do
-run --steps 20 --warmup 5
-run --steps 20 --warmup 5 --frames-per-gpu 16
-run --steps 20 --warmup 5 --streams 4
-run --steps 20 --warmup 5 --streams 16
-run --steps 20 --warmup 5 --frames-per-gpu 4 --streams 16
-done
+CERES_LIB=$PWD/ceres-raytracer_amd/variants/libceres_hip_pk1.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scene.py -q -x -k "not dropin" --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -ne 0 ] && exit $rc
+SOLO=1 LIBS="ceres-raytracer_amd/libceres_hip.so ceres-raytracer_amd/variants/libceres_hip_pk1.so" CONFIGS="dragon_1080 bunny_1080 dragon_4096 proc_c5" bash tools/ab_batch_session.sh
