@@ -141,7 +141,10 @@ int ceres_orbit_cameras_f64(const double eye[3], const double dir[3], const doub
 /* Upload a scene to HIP device `device` (re-laid for the GPU: sibling-pair 64-B node records,
  * triangles permuted into leaf order).  The caller keeps ownership of its host arrays; they
  * may be freed after the call.  Returns NULL on failure (see ceres_last_error).
- * Replaces the (bvh, triangles, tri_norms) arguments of render() (render.hpp:87-88). */
+ * Replaces the (bvh, triangles, tri_norms) arguments of render() (render.hpp:87-88).
+ * Limits (CERES_EUNSUPPORTED): below 2^32 triangles and nodes; the shadow-ray BVH4 packs each
+ * child in one word, so leaves hold at most 31 triangles (BinnedSahBuilder's hold at most 16)
+ * and triangle slots / BVH4 records stay below 2^27. */
 ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* norm36,
                                 const void* nodes32, size_t n_nodes, const uint64_t* prim64,
                                 int device, uint32_t flags);
