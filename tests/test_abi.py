@@ -119,3 +119,27 @@ int main() {
     r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I/root/reference/lib", "-I" + os.path.join(REPO, "include"),
                         str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_scene_rejects_leaf_too_large_for_packed_bvh4(pkg):
+    """The shadow BVH4 packs a child in one word (Node4::child: first << 5 | count), so a leaf of
+    more than 31 triangles is refused at scene creation -- on the host, before any device call
+    (CERES_EUNSUPPORTED), on a GPU box and off it alike."""
+    import numpy as np
+    n = 41
+    tri = np.zeros((n, 12), np.float32)                  # {p0, e1, e2, n}: any finite values
+    tri[:, 3] = 1.0
+    tri[:, 8] = 1.0
+    nor = np.zeros((n, 9), np.float32)
+    nodes = np.zeros(3, dtype=[("b", np.float32, 6), ("count", np.uint32), ("first", np.uint32)])
+    nodes["b"][:] = [-1, 1, -1, 1, -1, 1]
+    nodes[0]["count"], nodes[0]["first"] = 0, 1           # root: children 1 and 2
+    nodes[1]["count"], nodes[1]["first"] = 40, 0          # a leaf of 40 triangles
+    nodes[2]["count"], nodes[2]["first"] = 1, 40
+    prim = np.arange(n, dtype=np.uint64)
+    L = pkg.lib()
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))     # noqa: E731
+    h = L.ceres_scene_create(fp(tri), n, fp(nor), nodes.ctypes.data_as(ctypes.c_void_p), 3,
+                             prim.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 0, 0)
+    assert not h
+    assert b"BVH4" in L.ceres_last_error()
