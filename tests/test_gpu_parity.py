@@ -292,6 +292,32 @@ def test_batch_of_64_frames_matches_single_frames(gpu):
             assert torch.equal(rgb[f], one), f"frame {f}, tiling {til}"
 
 
+def test_large_frame_batch_matches_single_frames(gpu):
+    """Frames of >= 4 Mpixel are dealt frame after frame in a batch (CERES_FRAME_MAJOR_PIXELS)
+    instead of interleaved: every frame's PPM body == a one-frame render, whole frames and one
+    rank of a 3-way row split."""
+    import torch
+    pkg = gpu
+    name = "dragon_640"
+    cfg = configs.CONFIGS[name]
+    W, H = 2048, 2048
+    scene, _, _, _ = scene_for(pkg, name)
+    cam0 = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    b12, s3 = pkg.orbit_cameras(cam0, cfg["sun"], W, H, 3, axis=configs.BENCH_ORBIT[0], step_deg=20.0,
+                                rotate_first=False)
+    st = torch.cuda.current_stream().cuda_stream
+    for til in (pkg.Tiling(H, 0, 1), pkg.Tiling(8, 1, 3)):
+        rows = pkg.local_rows(H, til)
+        rgb = torch.zeros((3, rows, 3 * W), dtype=torch.uint8, device="cuda")
+        scene.render_batch_device(b12, s3, W, H, tiling=til, d_rgb8=rgb.data_ptr(), stream=st)
+        one = torch.zeros((rows, 3 * W), dtype=torch.uint8, device="cuda")
+        for f in range(3):
+            scene.render_device(b12[f], s3[f], W, H, tiling=til, d_rgb8=one.data_ptr(), stream=st)
+            torch.cuda.synchronize()
+            assert torch.equal(rgb[f], one), f"frame {f}, tiling {til}"
+        assert int(rgb.max()) > 0
+
+
 def test_batch_rejects_bad_frame_counts(gpu):
     pkg = gpu
     scene, _, _, _ = scene_for(pkg, "tri1")

@@ -8,6 +8,6 @@ for c in ${CONFIGS:-dragon_1080 bunny_1080}; do
   timeout -k 10 300 python tools/ab.py $c ${ROUNDS:-20} $L > gpurun_out/abs_$c.log 2>&1 || { tail -5 gpurun_out/abs_$c.log; exit 3; }
   summ gpurun_out/abs_$c.log solo
   fi
-  AB_STREAMS=8 AB_BATCH=8 AB_FRAMES=64 timeout -k 10 300 python tools/ab.py $c ${ROUNDS:-8} $L > gpurun_out/ab_$c.log 2>&1 || { tail -5 gpurun_out/ab_$c.log; exit 3; }
-  summ gpurun_out/ab_$c.log batch8x8
+  AB_STREAMS=8 AB_BATCH=${BATCH:-8} AB_FRAMES=${NFRAMES:-64} timeout -k 10 300 python tools/ab.py $c ${ROUNDS:-8} $L > gpurun_out/ab_$c.log 2>&1 || { tail -5 gpurun_out/ab_$c.log; exit 3; }
+  summ gpurun_out/ab_$c.log batch${BATCH:-8}x8
 done
