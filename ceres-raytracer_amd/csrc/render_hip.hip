@@ -1522,7 +1522,8 @@ int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
 }
 
 // Centre-first order of a batch's tile x tile tiles for the fused kernel: ascending distance of the
-// tile centre (global pixel coordinates) from the image centre, frames interleaved.  Cached
+// tile centre (global pixel coordinates) from the image centre, frames interleaved (views of
+// CERES_FRAME_MAJOR_PIXELS and more: frame after frame).  Cached
 // on the scene per (W, H, tiling, frames, tile, cluster) -- up to kMaxTileOrders orders; the
 // least recently used one is retired (freed later, see ceres_scene::retired), so eviction
 // neither rewrites an order a launch in flight reads nor stalls the streams.
