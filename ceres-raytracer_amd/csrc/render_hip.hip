@@ -1265,14 +1265,25 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     // this wavefront's tile-order entries, read once through the scalar cache (a vector load of a
     // uniform address would put a full vector-memory round trip in front of every tile; the order
     // buffer is padded to a multiple of 4 entries)
-    static_assert(kTPW == 1 || kTPW == 4, "CERES_TILES_PER_WAVE must be 1 or 4");
-    uint4 tiles4;
-    if constexpr (kTPW == 4) tiles4 = sload_u4(P.tile_order + 4 * size_t(blockIdx.x), 0);
-    else tiles4.x = sload_u32(P.tile_order + blockIdx.x);
+    static_assert(kTPW == 1 || kTPW == 2 || kTPW == 4 || kTPW == 8, "CERES_TILES_PER_WAVE must be 1, 2, 4 or 8");
+    uint4 tiles4 = make_uint4(0, 0, 0, 0), tiles4b = make_uint4(0, 0, 0, 0);
+    if constexpr (kTPW == 8) {
+        tiles4 = sload_u4(P.tile_order + 8 * size_t(blockIdx.x), 0);
+        tiles4b = sload_u4(P.tile_order + 8 * size_t(blockIdx.x), 1);
+    } else if constexpr (kTPW == 4) {
+        tiles4 = sload_u4(P.tile_order + 4 * size_t(blockIdx.x), 0);
+    } else if constexpr (kTPW == 2) {
+        tiles4.x = sload_u32(P.tile_order + 2 * size_t(blockIdx.x));
+        tiles4.y = sload_u32(P.tile_order + 2 * size_t(blockIdx.x) + 1);
+    } else {
+        tiles4.x = sload_u32(P.tile_order + blockIdx.x);
+    }
     for (uint32_t q = 0; q < kTPW; ++q) {
     const uint32_t slot_q = blockIdx.x * kTPW + q;
     if (kTPW > 1 && slot_q >= n_tiles) break;
-    const uint32_t t = kTPW == 1 ? tiles4.x : q == 0 ? tiles4.x : q == 1 ? tiles4.y : q == 2 ? tiles4.z : tiles4.w;
+    const uint4 tq = q < 4 ? tiles4 : tiles4b;
+    const uint32_t qq = q & 3;
+    const uint32_t t = kTPW == 1 ? tiles4.x : qq == 0 ? tq.x : qq == 1 ? tq.y : qq == 2 ? tq.z : tq.w;
     const uint32_t f = t / per_frame;
     const uint32_t rem = t - f * per_frame;
     const uint32_t by = rem / P.tiles_x, bx = rem - by * P.tiles_x;
@@ -1502,9 +1513,9 @@ int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
         }
     }
     o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile; o.cluster = cluster;
-    // padded to a multiple of 4 entries (zeros): the fused kernel reads its tile-order entries
-    // four at a time through the scalar cache
-    const size_t padded = (n + 3) / 4 * 4;
+    // padded to a multiple of 8 entries (zeros): the fused kernel reads its tile-order entries
+    // up to eight at a time through the scalar cache
+    const size_t padded = (n + 7) / 8 * 8;
     if (!o.d) {
         HIP_TRY(hipMalloc(&o.d, padded * sizeof(uint32_t)));
         o.cap = padded;
