@@ -67,7 +67,7 @@
 #define CERES_DIAG_EXTRA_VALU 0               // diagnostic: N extra dependent VALU per primary step
 #endif
 #ifndef CERES_LANE_QUADS
-#define CERES_LANE_QUADS 0                    // fused kernel: quads of lanes are 2x2 pixel blocks (else 4x1)
+#define CERES_LANE_QUADS 1                    // fused kernel: lanes in Morton order over the 8x8 tile, quads = 2x2 blocks (else row-major, quads 4x1)
 #endif
 #ifndef CERES_SU_ROOT
 #define CERES_SU_ROOT 0                       // trace(): the root record through the scalar cache (A/B: -1..+2 %, noise)
