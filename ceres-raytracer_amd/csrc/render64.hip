@@ -38,6 +38,9 @@ namespace dev64 {
 #ifndef CERES64_WG
 #define CERES64_WG 64            // workgroup: 64 = one 8x8 tile (a long tile pins only its own LDS), 256 = 16x16
 #endif
+#ifndef CERES_LANE_QUADS64
+#define CERES_LANE_QUADS64 0     // lanes in Morton order over the 8x8 tile (else row-major)
+#endif
 constexpr int kBlock = CERES64_WG;
 constexpr uint32_t kTile = kBlock == 256 ? 16u : 8u;
 
@@ -220,8 +223,14 @@ __global__ __launch_bounds__(kBlock) void ceres_render64(const KParams64 P) {
     uint32_t* stk = lds + tid;
     const uint32_t t = __builtin_amdgcn_readfirstlane(P.tile_order[blockIdx.x]);
     const uint32_t tby = t / P.tiles_x, tbx = t - tby * P.tiles_x;
-    const uint32_t i = tbx * kTile + (kBlock == 256 ? (wave & 1u) * 8u : 0u) + (lane & 7u);
-    const uint32_t j = tby * kTile + (kBlock == 256 ? (wave >> 1) * 8u : 0u) + (lane >> 3);
+#if CERES_LANE_QUADS64
+    // lanes in Morton order over the wavefront's 8x8 tile (quads = 2x2 pixel blocks)
+    const uint32_t lx = (lane & 1u) | ((lane >> 1) & 2u) | ((lane >> 2) & 4u), ly = ((lane >> 1) & 1u) | ((lane >> 2) & 2u) | ((lane >> 3) & 4u);
+#else
+    const uint32_t lx = lane & 7u, ly = lane >> 3;
+#endif
+    const uint32_t i = tbx * kTile + (kBlock == 256 ? (wave & 1u) * 8u : 0u) + lx;
+    const uint32_t j = tby * kTile + (kBlock == 256 ? (wave >> 1) * 8u : 0u) + ly;
     const bool valid = i < P.W && j < P.H;
     bool overflow = false;
     uint32_t n_hit = 0, n_shadow = 0, n_occ = 0;

@@ -66,6 +66,9 @@
 #ifndef CERES_DIAG_EXTRA_VALU
 #define CERES_DIAG_EXTRA_VALU 0               // diagnostic: N extra dependent VALU per primary step
 #endif
+#ifndef CERES_PRIMARY_LANE_QUADS
+#define CERES_PRIMARY_LANE_QUADS 0            // primary kernel: Morton lane order as the fused kernel (measured slower on C2)
+#endif
 #ifndef CERES_LANE_QUADS
 #define CERES_LANE_QUADS 1                    // fused kernel: lanes in Morton order over the 8x8 tile, quads = 2x2 blocks (else row-major, quads 4x1)
 #endif
@@ -807,8 +810,14 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     uint32_t* stk = lds + tid;                                       // [entries][kBlock]
     const uint32_t f = blockIdx.y / P.row_blocks_per_frame;          // workgroup-uniform frame
     const uint32_t by = blockIdx.y - f * P.row_blocks_per_frame;
-    const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const uint32_t lr = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+#if CERES_PRIMARY_LANE_QUADS
+    // lanes in Morton order over the wavefront's 8x8 tile (as the fused kernel)
+    const uint32_t lx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4), ly = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
+#else
+    const uint32_t lx = lane & 7, ly = lane >> 3;
+#endif
+    const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + lx;
+    const uint32_t lr = by * 16 + (wave >> 1) * 8 + ly;
     const bool active = i < P.W && lr < P.local_rows;
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;          // batch pixel (< 2^32, host-checked)
     bool hit = false, job = false;
