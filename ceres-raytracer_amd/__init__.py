@@ -425,14 +425,16 @@ class Scene:
         _check(lib().ceres_scene_set_timing(self._h, 1 if on else 0))
 
     def wave_log(self, max_waves=1 << 16):
-        """Diagnostic per-wavefront records of the last shadow launch (stats scenes): begin/end
-        wall clock, longest node-pair chain, stamped iterations, box/leaf/next clocks, pairs."""
+        """Diagnostic per-wavefront records of the last full-mode render (stats scenes), one row per
+        8x8 tile: start / after primary / end (100-MHz ticks), longest primary chain, shadow-loop
+        trips, primary hits, primary and shadow node pairs of the wavefront."""
         out = np.zeros(8 * max_waves, np.uint64)
         n = _sz()
         _check(lib().ceres_scene_wave_log(self._h, _p(out, ctypes.c_uint64), max_waves, ctypes.byref(n)))
         return out[: 8 * n.value].reshape(-1, 8)
 
     def read_timing(self):
+        """(kernel ms summed over the renders since set_timing, 0.0, renders)."""
         p, q, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
         _check(lib().ceres_scene_read_timing(self._h, ctypes.byref(p), ctypes.byref(q), ctypes.byref(n)))
         return p.value, q.value, n.value

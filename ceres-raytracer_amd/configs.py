@@ -60,6 +60,10 @@ CONFIGS = {
     "tri1": _cfg(_TINY, obj="@golden/tri1.obj", W=64, H=48),
     "quad": _cfg(_TINY, obj="@golden/quad.obj", W=64, H=48),
     "degenerate": _cfg(_TINY, obj="@golden/degenerate.obj", W=64, H=48),
+    # leaves of 40 and 130 triangles (coincident copies: BinnedSahBuilder cannot split them,
+    # binned_sah_builder.hpp:199-232) casting shadows on a floor; the shadow BVH4 stores them as
+    # piece nodes (build_shadow_bvh4)
+    "dupleaf": _cfg(_TINY, obj="@golden/dupleaf.obj", W=96, H=64, sun=(-30.0, -15.0, -20.0)),
     # anim.cpp:76-88 orbit poses: the C3 camera + sun after `count` Transform rotations of
     # step_deg about the axis (the bench's weak-scaling frames are this orbit about z)
     "dragon_orbit3_333x217": _cfg(_DRAGON, W=333, H=217, orbit=((0.0, 0.0, 1.0), 45.0, 3)),

@@ -78,26 +78,14 @@ __host__ __device__
 #endif
 inline uint32_t node4_child(uint32_t count, uint32_t first) { return first << kNode4CountBits | count; }
 
-struct ShadowJob {             // one queued shadow ray (render.hpp:127-136), 32 B
-    uint32_t pixel;            // batch pixel index = (frame * local_rows + local_row) * W + i
-    uint32_t slot;             // leaf slot of the primary hit
-    float u, v;                // barycentrics of the primary hit (reference convention)
-    float px, py, pz;          // offset hit point = shadow ray origin
-    uint32_t pad;
-};
-static_assert(sizeof(ShadowJob) == 32, "ShadowJob");
-
-constexpr int kShards = 32;    // shadow-queue / counter shards (one 128-B line each)
+constexpr int kShards = 32;    // counter shards (one 128-B line each), wavefront w adds to shard w % 32
 struct alignas(128) Shard {
-    uint32_t queued;           // shadow rays traced (twopass: jobs appended to this shard)
+    uint32_t queued;           // shadow rays traced
     uint32_t error;            // traversal stack overflow flag
     unsigned long long hits;   // primary hits + occluded shadow rays
     unsigned long long pairs;  // node-pair visits (stats variant)
     unsigned long long tests;  // triangle tests (stats variant)
-    unsigned long long primary;
-    uint32_t taken;            // persistent shadow kernel: jobs of this shard claimed so far
-    uint32_t reserved;
-    uint32_t pad[20];
+    uint32_t pad[24];
 };
 static_assert(sizeof(Shard) == 128, "Shard");
 
@@ -114,8 +102,7 @@ struct KParams {
     uint32_t row_blocks_per_frame;               // 16-row blocks of local rows per frame (primary grid.y)
     uint32_t stack_entries;
     uint32_t root_leaf_count, root_leaf_first;   // root is a leaf (single_ray_traverser.hpp:72-73)
-    uint32_t shard_capacity;                     // jobs per shard
-    uint32_t shadow_stack_entries;               // BVH4 traversal stack (shadow kernel)
+    uint32_t shadow_stack_entries;               // BVH4 traversal stack (shadow rays)
     uint32_t tiles_x;                            // tile columns per row (fused kernel)
     uint32_t lds_entries;                        // fused kernel: LDS stack slots per lane (24-bit planes)
     const uint32_t* tile_order;                  // fused kernel: block -> batch tile (centre first)
@@ -126,13 +113,12 @@ struct KParams {
     const float* norms;
     float* pixels;             // [frames][local_rows][W][3] floats, row 0 = bottom (render.hpp:107)
     uint8_t* rgb8;             // [frames][local_rows][W][3] PPM body rows, top row first
-    ShadowJob* jobs;
     Shard* shards;
     // optional per-pixel hit records (G-buffer / parity output), batch pixel order
     int32_t* rec_prim;         // original triangle index, -1 on a primary miss
     float* rec_tuv;            // t, u, v of the primary hit
     int8_t* rec_shadow;        // -1 no shadow ray, 0 lit, 1 occluded
-    // diagnostic (stats scenes only): 8 x u64 per wavefront of the shadow kernel
+    // diagnostic (stats scenes only): 8 x u64 per wavefront of the fused kernel
     unsigned long long* wave_log;
 };
 static_assert(sizeof(KParams) <= 4096, "KParams must fit the 4 KB kernel-argument limit");

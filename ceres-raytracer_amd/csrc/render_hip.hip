@@ -6,14 +6,12 @@
 // the offset shadow ray (render.hpp:119-138) and smooth Blinn-Phong shading (render.hpp:46-84),
 // plus the PPM quantiser of static.cpp:135-147.
 //
-// Full mode (default): ONE kernel per batch of frames, ceres_fused (DESIGN.md "Kernels"): one
-// 64-thread workgroup per 8x8 pixel tile (coherent primary rays), tiles walked centre-first;
-// closest-hit BVH2 traversal per pixel (software-pipelined: the next record is loaded before
-// the step's triangle tests), then the tile's shadow rays with intra-wavefront work stealing
-// over an exact BVH4 collapse (any-hit: only the boolean matters, render.hpp:139), then
-// shading of the lit pixels.  Kept for A/B and the primary-only mode: ceres_primary (hits
-// COMPACTED into a sharded shadow-ray queue with a wavefront __ballot + popcount prefix) and
-// ceres_shadow / ceres_shadow_steal over that queue.
+// Full mode: ONE kernel per batch of frames, ceres_fused (DESIGN.md "Kernels"): one 64-thread
+// workgroup per 8x8 pixel tile (coherent primary rays), tiles walked centre-first; closest-hit
+// BVH2 traversal per pixel (software-pipelined: the next record is loaded before the step's
+// triangle tests), then the tile's shadow rays over an exact BVH4 collapse (any-hit: only the
+// boolean matters, render.hpp:139; one-frame launches share the rays' work among the lanes),
+// then shading of the lit pixels.  Primary-only mode (C2): ceres_primary.
 // A batch is 1..kMaxFrames frames (own camera + sun each, e.g. the anim.cpp:93-110 orbit),
 // each restricted to this rank's rows (ceres_tiling).
 // Traversal stacks live in LDS ([entries][lanes], lane-contiguous = bank-conflict free),
@@ -42,62 +40,11 @@
 
 #pragma clang fp contract(off)
 
-#ifndef CERES_STEP_SELECT
-#define CERES_STEP_SELECT 1   // select-based next-node step in trace() (0: the branchy A/B baseline)
-#endif
-#ifndef CERES_PREFETCH_NEXT
-#define CERES_PREFETCH_NEXT 1 // trace(): issue the next record's load before the step's triangle tests
-#endif
-#ifndef CERES_SCALAR_UNIFORM
-#define CERES_SCALAR_UNIFORM 1 // wave-uniform record fetches through the scalar cache (see uniform_id)
-#endif
 #ifndef CERES_TILES_PER_WAVE
-#define CERES_TILES_PER_WAVE 4                // fused kernel, batches: consecutive tile-order entries (1 or 4) per
-#endif                                        // wavefront (A/B, 8-frame batches x 8 streams: 2 -1..-3 %, 4 -3..-4 %)
-#ifndef CERES_TILE_CLUSTER
-#define CERES_TILE_CLUSTER 0                  // batches: each wavefront's tiles form a 2x2 cluster (A/B: +3..5 %, not kept)
-#endif
-#ifndef CERES_FOOTPRINT_PAD
-#define CERES_FOOTPRINT_PAD 0                 // diagnostic: pad the pair records to 2x their footprint
-#endif
-#ifndef CERES_DIAG_EXTRA_LOAD
-#define CERES_DIAG_EXTRA_LOAD 0               // diagnostic: an extra vector load per primary step
-#endif
-#ifndef CERES_DIAG_EXTRA_VALU
-#define CERES_DIAG_EXTRA_VALU 0               // diagnostic: N extra dependent VALU per primary step
-#endif
-#ifndef CERES_PRIMARY_LANE_QUADS
-#define CERES_PRIMARY_LANE_QUADS 0            // primary kernel: Morton lane order as the fused kernel (measured slower on C2)
-#endif
-#ifndef CERES_LANE_QUADS
-#define CERES_LANE_QUADS 1                    // fused kernel: lanes in Morton order over the 8x8 tile, quads = 2x2 blocks (else row-major, quads 4x1)
-#endif
-#ifndef CERES_SU_ROOT
-#define CERES_SU_ROOT 0                       // trace(): the root record through the scalar cache (A/B: -1..+2 %, noise)
-#endif
-#ifndef CERES_TRI_FIRST
-#define CERES_TRI_FIRST 0                     // trace(): first leaf triangle fetched before the next record (+12 VGPRs: spills, 2x slower)
-#endif
-#ifndef CERES_NT_STORE
-#define CERES_NT_STORE 0                      // non-temporal framebuffer stores
-#endif
-#ifndef CERES_FUSED_SHADOW_BVH2
-#define CERES_FUSED_SHADOW_BVH2 0             // batch shadow rays over the BVH2 (trace<true>) instead of the BVH4
-#endif
+#define CERES_TILES_PER_WAVE 4                // fused kernel, batches: consecutive tile-order entries (1, 2, 4 or 8) per
+#endif                                        // wavefront (A/B, 16-frame batches x 8 streams: 4 beats 2 by 2 %, 8 = 4)
 #ifndef CERES_FRAME_MAJOR_PIXELS
 #define CERES_FRAME_MAJOR_PIXELS (1u << 22)    // batches of frames of >= this many pixels: frame after frame (0: never)
-#endif
-#ifndef CERES_SU_PAIR
-#define CERES_SU_PAIR 0                       // ... of primary BVH2 sibling pairs (A/B: C3 -0.6 %, bunny +6 %)
-#endif
-#ifndef CERES_SU_TRI
-#define CERES_SU_TRI CERES_SCALAR_UNIFORM     // ... of leaf triangles
-#endif
-#ifndef CERES_SU_TRI2
-#define CERES_SU_TRI2 0                       // ... and of leaf triangles two distinct ones among the lanes
-#endif
-#ifndef CERES_SU_NODE4
-#define CERES_SU_NODE4 CERES_SCALAR_UNIFORM   // ... of shadow BVH4 nodes
 #endif
 
 namespace ceres {
@@ -160,21 +107,8 @@ __device__ __forceinline__ TriV load_tri_s(const Tri48* t) {
 }
 // triangle `idx` for the active lanes: one scalar fetch when they all test the same triangle
 __device__ __forceinline__ TriV load_tri_u(const Tri48* tris, uint32_t idx) {
-#if CERES_SU_TRI
     uint32_t r;
     if (uniform_id(idx, r)) return load_tri_s(tris + r);
-#if CERES_SU_TRI2
-    // two distinct triangles among the active lanes: two scalar fetches and a per-lane select
-    const unsigned long long rest = __ballot(idx != r);
-    const uint32_t r1 = __builtin_amdgcn_readlane(idx, __builtin_ctzll(rest));
-    if (__ballot(idx != r && idx != r1) == 0) {
-        const TriV a = load_tri_s(tris + r), b = load_tri_s(tris + r1);
-        const bool first = idx == r;
-        auto sel = [first](F3 x, F3 y) { return F3{first ? x.x : y.x, first ? x.y : y.y, first ? x.z : y.z}; };
-        return {sel(a.p0, b.p0), sel(a.e1, b.e1), sel(a.e2, b.e2), sel(a.n, b.n)};
-    }
-#endif
-#endif
     return load_tri(tris + idx);
 }
 
@@ -185,14 +119,10 @@ __device__ __forceinline__ TriV load_tri_u(const Tri48* tris, uint32_t idx) {
 // tests/test_gpu_parity.py::test_fast_reciprocal_is_exact).  Zero, denormal, huge, inf and NaN
 // inputs take the full v_div_scale/fmas/fixup division.
 __device__ __forceinline__ float rcp_exact(float x) {
-#ifdef CERES_SLOW_RCP
-    return 1.0f / x;
-#else
     const uint32_t m = __float_as_uint(x) & 0x7fffffffu;
     if (__builtin_expect(m - 0x00800000u >= 0x7e000000u - 0x00800000u, 0)) return 1.0f / x;
     const float r0 = __builtin_amdgcn_rcpf(x);
     return __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
-#endif
 }
 
 // 24-bit LDS stack entries for scenes whose node indices need more than 16 bits but fewer
@@ -208,64 +138,6 @@ struct Stk24 {
     };
     __device__ __forceinline__ Ref operator[](uint32_t i) const { return {lo + i, hi + i}; }
 };
-
-// Diagnostic build only (make variant DEFS=-DCERES_DIAG_UNIFORM=1, tools/diag_uniform.py): per
-// wave-step of a loop, how many distinct records the wave's active lanes fetch.  g_diag[base..+3]
-// += steps, steps with one record for all active lanes, distinct records, active lanes.
-#ifndef CERES_DIAG_UNIFORM
-#define CERES_DIAG_UNIFORM 0
-#endif
-#if CERES_DIAG_UNIFORM
-__device__ unsigned long long g_diag[34];
-__device__ const uint32_t* g_diag_parent;     // pair index -> pair index of its parent (host-built)
-__device__ __forceinline__ uint32_t count_distinct(uint32_t id) {
-    uint32_t distinct = 0;
-    unsigned long long rest = __ballot(1);
-    while (rest) {
-        const uint32_t f = __builtin_amdgcn_readlane(id, __builtin_ctzll(rest));
-        rest &= ~__ballot(id == f);
-        ++distinct;
-    }
-    return distinct;
-}
-__device__ __forceinline__ void diag_step(uint32_t id, int base) {
-    const unsigned long long m = __ballot(1);
-    const uint32_t distinct = count_distinct(id);
-    if (base == 0) {
-        // primary BVH2 records: distinct 128-B lines now (two 64-B records per line, DFS order)
-        // and with sibling records paired in one line (distinct parents)
-        const uint32_t lines = count_distinct(id >> 1);
-        const uint32_t parents = count_distinct(id == 0 ? 0xffffffffu : g_diag_parent[id]);
-        if (__lane_id() == uint32_t(__builtin_ctzll(m))) {
-            atomicAdd(&g_diag[32], (unsigned long long)lines);
-            atomicAdd(&g_diag[33], (unsigned long long)parents);
-        }
-    }
-    // quads of lanes (4k..4k+3): active quads, quads whose active lanes share one record, and
-    // wave-steps where every active quad does (g_diag[16 + base / 4 * 4 ..])
-    const uint32_t q0 = __shfl(id, __lane_id() & ~3u, 64), q1 = __shfl(id, (__lane_id() & ~3u) + 1, 64);
-    const uint32_t q2 = __shfl(id, (__lane_id() & ~3u) + 2, 64), q3 = __shfl(id, (__lane_id() & ~3u) + 3, 64);
-    const unsigned long long qa = m >> (__lane_id() & ~3u) & 0xfull;
-    const bool quni = (!(qa & 1) || q0 == id) && (!(qa & 2) || q1 == id) && (!(qa & 4) || q2 == id) && (!(qa & 8) || q3 == id);
-    const unsigned long long qbad = __ballot(!quni);
-    uint32_t nq = 0, nqu = 0;
-    for (int k = 0; k < 16; ++k) {
-        if (m >> (4 * k) & 0xfull) { ++nq; if (!(qbad >> (4 * k) & 0xfull)) ++nqu; }
-    }
-    if (__lane_id() == uint32_t(__builtin_ctzll(m))) {
-        atomicAdd(&g_diag[16 + base], (unsigned long long)nq);
-        atomicAdd(&g_diag[16 + base + 1], (unsigned long long)nqu);
-        atomicAdd(&g_diag[16 + base + 2], qbad == 0 ? 1ull : 0ull);
-        atomicAdd(&g_diag[base], 1ull);
-        atomicAdd(&g_diag[base + 1], distinct == 1 ? 1ull : 0ull);
-        atomicAdd(&g_diag[base + 2], (unsigned long long)distinct);
-        atomicAdd(&g_diag[base + 3], (unsigned long long)__popcll(m));
-    }
-}
-#define CERES_DIAG(id, base) diag_step((id), (base))
-#else
-#define CERES_DIAG(id, base) ((void)0)
-#endif
 
 // Per-ray hit; closest hit keeps the LAST accepted hit with t <= tmax (intersect_leaf :54-60).
 struct Hit { uint32_t slot; float t, u, v; };
@@ -338,16 +210,6 @@ __device__ __forceinline__ void slab_box(const Slab<kRobust>& s, float lox, floa
     }
 }
 
-// Diagnostic section clocks (stats builds only): wave-uniform s_memtime sums per trace().
-struct Stamps { unsigned long long box = 0, leaf = 0, next = 0, iters = 0; };
-__device__ __forceinline__ unsigned long long stamp() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-
 // Eager BVH2 traversal, single_ray_traverser.hpp:68-126 with FastNodeIntersector
 // (node_intersectors.hpp:35-47,83-103).  Exactly the reference's visiting order: both
 // children's slab tests use the tmax from before this step's leaves; left leaf triangles,
@@ -363,7 +225,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 // slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
 template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false>
 __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hit& best,
-                                      uint32_t& n_pairs, uint32_t& n_tests, bool& overflow, Stamps* ss = nullptr) {
+                                      uint32_t& n_pairs, uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f;
     float tmax = FLT_MAX;                                           // ray.hpp:17-21
     bool have = false;
@@ -381,234 +243,55 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     }
     const Slab<kRobust> sl = make_slab<kRobust>(o, d);
     uint32_t sp = 0;
-#if CERES_DIAG_EXTRA_LOAD || CERES_DIAG_EXTRA_VALU
-    float diag_sink = 0.f;
-    struct SinkGuard {                                // keeps the diagnostic work alive
-        float& v; const KParams& P;
-        __device__ ~SinkGuard() { if (P.frames == 0xffffffffu) P.pixels[0] = v; }
-    } guard{diag_sink, P};
-#endif
-#if CERES_PREFETCH_NEXT
-    if (!(kStats && ss)) {
-        // Same steps, software-pipelined: the next record (near child or stack top) follows from
-        // this step's box tests alone (the leaf hits only lower tmax for LATER steps, :89-121),
-        // so its load is issued before this step's triangle tests and overlaps them.
-#if CERES_SU_PAIR
-        // Two copies of the step: one on a record the whole wavefront shares, read through the
-        // scalar cache into SGPRs (sA..sL, used by the box tests as scalar operands -- no TA/TD
-        // traffic, no copies), one on a per-lane record in VGPRs (vA..vL).  The next step's
-        // record is fetched the same way, chosen by whether every live lane continues with it.
-        float4 sA, sB, sC, vA, vB, vC;
-        uint4 sL, vL;
-        {
-            const SiblingPair* q0 = P.pairs;                                 // root's children (:81)
-            sA = sload_f4(q0, 0); sB = sload_f4(q0, 1); sC = sload_f4(q0, 2); sL = sload_u4(q0, 3);
-        }
-        bool uni = true;
-        while (true) {                                                // :82-123
-            if (kStats) ++n_pairs;
-            const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];
-            float le, lx, re, rx;
-            uint4 L;
-            // (the empty asm markers keep the compiler from merging the two copies into one
-            // with per-operand selects, which would cost 32 VALU per step)
-            if (uni) {                                                // SGPR operands
-                slab_box<kRobust>(sl, sA.x, sA.y, sA.z, sA.w, sB.x, sB.y, tmin, tmax, le, lx);
-                slab_box<kRobust>(sl, sB.z, sB.w, sC.x, sC.y, sC.z, sC.w, tmin, tmax, re, rx);
-                L = sL;
-                asm volatile("; uniform pair" ::);
-            } else {
-                slab_box<kRobust>(sl, vA.x, vA.y, vA.z, vA.w, vB.x, vB.y, tmin, tmax, le, lx);
-                slab_box<kRobust>(sl, vB.z, vB.w, vC.x, vC.y, vC.z, vC.w, tmin, tmax, re, rx);
-                L = vL;
-                asm volatile("; per-lane pair" ::);
-            }
-#else
-#if CERES_SU_ROOT
-        // the root's children (:81): the same record for every ray, read through the scalar
-        // cache (its latency is exposed: nothing else is in flight yet)
-        float4 A = sload_f4(P.pairs, 0), B = sload_f4(P.pairs, 1), C = sload_f4(P.pairs, 2);
-        uint4 L = sload_u4(P.pairs, 3);
-#else
-        const float4* q = reinterpret_cast<const float4*>(P.pairs);  // pair of the root's children (:81)
-        float4 A = q[0], B = q[1], C = q[2];
-        uint4 L = reinterpret_cast<const uint4*>(q)[3];
-#endif
-        uint32_t rec = 0;
-        (void)rec;
-        while (true) {                                                // :82-123
-            if (kStats) ++n_pairs;
-            if (!kAnyHit) CERES_DIAG(rec, 0);
-            const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];
-            float le, lx, re, rx;
-            slab_box<kRobust>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
-            slab_box<kRobust>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
-#endif
-            const bool hit_l = le <= lx, hit_r = re <= rx;
-            const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
-            const bool both = go_l && go_r, none = !go_l && !go_r;
-            const bool swap = le > re;                                // near first, ties left (:109-115)
-            overflow |= both && sp >= P.stack_entries;
-            stk[(sp < P.stack_entries ? sp : P.stack_entries) * kS] = swap ? L.y : L.w;
-            const bool done = none && sp == 0;                        // :118-121
-            const uint32_t near = both ? (swap ? L.w : L.y) : (go_l ? L.y : L.w);   // :115-117
-            const uint32_t nxt = none ? top : near;
-            sp = both ? (sp < P.stack_entries ? sp + 1 : sp) : (none ? (sp ? sp - 1 : 0) : sp);
-            uint32_t k = 0, k_end = 0, k2 = 0, k2_end = 0;
-            if (hit_l && L.x) { k = L.y; k_end = L.y + L.x; }
-            if (hit_r && L.z) { k2 = L.w; k2_end = L.w + L.z; }
-            if (kStats) n_tests += (k_end - k) + (k2_end - k2);
-#if CERES_SU_PAIR
-            bool un = false;
-            const unsigned long long live = __ballot(!done);
-            if (live) {
-                const uint32_t rn = __builtin_amdgcn_readlane(nxt, __builtin_ctzll(live));
-                un = __ballot(!done && nxt != rn) == 0;
-                if (un) {
-                    const SiblingPair* nq = P.pairs + rn;
-                    sA = sload_f4(nq, 0); sB = sload_f4(nq, 1); sC = sload_f4(nq, 2); sL = sload_u4(nq, 3);
-                }
-            }
-            if (!un && !done) {
-                const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
-                vA = nq[0]; vB = nq[1]; vC = nq[2]; vL = reinterpret_cast<const uint4*>(nq)[3];
-            }
-            uni = un;
-#else
-#if CERES_TRI_FIRST
-            // The first leaf triangle's fetch goes out before the next record's: vmcnt retires in
-            // issue order, so the first test then waits for its triangle only, not for the
-            // prefetch as well.
-            const bool any_leaf = k < k_end || k2 < k2_end;
-            TriV tr0;
-            uint32_t idx0 = 0;
-            if (any_leaf) {
-                idx0 = k < k_end ? k++ : k2++;
-                tr0 = load_tri_u(P.tris, idx0);
-            }
-#endif
-            float4 nA, nB, nC;                                        // undefined for done lanes
-            uint4 nL;
-#if CERES_DIAG_EXTRA_LOAD >= 2
-            float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
-            if (!done) {
-                const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
-                nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
-#if CERES_DIAG_EXTRA_LOAD
-                // diagnostic A/B: one more dwordx4 per step (TA/TD sensitivity)
-#if CERES_DIAG_EXTRA_LOAD == 1                                  // 4 x dword
-                const volatile float* xq = reinterpret_cast<const volatile float*>(nq + 1 + (nxt & 1));
-                diag_sink += xq[0] + xq[1] + xq[2] + xq[3];
-#elif CERES_DIAG_EXTRA_LOAD == 2                                // 1 x dwordx4, consumed after the leaves
-                xv = reinterpret_cast<const float4*>(P.tris + nxt)[0];   // nxt < n_pairs < n_tri
-#else                                                             // the same by a quarter of the lanes
-                if ((__lane_id() & 3) == 0) xv = reinterpret_cast<const float4*>(P.tris + nxt)[0];
-#endif
-#endif
-            }
-#endif
-#if CERES_DIAG_EXTRA_VALU
-            // diagnostic A/B: a chain of dependent VALU per step (issue sensitivity)
-#pragma unroll
-            for (int z = 0; z < CERES_DIAG_EXTRA_VALU; ++z) diag_sink = __builtin_fmaf(diag_sink, 0.999f, le);
-#endif
-#if CERES_TRI_FIRST
-            if (any_leaf) {
-                if (!kAnyHit) CERES_DIAG(idx0, 4);
-                float t, u, v;
-                if (tri_test(tr0, o, d, tmin, tmax, t, u, v)) {
-                    best = {idx0, t, u, v}; have = true;
-                    if (kAnyHit) return true;
-                    tmax = t;
-                }
-            }
-#endif
-            while (k < k_end || k2 < k2_end) {
-                const uint32_t idx = k < k_end ? k++ : k2++;
-                if (!kAnyHit) CERES_DIAG(idx, 4);
-                float t, u, v;
-                if (tri_test(load_tri_u(P.tris, idx), o, d, tmin, tmax, t, u, v)) {
-                    best = {idx, t, u, v}; have = true;
-                    if (kAnyHit) return true;
-                    tmax = t;
-                }
-            }
-#if CERES_DIAG_EXTRA_LOAD >= 2
-            diag_sink += xv.x + xv.y + xv.z + xv.w;
-#endif
-            if (done) break;
-#if !CERES_SU_PAIR
-            A = nA; B = nB; C = nC; L = nL;
-            rec = nxt;
-#endif
-        }
-        return have;
-    }
-#endif
-    uint32_t cur = 0;                                                 // pair of the root's children (:81)
-    unsigned long long c0 = 0, c1 = 0, c2 = 0;
+    // Software-pipelined steps: the next record (near child or stack top) follows from this
+    // step's box tests alone (the leaf hits only lower tmax for LATER steps, :89-121), so its
+    // load is issued before this step's triangle tests and overlaps them.
+    const float4* q = reinterpret_cast<const float4*>(P.pairs);       // pair of the root's children (:81)
+    float4 A = q[0], B = q[1], C = q[2];
+    uint4 L = reinterpret_cast<const uint4*>(q)[3];
     while (true) {                                                    // :82-123
         if (kStats) ++n_pairs;
-
-        if (kStats && ss) c0 = stamp();
-        const float4* q = reinterpret_cast<const float4*>(P.pairs + cur);
-        const float4 A = q[0], B = q[1], C = q[2];
-        const uint4 L = reinterpret_cast<const uint4*>(q)[3];
-#if CERES_STEP_SELECT
-        const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];         // popped if this step descends nowhere
-#endif
+        const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];             // popped if this step descends nowhere
         // left bounds A.x A.y | A.z A.w | B.x B.y ; right bounds B.z B.w | C.x C.y | C.z C.w
         float le, lx, re, rx;
         slab_box<kRobust>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
         slab_box<kRobust>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
         const bool hit_l = le <= lx, hit_r = re <= rx;
-        if (kStats && ss) { volatile bool keep = hit_l | hit_r; (void)keep; c1 = stamp(); }
+        const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
+        // the three cases as selects: the far child is written to slot sp every step (a free slot
+        // unless this step pushes; the LDS stack has stack_entries + 1 slots), the stack top was
+        // read at the start of the step, only the exit branches
+        const bool both = go_l && go_r, none = !go_l && !go_r;
+        const bool swap = le > re;                                    // near first, ties left (:109-115)
+        overflow |= both && sp >= P.stack_entries;
+        stk[(sp < P.stack_entries ? sp : P.stack_entries) * kS] = swap ? L.y : L.w;
+        const bool done = none && sp == 0;                            // :118-121
+        const uint32_t near = both ? (swap ? L.w : L.y) : (go_l ? L.y : L.w);   // :115-117
+        const uint32_t nxt = none ? top : near;
+        sp = both ? (sp < P.stack_entries ? sp + 1 : sp) : (none ? (sp ? sp - 1 : 0) : sp);
         // leaves of this step, left then right (intersect_leaf on each, :89-107), one loop so a
         // wavefront runs max(left + right) trips rather than max(left) + max(right)
         uint32_t k = 0, k_end = 0, k2 = 0, k2_end = 0;
         if (hit_l && L.x) { k = L.y; k_end = L.y + L.x; }
         if (hit_r && L.z) { k2 = L.w; k2_end = L.w + L.z; }
         if (kStats) n_tests += (k_end - k) + (k2_end - k2);
+        float4 nA, nB, nC;                                            // undefined for done lanes
+        uint4 nL;
+        if (!done) {
+            const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
+            nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
+        }
         while (k < k_end || k2 < k2_end) {
             const uint32_t idx = k < k_end ? k++ : k2++;
             float t, u, v;
-            if (tri_test(load_tri(P.tris + idx), o, d, tmin, tmax, t, u, v)) {
+            if (tri_test(load_tri_u(P.tris, idx), o, d, tmin, tmax, t, u, v)) {
                 best = {idx, t, u, v}; have = true;
-                if (kAnyHit) { if (kStats && ss) { ss->box += c1 - c0; ss->iters++; } return true; }
+                if (kAnyHit) return true;
                 tmax = t;
             }
         }
-        if (kStats && ss) { c2 = stamp(); ss->box += c1 - c0; ss->leaf += c2 - c1; ss->iters++; }
-        const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
-#if CERES_STEP_SELECT
-        // the same three cases with selects: the far child is written to slot sp every step
-        // (a free slot unless this step pushes; the LDS stack has stack_entries + 1 slots), the
-        // stack top was read at the start of the step, only the exit branches
-        const bool both = go_l && go_r, none = !go_l && !go_r;
-        const bool swap = le > re;                                    // near first, ties left (:109-115)
-        overflow |= both && sp >= P.stack_entries;
-        stk[(sp < P.stack_entries ? sp : P.stack_entries) * kS] = swap ? L.y : L.w;
-        if (none && sp == 0) { if (kStats && ss) ss->next += stamp() - c2; break; }   // :118-121
-        const uint32_t near = both ? (swap ? L.w : L.y) : (go_l ? L.y : L.w);        // :115-117
-        cur = none ? top : near;
-        sp = both ? (sp < P.stack_entries ? sp + 1 : sp) : (none ? sp - 1 : sp);
-#else
-        if (go_l && go_r) {                                           // near first, ties left (:109-115)
-            const bool swap = le > re;
-            if (sp >= P.stack_entries) { overflow = true; return have; }
-            stk[sp * kS] = swap ? L.y : L.w;
-            ++sp;
-            cur = swap ? L.w : L.y;
-        } else if (go_l || go_r) {
-            cur = go_l ? L.y : L.w;                                   // :115-117
-        } else {
-            if (sp == 0) { if (kStats && ss) ss->next += stamp() - c2; break; }   // :118-121
-            --sp;
-            cur = stk[sp * kS];
-        }
-#endif
-        if (kStats && ss) ss->next += stamp() - c2;
+        if (done) break;
+        A = nA; B = nB; C = nC; L = nL;
     }
     return have;
 }
@@ -628,14 +311,12 @@ __device__ __forceinline__ uint32_t n4_count(uint32_t w) { return w & kNode4MaxC
 __device__ __forceinline__ uint32_t n4_first(uint32_t w) { return w >> kNode4CountBits; }
 // node `cur` for the active lanes: one scalar fetch when they all visit the same node
 __device__ __forceinline__ N4 load_n4_u(const Node4* nodes, uint32_t cur) {
-#if CERES_SU_NODE4
     uint32_t r;
     if (uniform_id(cur, r)) {
         const Node4* q = nodes + r;
         return {sload_f4(q, 0), sload_f4(q, 1), sload_f4(q, 2), sload_f4(q, 3), sload_f4(q, 4), sload_f4(q, 5),
                 sload_u4(q, 6)};
     }
-#endif
     return load_n4(nodes + cur);
 }
 __device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
@@ -653,18 +334,14 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
     uint32_t sp = 0, cur = 0;
     while (true) {
         if (kStats) ++n_pairs;
-        CERES_DIAG(cur, 8);
         float4 LX, HX, LY, HY, LZ, HZ;
         uint4 CH;
-#if CERES_SU_NODE4
         uint32_t rc;
         if (uniform_id(cur, rc)) {
             const Node4* q = P.nodes4 + rc;
             LX = sload_f4(q, 0); HX = sload_f4(q, 1); LY = sload_f4(q, 2); HY = sload_f4(q, 3);
             LZ = sload_f4(q, 4); HZ = sload_f4(q, 5); CH = sload_u4(q, 6);
-        } else
-#endif
-        {
+        } else {
             const float4* q = reinterpret_cast<const float4*>(P.nodes4 + cur);
             LX = q[0]; HX = q[1]; LY = q[2]; HY = q[3]; LZ = q[4]; HZ = q[5];
             CH = reinterpret_cast<const uint4*>(q)[6];
@@ -695,7 +372,6 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
                 k_end = k + (c == 0 ? cnt[0] : c == 1 ? cnt[1] : c == 2 ? cnt[2] : cnt[3]);
                 if (kStats) n_tests += k_end - k;
             }
-            CERES_DIAG(k, 12);
             float t, u, v;
             if (tri_test(load_tri_u(P.tris, k), o, d, tmin, tmax, t, u, v)) return true;
             ++k;
@@ -739,18 +415,6 @@ __device__ __forceinline__ uint8_t quantize(float x) {               // static.c
 __device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32_t lr, uint32_t i, float c0, float c1,
                                             float c2) {
     const size_t frame_base = size_t(f) * P.local_rows;
-#if CERES_NT_STORE
-    // A/B: streaming (non-temporal) framebuffer stores, so they do not evict the scene from L2
-    if (P.pixels) {
-        float* q = P.pixels + 3 * ((frame_base + lr) * P.W + i);
-        __builtin_nontemporal_store(c0, q); __builtin_nontemporal_store(c1, q + 1); __builtin_nontemporal_store(c2, q + 2);
-    }
-    if (P.rgb8) {
-        uint8_t* q = P.rgb8 + 3 * ((frame_base + (P.local_rows - 1 - lr)) * P.W + i);
-        __builtin_nontemporal_store(quantize(c0), q); __builtin_nontemporal_store(quantize(c1), q + 1);
-        __builtin_nontemporal_store(quantize(c2), q + 2);
-    }
-#else
     if (P.pixels) {
         float* q = P.pixels + 3 * ((frame_base + lr) * P.W + i);
         q[0] = c0; q[1] = c1; q[2] = c2;
@@ -759,7 +423,6 @@ __device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32
         uint8_t* q = P.rgb8 + 3 * ((frame_base + (P.local_rows - 1 - lr)) * P.W + i);
         q[0] = quantize(c0); q[1] = quantize(c1); q[2] = quantize(c2);
     }
-#endif
 }
 
 __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t lr) {
@@ -799,32 +462,27 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
     return x;
 }
 
-// ---------------------------------------------------------------- primary kernel
+// ---------------------------------------------------------------- primary-only kernel
+// The "primary rays only" mode (C2; pixel = |normalize(tri.n)|, render.hpp:123-125).
 // grid.x: 16-pixel column blocks; grid.y: frames x 16-row blocks of this rank's rows.  The
-// four wavefronts of a workgroup take the 2x2 8x8 tiles of its 16x16 pixels.  Every wavefront
-// is independent: no workgroup barrier, one queue atomic per wavefront.
-template <int kMode, bool kStats, bool kRobust>
+// four wavefronts of a workgroup take the 2x2 8x8 tiles of its 16x16 pixels (row-major lanes:
+// C2's rays are coherent already, the Morton lane order measured +2.5 % on solo frames here).
+template <bool kStats, bool kRobust>
 __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* stk = lds + tid;                                       // [entries][kBlock]
     const uint32_t f = blockIdx.y / P.row_blocks_per_frame;          // workgroup-uniform frame
     const uint32_t by = blockIdx.y - f * P.row_blocks_per_frame;
-#if CERES_PRIMARY_LANE_QUADS
-    // lanes in Morton order over the wavefront's 8x8 tile (as the fused kernel)
-    const uint32_t lx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4), ly = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
-#else
     const uint32_t lx = lane & 7, ly = lane >> 3;
-#endif
     const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + lx;
     const uint32_t lr = by * 16 + (wave >> 1) * 8 + ly;
     const bool active = i < P.W && lr < P.local_rows;
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;          // batch pixel (< 2^32, host-checked)
-    bool hit = false, job = false;
+    bool hit = false;
     Hit h{0, 0.f, 0.f, 0.f};
     uint32_t n_pairs = 0, n_tests = 0;
     bool overflow = false;
-    F3 shadow_o{0.f, 0.f, 0.f};
     if (active) {
         const F3 view = primary_dir(P, f, i, global_row(P, lr));
         hit = trace<false, kStats, kBlock, uint32_t*, kRobust>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
@@ -837,40 +495,15 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
         }
         if (!hit) {
             store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);                 // render.hpp:116-117
-        } else {
-            const TriV tr = load_tri(P.tris + h.slot);
-            const F3 normal = normalize(tr.n);
-            if (kMode == CERES_MODE_PRIMARY) {                       // render.hpp:123-125
-                store_pixel(P, f, lr, i, fabsf(normal.x), fabsf(normal.y), fabsf(normal.z));
-            } else {                                                 // render.hpp:127-133
-                const F3 p1 = tr.p0 - tr.e1, p2 = tr.p0 + tr.e2;
-                F3 p = tr.p0 * h.u + p1 * h.v + p2 * (1 - h.u - h.v);
-                const float scale = -0.00001;
-                p = p + normal * scale;
-                shadow_o = p;
-                job = true;
-            }
+        } else {                                                     // render.hpp:123-125
+            const F3 normal = normalize(load_tri(P.tris + h.slot).n);
+            store_pixel(P, f, lr, i, fabsf(normal.x), fabsf(normal.y), fabsf(normal.z));
         }
     }
-    // wave-level compaction of the shadow rays: ballot + popcount prefix, one atomic per wave
     const uint32_t wave_id = (blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave;
     const uint32_t shard = wave_id % kShards;
-    const unsigned long long jm = __ballot(job);
     const uint32_t nh = __popcll(__ballot(hit));
-    uint32_t base = 0;
-    if (lane == 0) {
-        if (jm) base = atomicAdd(&P.shards[shard].queued, uint32_t(__popcll(jm)));
-        if (nh) atomicAdd(&P.shards[shard].hits, (unsigned long long)nh);
-    }
-    if (jm) {
-        base = __shfl(base, 0, 64);
-        if (job) {
-            const uint32_t off = base + __popcll(jm & ((1ull << lane) - 1ull));
-            float4* q = reinterpret_cast<float4*>(P.jobs + size_t(shard) * P.shard_capacity + off);
-            q[0] = make_float4(__uint_as_float(px), __uint_as_float(h.slot), h.u, h.v);
-            q[1] = make_float4(shadow_o.x, shadow_o.y, shadow_o.z, 0.f);
-        }
-    }
+    if (lane == 0 && nh) atomicAdd(&P.shards[shard].hits, (unsigned long long)nh);
     if (kStats) {
         const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
         if (lane == 0) {
@@ -893,125 +526,19 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 #ifndef CERES_STACK24
 #define CERES_STACK24 1          // 24-bit LDS stack entries for scenes with < 2^24 pairs and BVH4 nodes
 #endif
-#ifndef CERES_TILE_XCD_WEDGE
-#define CERES_TILE_XCD_WEDGE 0   // XCD group w renders angular wedge w of every frame (L2 locality)
-#endif
-#ifndef CERES_TILE_SHUFFLE_WINDOW
-#define CERES_TILE_SHUFFLE_WINDOW 64   // tiles per shuffled window of the centre-first order
-#endif
-#ifndef CERES_TILE_XCD_MIX
-#define CERES_TILE_XCD_MIX 3     // tile order vs XCDs: 3 shuffle windows of 64 (default), 2 the same for batches only,
-                                 // 1 rotate runs of 8 for batches, 0 plain centre-first
-#endif
-#ifndef CERES_FUSED_STEAL
-#define CERES_FUSED_STEAL 2      // fused shadow phase: 1 work stealing, 0 one ray per lane, 2 stealing for one-frame launches only
-#endif
-#ifndef CERES_FUSED_WG
-#define CERES_FUSED_WG 64        // fused kernel workgroup: 64 (8x8 tile, default) or 256 (16x16 tile)
-#endif
-static_assert(CERES_FUSED_WG == 256 || CERES_FUSED_WG == 64, "CERES_FUSED_WG must be 64 or 256");
-#ifndef CERES_FUSED
-#define CERES_FUSED 1            // full mode as ONE kernel (ceres_fused) instead of primary + shadow
-#endif
-#ifndef CERES_SHADOW_KERNEL
-#define CERES_SHADOW_KERNEL 1    // 0: one shadow ray per lane (ceres_shadow), 1: + intra-wavefront work stealing
-#endif
-#if CERES_SHADOW_KERNEL == 1
-#define CERES_SHADOW_FN ceres_shadow_steal
-#else
-#define CERES_SHADOW_FN ceres_shadow
-#endif
+constexpr size_t kTileShuffleWindow = 64;   // tiles per shuffled window of the centre-first order (XCD balance)
 
-// ---------------------------------------------------------------- shadow kernel
-template <bool kStats, bool kRobust>
-__global__ __launch_bounds__(kBlock) void ceres_shadow(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t* stk = lds + tid;
-    // per-shard job prefix in LDS (a per-lane binary search over a register array would be
-    // dynamically indexed and spill to scratch): wave 0 scans the 32 shard counters
-    __shared__ uint32_t pre[kShards + 1];
-    if (wave == 0) {
-        uint32_t x = lane < kShards ? P.shards[lane].queued : 0u;
-#pragma unroll
-        for (int off = 1; off < kShards; off <<= 1) {
-            const uint32_t y = __shfl_up(x, off, 64);
-            if (lane >= uint32_t(off)) x += y;
-        }
-        if (lane < kShards) pre[lane + 1] = x;
-        if (lane == 0) pre[0] = 0;
-    }
-    __syncthreads();
-    const uint32_t total = pre[kShards];
-    const uint32_t frame_pixels = P.local_rows * P.W;
-    uint32_t occluded = 0, n_pairs = 0, n_tests = 0;
-    bool overflow = false;
-    unsigned long long t_begin = 0;
-    Stamps stamps;
-    if (kStats) t_begin = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t g = blockIdx.x * kBlock + tid; g < total; g += gridDim.x * kBlock) {
-        uint32_t s = 0;                                              // shard holding global job g
-#pragma unroll
-        for (uint32_t step = 16; step > 0; step >>= 1)
-            if (pre[s + step] <= g) s += step;
-        const float4* q = reinterpret_cast<const float4*>(P.jobs + size_t(s) * P.shard_capacity + (g - pre[s]));
-        const float4 J0 = q[0], J1 = q[1];
-        const uint32_t pix = __float_as_uint(J0.x), slot = __float_as_uint(J0.y);
-        const float hu = J0.z, hv = J0.w;
-        const uint32_t f = P.frames > 1 ? pix / frame_pixels : 0;
-        const uint32_t rem = pix - f * frame_pixels;
-        const uint32_t lr = rem / P.W, i = rem - lr * P.W;
-        const F3 o{J1.x, J1.y, J1.z};
-        const F3 sun_line = normalize(f3(P.cam[f].sun) - o);        // render.hpp:135
-#ifdef CERES_SHADOW_BVH2
-        Hit h2{0, 0.f, 0.f, 0.f};
-        const bool blocked = trace<true, kStats, kBlock, uint32_t*, kRobust>(P, o, sun_line, stk, h2, n_pairs, n_tests,
-                                                                             overflow, kStats ? &stamps : nullptr);
-#else
-        const bool blocked = trace_any4<kStats, kBlock, uint32_t*, kRobust>(P, o, sun_line, stk, n_pairs, n_tests, overflow);
-#endif
-        if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
-        if (blocked) {                                               // render.hpp:147-150
-            ++occluded;
-            store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);
-        } else {                                                     // render.hpp:139-146
-            const F3 view = primary_dir(P, f, i, global_row(P, lr));
-            float c[3];
-            shade(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
-            store_pixel(P, f, lr, i, c[0], c[1], c[2]);
-        }
-    }
-    const uint32_t wo = wave_sum(occluded);
-    const uint32_t shard = (blockIdx.x * (kBlock / 64) + wave) % kShards;
-    if (lane == 0 && wo) atomicAdd(&P.shards[shard].hits, (unsigned long long)wo);
-    if (kStats) {
-        const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
-        uint32_t mp = n_pairs;                                       // longest chain in the wave
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) mp = max(mp, __shfl_xor(mp, off, 64));
-        if (lane == 0) {
-            atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
-            atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
-            if (P.wave_log) {                                        // diagnostic wave timeline
-                unsigned long long* w = P.wave_log + 8 * size_t(blockIdx.x * (kBlock / 64) + wave);
-                w[0] = t_begin; w[1] = __builtin_amdgcn_s_memrealtime(); w[2] = mp; w[3] = stamps.iters;
-                w[4] = stamps.box; w[5] = stamps.leaf; w[6] = stamps.next; w[7] = wp;
-            }
-        }
-    }
-    if (overflow) atomicOr(&P.shards[shard].error, 1u);
-}
-
-// ---------------------------------------------------------------- work-stealing shadow kernel
-// One shadow ray per lane like ceres_shadow, but the wavefront shares the work of its rays:
+// ---------------------------------------------------------------- work-stealing shadow phase
+// One-frame launches (latency-bound: a frame ends when its slowest tiles end) trace a
+// wavefront's shadow rays with the work shared among its lanes:
 // a shadow ray is any-hit, so the subtrees left on a ray's stack may be traversed in any
 // order and by any lane, and the ray is occluded iff ANY of those pieces finds a triangle hit
 // (the same set of leaf tests as trace_any4, see build_shadow_bvh4).  After every step, lanes
 // that have finished their own piece take the BOTTOM entry (the largest pending subtree) of a
 // lane that still has stacked subtrees, together with that ray's origin / inverse direction
 // (cross-lane shuffles); a hit marks the owning lane's pixel occluded in LDS and cancels the
-// ray's other pieces.  A single long ray -- 60+ BVH4 steps on C3, which set the kernel's
-// duration in ceres_shadow -- is thus traversed by up to 64 lanes at once.  Pixels are shaded
+// ray's other pieces.  A single long ray -- 60+ BVH4 steps on C3, which set the duration of a
+// one-ray-per-lane frame -- is thus traversed by up to 64 lanes at once.  Pixels are shaded
 // together once the wavefront has no work left.  Stacks are per-lane ring buffers in LDS.
 struct RayWork {
     F3 o, d;
@@ -1027,7 +554,6 @@ struct StealLdsT {
     uint32_t mail[kS];               // stolen node, by thief rank within the wavefront
     uint32_t from[kS];               // donor lane, by thief rank
 };
-using StealLds = StealLdsT<kBlock>;
 
 // Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
 // intra-wavefront work stealing; on return L.blocked[tid] holds the lane's answer.  Must be
@@ -1177,77 +703,19 @@ __device__ __forceinline__ void finish_pixel(const KParams& P, uint32_t f, uint3
     }
 }
 
-template <bool kStats, bool kRobust>
-__global__ __launch_bounds__(kBlock) void ceres_shadow_steal(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ uint32_t pre[kShards + 1];
-    __shared__ StealLds L;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t* stk = lds + tid;
-    if (wave == 0) {
-        uint32_t x = lane < kShards ? P.shards[lane].queued : 0u;
-#pragma unroll
-        for (int off = 1; off < kShards; off <<= 1) {
-            const uint32_t y = __shfl_up(x, off, 64);
-            if (lane >= uint32_t(off)) x += y;
-        }
-        if (lane < kShards) pre[lane + 1] = x;
-        if (lane == 0) pre[0] = 0;
-    }
-    __syncthreads();
-    const uint32_t total = pre[kShards];
-    const uint32_t frame_pixels = P.local_rows * P.W;
-    uint32_t occluded = 0, n_pairs = 0, n_tests = 0;
-    bool overflow = false;
-    for (uint32_t g0 = blockIdx.x * kBlock; g0 < total; g0 += gridDim.x * kBlock) {
-        const uint32_t g = g0 + tid;
-        const bool has_job = g < total;
-        uint32_t pix = 0, slot = 0, f = 0;
-        float hu = 0.f, hv = 0.f;
-        RayWork w{};
-        if (has_job) {
-            uint32_t sh = 0;
-#pragma unroll
-            for (uint32_t step = 16; step > 0; step >>= 1)
-                if (pre[sh + step] <= g) sh += step;
-            const float4* q = reinterpret_cast<const float4*>(P.jobs + size_t(sh) * P.shard_capacity + (g - pre[sh]));
-            const float4 J0 = q[0], J1 = q[1];
-            pix = __float_as_uint(J0.x); slot = __float_as_uint(J0.y); hu = J0.z; hv = J0.w;
-            f = P.frames > 1 ? pix / frame_pixels : 0;
-            w = make_shadow_ray<kRobust>(F3{J1.x, J1.y, J1.z}, f3(P.cam[f].sun));
-        }
-        steal_traverse<kStats, kBlock, uint32_t*, kRobust>(P, has_job, w, stk, L, tid, lane, n_pairs, n_tests, overflow);
-        if (has_job) {                                                   // shade every pixel together
-            const uint32_t rem = pix - f * frame_pixels;
-            const uint32_t lr = rem / P.W, i = rem - lr * P.W;
-            finish_pixel(P, f, lr, i, pix, L.blocked[tid] != 0, w.d, slot, hu, hv, occluded);
-        }
-        __syncthreads();                                                 // L reuse next round
-    }
-    const uint32_t wo = wave_sum(occluded);
-    const uint32_t shard = (blockIdx.x * (kBlock / 64) + wave) % kShards;
-    if (lane == 0 && wo) atomicAdd(&P.shards[shard].hits, (unsigned long long)wo);
-    if (kStats) {
-        const uint32_t wp = wave_sum(n_pairs), wt = wave_sum(n_tests);
-        if (lane == 0) {
-            atomicAdd(&P.shards[shard].pairs, (unsigned long long)wp);
-            atomicAdd(&P.shards[shard].tests, (unsigned long long)wt);
-        }
-    }
-    if (overflow) atomicOr(&P.shards[shard].error, 1u);
-}
-
 // ---------------------------------------------------------------- fused frame kernel
 // Primary + shadow + shading of an 8x8 pixel tile per wavefront in ONE kernel: each wavefront
 // traces its tile's primary rays (BVH2, exact reference order), then the shadow rays of its
-// own hits with intra-wavefront work stealing (lanes whose pixel missed help the others), then
-// shades.  No shadow-ray queue in HBM, no second launch: the shadow work of early tiles
-// overlaps the primary work of later ones.  Same results as ceres_primary + ceres_shadow.
-template <bool kStats, int kB, typename StkT, int kMinW, bool kRobust, bool kSteal>
-__global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
+// own hits over the BVH4 (any-hit; one-frame launches with intra-wavefront work stealing, lanes
+// whose pixel missed help the others), then shades.  No shadow-ray queue in HBM, no second
+// launch: the shadow work of early tiles overlaps the primary work of later ones.
+constexpr int kFusedB = 64;      // single-wavefront workgroups (LDS is released per workgroup)
+template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal>
+__global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
+    constexpr int kB = kFusedB;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ StealLdsT<kB> L;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t lane = threadIdx.x, tid = lane;
     // traversal stacks [entry][lane]: 16-, 24- or 32-bit entries, the narrowest every node index
     // of the scene fits (host choice)
     StkT stk;
@@ -1256,24 +724,22 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
                     reinterpret_cast<uint8_t*>(lds) + size_t(P.lds_entries) * kB * 2 + tid};
     else
         stk = reinterpret_cast<StkT>(lds) + tid;
-    // 1-D grid over the batch's tiles in tile_order (centre of the image first, so the
-    // expensive tiles start early and cheap background tiles fill the end of the launch).
-    // kB = 256: a 16x16 tile per workgroup, its four 8x8 quarters one per wavefront;
-    // kB = 64: one 8x8 tile per single-wavefront workgroup, so a long tile holds only its own
-    // LDS and wave slot, never three finished siblings' (LDS is released per workgroup).
-    constexpr uint32_t kTile = kB == 256 ? 16 : 8;
+    // 1-D grid over the batch's 8x8 tiles in tile_order (centre of the image first, so the
+    // expensive tiles start early and cheap background tiles fill the end of the launch); one
+    // tile per single-wavefront workgroup, so a long tile holds only its own LDS and wave slot.
+    constexpr uint32_t kTile = 8;
     // kTPW consecutive entries of the order per wavefront in batches (throughput: fewer, longer
     // wavefronts -- the background tiles' short waves are mostly launch and first-fetch latency);
     // one per wavefront for single frames (latency: their longest tiles set the frame time) and
     // in stats builds (the wave log is per tile)
-    constexpr uint32_t kTPW = (kStats || kB != 64 || kSteal) ? 1 : CERES_TILES_PER_WAVE;
+    constexpr uint32_t kTPW = (kStats || kSteal) ? 1 : CERES_TILES_PER_WAVE;
     const uint32_t per_frame = P.tiles_x * P.row_blocks_per_frame;
     const uint32_t n_tiles = per_frame * P.frames;
     uint32_t n_shadow = 0, occluded = 0, n_pairs = 0, n_tests = 0;
     bool overflow = false;
     // this wavefront's tile-order entries, read once through the scalar cache (a vector load of a
     // uniform address would put a full vector-memory round trip in front of every tile; the order
-    // buffer is padded to a multiple of 4 entries)
+    // buffer is padded to a multiple of 8 entries)
     static_assert(kTPW == 1 || kTPW == 2 || kTPW == 4 || kTPW == 8, "CERES_TILES_PER_WAVE must be 1, 2, 4 or 8");
     uint4 tiles4 = make_uint4(0, 0, 0, 0), tiles4b = make_uint4(0, 0, 0, 0);
     if constexpr (kTPW == 8) {
@@ -1296,14 +762,12 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     const uint32_t f = t / per_frame;
     const uint32_t rem = t - f * per_frame;
     const uint32_t by = rem / P.tiles_x, bx = rem - by * P.tiles_x;
-#if CERES_LANE_QUADS
-    // lane -> pixel with every quad of lanes (4k..4k+3) a 2x2 pixel block
+    // lanes in Morton order over the tile: every quad of lanes (4k..4k+3) is a 2x2 pixel block,
+    // so the quads the texture addresser processes together hold neighbouring rays (A/B: solo
+    // C3 -2.4 %, C5 batches -1.5 %)
     const uint32_t lx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4), ly = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
-#else
-    const uint32_t lx = lane & 7, ly = lane >> 3;
-#endif
-    const uint32_t i = bx * kTile + (kB == 256 ? (wave & 1) * 8 : 0) + lx;
-    const uint32_t lr = by * kTile + (kB == 256 ? (wave >> 1) * 8 : 0) + ly;
+    const uint32_t i = bx * kTile + lx;
+    const uint32_t lr = by * kTile + ly;
     const bool active = i < P.W && lr < P.local_rows;
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;
     bool hit = false;
@@ -1344,15 +808,7 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
     if constexpr (kSteal)
         steal_traverse<kStats, kB, StkT, kRobust>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
     else
-    {
-#if CERES_FUSED_SHADOW_BVH2
-        // A/B: any-hit over the reference BVH2 with the pipelined step of trace()
-        Hit h2{0, 0.f, 0.f, 0.f};
-        L.blocked[tid] = hit && trace<true, kStats, kB, StkT, kRobust>(P, w.o, w.d, stk, h2, n_pairs, n_tests, overflow) ? 1u : 0u;
-#else
         L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
-#endif
-    }
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
@@ -1362,15 +818,14 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kMinW))) voi
         for (int off = 32; off > 0; off >>= 1) mx = max(mx, uint32_t(__shfl_xor(int(mx), off, 64)));
         const uint32_t sp = wave_sum(prim_pairs), ss = wave_sum(n_pairs - prim_pairs);
         if (lane == 0) {
-            unsigned long long* wl = P.wave_log + 8 * size_t(blockIdx.x * (kB / 64) + wave);
+            unsigned long long* wl = P.wave_log + 8 * size_t(blockIdx.x);
             wl[0] = t_start; wl[1] = t_primary; wl[2] = t_end; wl[3] = mx; wl[4] = shadow_iters;
             wl[5] = n_shadow_t; wl[6] = sp; wl[7] = ss;
         }
     }
     }
     const uint32_t wo = wave_sum(occluded);
-    const uint32_t wave_id = blockIdx.x * (kB / 64) + wave;
-    const uint32_t shard = wave_id % kShards;
+    const uint32_t shard = blockIdx.x % kShards;
     if (lane == 0 && n_shadow) {
         atomicAdd(&P.shards[shard].queued, n_shadow);                  // shadow rays traced
         atomicAdd(&P.shards[shard].hits, (unsigned long long)(n_shadow + wo));
@@ -1469,10 +924,10 @@ void ceres::scene_release(ceres_scene* s) {
     for (auto& d : s->retired) dfree(d);
     s->orders.clear(); s->retired.clear(); s->retired_bytes = 0;
     dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
-    dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_jobs); dfree(s->d_pixels); dfree(s->d_rgb8);
+    dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
     for (auto e : s->ev_used) (void)hipEventDestroy(e);
-    s->ev_pool.clear(); s->ev_used.clear(); s->ev_fused.clear();
+    s->ev_pool.clear(); s->ev_used.clear();
     if (s->stream) (void)hipStreamDestroy(s->stream);
     s->stream = nullptr;
 }
@@ -1486,12 +941,7 @@ size_t local_rows_of(size_t H, uint32_t rb, uint32_t rank, uint32_t world) {
     return rows;
 }
 
-int ensure_workspace(ceres_scene* s, size_t jobs, size_t px, bool want_px, bool want_rgb) {
-    if (jobs > s->jobs_cap) {
-        dfree(s->d_jobs);
-        HIP_TRY(hipMalloc(&s->d_jobs, jobs * sizeof(ShadowJob)));
-        s->jobs_cap = jobs;
-    }
+int ensure_workspace(ceres_scene* s, size_t px, bool want_px, bool want_rgb) {
     if ((want_px || want_rgb) && px > s->px_cap) {
         dfree(s->d_pixels); dfree(s->d_rgb8);
         HIP_TRY(hipMalloc(&s->d_pixels, px * 3 * sizeof(float)));
@@ -1501,27 +951,25 @@ int ensure_workspace(ceres_scene* s, size_t jobs, size_t px, bool want_px, bool 
     return CERES_OK;
 }
 
-constexpr uint32_t kFusedWG = CERES_FUSED_WG;
-
 // Caches `order` on the scene under its key (see ensure_tile_order) and uploads it.
 int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, uint32_t frames, uint32_t tile,
-                      uint32_t cluster, const std::vector<uint32_t>& order, hipStream_t stream, const uint32_t** out) {
+                      const std::vector<uint32_t>& order, hipStream_t stream, const uint32_t** out) {
     const size_t n = order.size();
     ceres_scene::TileOrder o;
     if (s->orders.size() >= ceres::kMaxTileOrders) {
         auto lru = std::min_element(s->orders.begin(), s->orders.end(),
                                     [](const auto& a, const auto& b) { return a.used < b.used; });
         s->retired.push_back(lru->d);                                // a launch may still read it
-        s->retired_bytes += lru->cap * sizeof(uint32_t);
+        s->retired_bytes += (lru->cap * sizeof(uint32_t) + kAllocGranule - 1) / kAllocGranule * kAllocGranule;
         s->orders.erase(lru);
-        if (s->retired_bytes > ceres::kRetiredBytes) {
+        if (s->retired_bytes > ceres::kRetiredBytes || s->retired.size() >= ceres::kMaxRetired) {
             HIP_TRY(hipDeviceSynchronize());
             for (auto& d : s->retired) dfree(d);
             s->retired.clear();
             s->retired_bytes = 0;
         }
     }
-    o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile; o.cluster = cluster;
+    o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile;
     // padded to a multiple of 8 entries (zeros): the fused kernel reads its tile-order entries
     // up to eight at a time through the scalar cache
     const size_t padded = (n + 7) / 8 * 8;
@@ -1543,62 +991,21 @@ int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
 
 // Centre-first order of a batch's tile x tile tiles for the fused kernel: ascending distance of the
 // tile centre (global pixel coordinates) from the image centre, frames interleaved (views of
-// CERES_FRAME_MAJOR_PIXELS and more: frame after frame).  Cached
-// on the scene per (W, H, tiling, frames, tile, cluster) -- up to kMaxTileOrders orders; the
-// least recently used one is retired (freed later, see ceres_scene::retired), so eviction
-// neither rewrites an order a launch in flight reads nor stalls the streams.
+// CERES_FRAME_MAJOR_PIXELS and more: frame after frame), then shuffled in windows of 64 for the
+// XCD balance.  Cached on the scene per (W, H, tiling, frames, tile) -- up to kMaxTileOrders
+// orders; the least recently used one is retired (freed later, see ceres_scene::retired), so
+// eviction neither rewrites an order a launch in flight reads nor stalls the streams.
 int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, size_t rows, uint32_t frames,
-                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out,
-                      uint32_t cluster = 1) {
+                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out) {
     for (auto& o : s->orders)
         if (o.W == W && o.H == H && o.row_block == t.row_block && o.rank == t.rank && o.world == t.world &&
-            o.frames == frames && o.tile == tile && o.cluster == cluster) {
+            o.frames == frames && o.tile == tile) {
             o.used = ++s->order_clock;
             *out = o.d;
             return CERES_OK;
         }
     const size_t n = size_t(bx) * by * frames;
     const double cx = 0.5 * double(W), cy = 0.5 * double(H);
-    if (cluster > 1) {
-        // Batches (several tiles per wavefront, kTPW): the order is built over clusters of
-        // cluster x cluster tiles, each expanded into its tiles consecutively, so the tiles one
-        // wavefront renders in turn are neighbours and share their BVH nodes and triangles in
-        // the CU's vector L1 (the loads' tail latency is set by L1 misses).  Clusters are
-        // centre-first and shuffled in windows for the XCD balance, as tiles are below.
-        const uint32_t cbx = (bx + cluster - 1) / cluster, cby = (by + cluster - 1) / cluster;
-        const size_t nc = size_t(cbx) * cby * frames;
-        std::vector<std::pair<double, uint32_t>> kc(nc);
-        const uint32_t span = cluster * tile;
-        for (uint32_t f = 0; f < frames; ++f)
-            for (uint32_t y = 0; y < cby; ++y) {
-                const size_t lr = std::min<size_t>(size_t(y) * span + span / 2, rows - 1);
-                const size_t j = ((lr / t.row_block) * t.world + t.rank) * t.row_block + lr % t.row_block;
-                for (uint32_t x = 0; x < cbx; ++x) {
-                    const double dx = double(x) * span + span / 2 - cx, dy = double(j) - cy;
-                    const uint32_t id = (f * cby + y) * cbx + x;
-                    kc[id] = {dx * dx + dy * dy, id};
-                }
-            }
-        std::stable_sort(kc.begin(), kc.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-        uint64_t st = 0x9e3779b97f4a7c15ull;
-        const size_t win = std::max<size_t>(1, CERES_TILE_SHUFFLE_WINDOW / (cluster * cluster));
-        for (size_t b0 = 0; b0 < nc; b0 += win) {
-            const size_t len = std::min<size_t>(win, nc - b0);
-            for (size_t q = len - 1; q > 0; --q) {
-                st = st * 6364136223846793005ull + 1442695040888963407ull;
-                std::swap(kc[b0 + q], kc[b0 + size_t((st >> 33) % (q + 1))]);
-            }
-        }
-        std::vector<uint32_t> order;
-        order.reserve(n);
-        for (const auto& c : kc) {
-            const uint32_t f = c.second / (cbx * cby), r = c.second % (cbx * cby);
-            const uint32_t y0 = (r / cbx) * cluster, x0 = (r % cbx) * cluster;
-            for (uint32_t y = y0; y < std::min(y0 + cluster, by); ++y)
-                for (uint32_t x = x0; x < std::min(x0 + cluster, bx); ++x) order.push_back((f * by + y) * bx + x);
-        }
-        return upload_tile_order(s, W, H, t, frames, tile, cluster, order, stream, out);
-    }
     std::vector<std::pair<double, uint32_t>> k(n);
     // Large views go one frame after another (each centre-first): the waves in flight then share
     // one view's BVH nodes and triangles in L2 instead of F views' (8 x 16-frame batches: dragon
@@ -1623,33 +1030,6 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     });
     std::vector<uint32_t> order(n);
     for (size_t q = 0; q < n; ++q) order[q] = k[q].second;
-#if CERES_TILE_XCD_WEDGE
-    // XCD-aware (cdna_hip_programming.md T1): workgroups b and b + 8 share an XCD and its L2, so
-    // give XCD-group w the tiles of wedge w of every frame (8 equal-count angular wedges about the
-    // image centre), each wedge centre-first: an L2 then serves one eighth of the view instead of
-    // all of it.
-    {
-        std::vector<uint32_t> wedge(n);
-        std::vector<std::pair<double, uint32_t>> ang;
-        for (uint32_t f = 0; f < frames; ++f) {
-            ang.clear();
-            for (uint32_t y = 0; y < by; ++y) {
-                const size_t lr = std::min<size_t>(size_t(y) * tile + tile / 2, rows - 1);
-                const size_t j = ((lr / t.row_block) * t.world + t.rank) * t.row_block + lr % t.row_block;
-                for (uint32_t x = 0; x < bx; ++x)
-                    ang.push_back({std::atan2(double(j) - cy, double(x) * tile + tile / 2 - cx), (f * by + y) * bx + x});
-            }
-            std::stable_sort(ang.begin(), ang.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-            for (size_t q = 0; q < ang.size(); ++q) wedge[ang[q].second] = uint32_t(q * 8 / ang.size());
-        }
-        std::vector<std::vector<uint32_t>> lists(8);
-        for (size_t q = 0; q < n; ++q) lists[wedge[order[q]]].push_back(order[q]);   // centre-first per wedge
-        size_t m = 0;
-        for (size_t i = 0; m < n; ++i)
-            for (int w = 0; w < 8; ++w)
-                if (i < lists[w].size()) order[m++] = lists[w][i];
-    }
-#elif CERES_TILE_XCD_MIX >= 2
     // Workgroups b and b + 8 share an XCD (MI355X_MICROARCH.md: blocks are dealt round-robin over
     // the 8 XCDs), and the XCD with the most work sets a launch's length.  The centre-first order
     // is regular -- equal-distance tiles of the F frames and mirror-image tiles sit side by side --
@@ -1657,28 +1037,15 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     // of four; the left half of a mesh).  Shuffling each window of 64 (fixed seed) keeps the order
     // centre-first at that granularity and gives every XCD an unbiased sample: solo bunny 1080p
     // -9.5 %, dragon 4096^2 -5.5 %; one rank of a 2-GPU split 40 % -> 0 % apart.
-    // (Mode 2: batches only; 3: always.)
-    if (CERES_TILE_XCD_MIX == 3 || frames > 1) {
-        uint64_t st = 0x9e3779b97f4a7c15ull;
-        for (size_t b0 = 0; b0 < n; b0 += CERES_TILE_SHUFFLE_WINDOW) {
-            const size_t len = std::min<size_t>(CERES_TILE_SHUFFLE_WINDOW, n - b0);
-            for (size_t q = len - 1; q > 0; --q) {
-                st = st * 6364136223846793005ull + 1442695040888963407ull;
-                std::swap(order[b0 + q], order[b0 + size_t((st >> 33) % (q + 1))]);
-            }
+    uint64_t st = 0x9e3779b97f4a7c15ull;
+    for (size_t b0 = 0; b0 < n; b0 += dev::kTileShuffleWindow) {
+        const size_t len = std::min<size_t>(dev::kTileShuffleWindow, n - b0);
+        for (size_t q = len - 1; q > 0; --q) {
+            st = st * 6364136223846793005ull + 1442695040888963407ull;
+            std::swap(order[b0 + q], order[b0 + size_t((st >> 33) % (q + 1))]);
         }
     }
-#elif CERES_TILE_XCD_MIX
-    // Workgroups b and b + 8 share an XCD (MI355X_MICROARCH.md: blocks are dealt round-robin
-    // over the 8 XCDs).  Equal-distance tiles of the F frames are adjacent in the order, so with
-    // F a divisor or multiple of 8 every XCD would get the same frames for the whole launch and
-    // the XCD holding the costliest view would set the launch's length.  Rotating each run of 8
-    // by its index deals every frame to every XCD.  (One frame: left as is -- the rotation only
-    // scatters neighbouring tiles over more L2s, +8 MB of DRAM reads per C3 frame.)
-    for (size_t b0 = 0; frames > 1 && b0 + 8 <= n; b0 += 8)
-        std::rotate(order.begin() + b0, order.begin() + b0 + (b0 / 8) % 8, order.begin() + b0 + 8);
-#endif
-    return upload_tile_order(s, W, H, t, frames, tile, 1, order, stream, out);
+    return upload_tile_order(s, W, H, t, frames, tile, order, stream, out);
 }
 
 // One batch: `frames` cameras (basis12 = frames x {eye, dir, iu, iv}) and suns (frames x 3).
@@ -1703,13 +1070,6 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     if ((d_rec_prim != nullptr) != (d_rec_tuv != nullptr) || (d_rec_prim != nullptr) != (d_rec_shadow != nullptr))
         return set_error(CERES_EINVAL, "render: hit records need all three arrays");
     HIP_TRY(hipSetDevice(s->device));
-    const size_t nwaves = size_t(bx) * by * frames * (dev::kBlock / 64);
-    const uint32_t cap = uint32_t(((nwaves + kShards - 1) / kShards) * 64);   // <= 64 jobs per wavefront
-    // only the two-pass path (ceres_primary -> shadow kernel) queues shadow jobs in HBM; the fused
-    // kernel and primary-only mode never touch them
-    const bool two_pass = !CERES_FUSED && mode == CERES_MODE_FULL;
-    if (two_pass)
-        if (int rc = ensure_workspace(s, size_t(cap) * kShards, 0, false, false)) return rc;
 
     KParams P{};
     for (uint32_t f = 0; f < frames; ++f) {
@@ -1725,58 +1085,49 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     P.stack_entries = s->stack_entries;
     P.shadow_stack_entries = s->shadow_stack_entries;
     P.root_leaf_count = s->root_leaf_count; P.root_leaf_first = s->root_leaf_first;
-    P.shard_capacity = cap;
     P.pairs = s->d_pairs; P.nodes4 = s->d_nodes4; P.tris = s->d_tris; P.orig = s->d_orig; P.norms = s->d_norms;
-    P.pixels = d_pixels; P.rgb8 = d_rgb8; P.jobs = s->d_jobs; P.shards = s->d_shards;
+    P.pixels = d_pixels; P.rgb8 = d_rgb8; P.shards = s->d_shards;
     P.rec_prim = d_rec_prim; P.rec_tuv = d_rec_tuv; P.rec_shadow = d_rec_shadow;
 
     const bool stats = (s->flags & CERES_SCENE_STATS) != 0;
-    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    const bool full = mode == CERES_MODE_FULL;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
     if (s->timing && rows) {
-        while (s->ev_pool.size() < 3) { hipEvent_t e; HIP_TRY(hipEventCreate(&e)); s->ev_pool.push_back(e); }
+        while (s->ev_pool.size() < 2) { hipEvent_t e; HIP_TRY(hipEventCreate(&e)); s->ev_pool.push_back(e); }
         e0 = s->ev_pool.back(); s->ev_pool.pop_back();
         e1 = s->ev_pool.back(); s->ev_pool.pop_back();
-        e2 = s->ev_pool.back(); s->ev_pool.pop_back();
-        s->ev_used.push_back(e0); s->ev_used.push_back(e1); s->ev_used.push_back(e2);
-        s->ev_fused.push_back(char(CERES_FUSED && mode == CERES_MODE_FULL));
+        s->ev_used.push_back(e0); s->ev_used.push_back(e1);
     }
-    // fused kernel tiles: kFusedWG = 256 -> 16x16 per workgroup, 64 -> 8x8
-    constexpr uint32_t ftile = kFusedWG == 256 ? 16 : 8;
+    constexpr uint32_t ftile = 8;                                    // fused kernel: 8x8 tiles
     const uint32_t fbx = uint32_t((W + ftile - 1) / ftile), fby = uint32_t((rows + ftile - 1) / ftile);
     const uint32_t* tile_order = nullptr;
-    // batches render CERES_TILES_PER_WAVE consecutive tiles per wavefront: 2x2 clusters of them
-    const bool clustered = CERES_FUSED_WG == 64 && CERES_TILES_PER_WAVE == 4 && CERES_TILE_CLUSTER &&
-                           !(s->flags & CERES_SCENE_STATS) && !(CERES_FUSED_STEAL == 1 || (CERES_FUSED_STEAL == 2 && frames == 1));
-    if (CERES_FUSED && mode == CERES_MODE_FULL && rows)
-        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order, clustered ? 2 : 1))
-            return rc;
-    // The shards must start at zero when they are read back (counters) or hold the two-pass
-    // shadow queue; the fused kernel without counters only adds to them, so its steady-state
-    // frames skip the memset (ceres_finalize re-zeroes them after every counted render).
-    const bool need_clean = d_counters || !(CERES_FUSED && mode == CERES_MODE_FULL);
+    if (full && rows)
+        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order)) return rc;
+    // The shards must start at zero when they are read back (counters) or count primary-only hits;
+    // the fused kernel without counters only adds to them, so its steady-state frames skip the
+    // memset (ceres_finalize re-zeroes them after every counted render).
+    const bool need_clean = d_counters || !full;
     if (need_clean && s->shards_dirty) HIP_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, stream));
     s->shards_dirty = true;
     if (rows) {                                                      // a rank may own no rows
         if (e0) HIP_TRY(hipEventRecord(e0, stream));
-        const size_t lds = size_t(s->stack_entries + CERES_STEP_SELECT) * dev::kBlock * 4;
-        const dim3 grid(bx, by * frames), block(dev::kBlock);
-        if (CERES_FUSED && mode == CERES_MODE_FULL) {
-            // one kernel: primary + work-stealing shadow + shading per 8x8 tile
+        if (full) {
+            // one kernel: primary + shadow + shading per 8x8 tile
             const size_t nmax = std::max(s->n_pairs, s->n_nodes4);
             const int stw = CERES_STACK16 && nmax < (1u << 16) ? 2 : CERES_STACK24 && nmax < (1u << 24) ? 3 : 4;
             const bool st16 = stw == 2;
-            P.lds_entries = uint32_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries));
-            const size_t flds = size_t(P.lds_entries) * kFusedWG * stw;
+            P.lds_entries = uint32_t(std::max(s->stack_entries + 1, s->shadow_stack_entries));
+            const size_t flds = size_t(P.lds_entries) * dev::kFusedB * stw;
             P.tile_order = tile_order;
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
             // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
-            const bool steal = CERES_FUSED_STEAL == 1 || (CERES_FUSED_STEAL == 2 && frames == 1);
-            const uint32_t tpw = (kFusedWG == 64 && !stats && !steal) ? CERES_TILES_PER_WAVE : 1;   // = kTPW
+            const bool steal = frames == 1;
+            const uint32_t tpw = (!stats && !steal) ? CERES_TILES_PER_WAVE : 1;   // = kTPW
             const uint32_t n_tiles = fbx * fby * frames;
-            const dim3 fgrid((n_tiles + tpw - 1) / tpw), fblock(kFusedWG);
+            const dim3 fgrid((n_tiles + tpw - 1) / tpw), fblock(dev::kFusedB);
             if (stats) {                                             // per-wave diagnostic timeline
-                const size_t waves = size_t(fbx) * fby * frames * (kFusedWG / 64);
+                const size_t waves = size_t(fbx) * fby * frames;
                 if (s->wave_log_waves < waves) {
                     dfree(s->d_wave_log);
                     HIP_TRY(hipMalloc(&s->d_wave_log, waves * 64));
@@ -1786,17 +1137,17 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
                 P.wave_log = s->d_wave_log;
                 s->last_grid_waves = waves;
             }
-            // small scenes (16-bit stacks, LDS for 7+ waves/SIMD) get a 7-wave VGPR budget: +3.7 % C3
-            // frames/s with 8 frames in flight; C5-size scenes keep the unconstrained allocation
+            // VGPR budgets: 16-bit-stack scenes (LDS for 7+ waves/SIMD) are compiled for 6 waves,
+            // C5-size scenes keep the unconstrained allocation
             constexpr int w16 = CERES_FUSED_MINW16, w32 = CERES_FUSED_MINW32;
             auto fused = [&](auto rt, auto st) {
                 constexpr bool R = decltype(rt)::value, T = decltype(st)::value;
-                if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint16_t*, 1, R, T>), fgrid, fblock, flds, stream, P);
-                else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
-                else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, kFusedWG, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);
-                else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint16_t*, w16, R, T>), fgrid, fblock, flds, stream, P);
-                else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
-                else hipLaunchKernelGGL((dev::ceres_fused<false, kFusedWG, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);
+                if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, uint16_t*, 1, R, T>), fgrid, fblock, flds, stream, P);
+                else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
+                else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);
+                else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, R, T>), fgrid, fblock, flds, stream, P);
+                else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);
             };
             auto fused_s = [&](auto rt) {
                 if (steal) fused(rt, std::true_type{});
@@ -1804,49 +1155,19 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             };
             if (robust) fused_s(std::true_type{});
             else fused_s(std::false_type{});
-            HIP_TRY(hipGetLastError());
-            if (e1) HIP_TRY(hipEventRecord(e1, stream));
-            if (e2) HIP_TRY(hipEventRecord(e2, stream));
         } else {
-        auto primary = [&](auto rt) {
-            constexpr bool R = decltype(rt)::value;
-            if (mode == CERES_MODE_PRIMARY) {
-                if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, true, R>), grid, block, lds, stream, P);
-                else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_PRIMARY, false, R>), grid, block, lds, stream, P);
-            } else {
-                if (stats) hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, true, R>), grid, block, lds, stream, P);
-                else hipLaunchKernelGGL((dev::ceres_primary<CERES_MODE_FULL, false, R>), grid, block, lds, stream, P);
-            }
-        };
-        if (robust) primary(std::true_type{});
-        else primary(std::false_type{});
+            const size_t lds = size_t(s->stack_entries + 1) * dev::kBlock * 4;
+            const dim3 grid(bx, by * frames), block(dev::kBlock);
+            auto primary = [&](auto rt) {
+                constexpr bool R = decltype(rt)::value;
+                if (stats) hipLaunchKernelGGL((dev::ceres_primary<true, R>), grid, block, lds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_primary<false, R>), grid, block, lds, stream, P);
+            };
+            if (robust) primary(std::true_type{});
+            else primary(std::false_type{});
+        }
         HIP_TRY(hipGetLastError());
         if (e1) HIP_TRY(hipEventRecord(e1, stream));
-        if (mode == CERES_MODE_FULL) {
-            // one lane per queued shadow ray (at most one per pixel), grid-stride beyond 8 workgroups/CU
-            const size_t want = (size_t(frames) * W * rows + dev::kBlock - 1) / dev::kBlock;
-            uint32_t sgrid = uint32_t(std::max<size_t>(1, std::min<size_t>(want, size_t(s->num_cus) * 8)));
-            const size_t slds = size_t(std::max(s->stack_entries + CERES_STEP_SELECT, s->shadow_stack_entries)) * dev::kBlock * 4;
-            if (stats) {
-                const size_t waves = size_t(sgrid) * (dev::kBlock / 64);
-                if (s->wave_log_waves < waves) {
-                    dfree(s->d_wave_log);
-                    HIP_TRY(hipMalloc(&s->d_wave_log, waves * 64));
-                    s->wave_log_waves = waves;
-                }
-                HIP_TRY(hipMemsetAsync(s->d_wave_log, 0, waves * 64, stream));
-                P.wave_log = s->d_wave_log;
-                s->last_grid_waves = waves;
-                if (robust) hipLaunchKernelGGL((dev::CERES_SHADOW_FN<true, true>), dim3(sgrid), block, slds, stream, P);
-                else hipLaunchKernelGGL((dev::CERES_SHADOW_FN<true, false>), dim3(sgrid), block, slds, stream, P);
-            } else {
-                if (robust) hipLaunchKernelGGL((dev::CERES_SHADOW_FN<false, true>), dim3(sgrid), block, slds, stream, P);
-                else hipLaunchKernelGGL((dev::CERES_SHADOW_FN<false, false>), dim3(sgrid), block, slds, stream, P);
-            }
-            HIP_TRY(hipGetLastError());
-        }
-        if (e2) HIP_TRY(hipEventRecord(e2, stream));
-        }
     }
     if (d_counters) {
         hipLaunchKernelGGL(dev::ceres_finalize, dim3(1), dim3(64), 0, stream, s->d_shards,
@@ -1875,15 +1196,6 @@ int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStrea
 
 extern "C" {
 
-#if CERES_DIAG_UNIFORM
-int ceres_diag_read(uint64_t* out) {            // diagnostic builds only: read and zero g_diag
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(ceres::dev::g_diag), sizeof(uint64_t) * 34));
-    static const uint64_t zero[34] = {};
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(ceres::dev::g_diag), zero, sizeof(zero)));
-    return CERES_OK;
-}
-#endif
-
 const char* ceres_last_error(void) { return error_buffer(); }
 const char* ceres_version(void) { return "ceres-mi355x 0.2 (gfx950)"; }
 int ceres_device_count(void) {
@@ -1892,8 +1204,7 @@ int ceres_device_count(void) {
     return n;
 }
 const char* ceres_kernel_names(void) {
-    return CERES_FUSED ? "ceres_fused,ceres_primary,ceres_finalize,ceres_assemble"
-                       : "ceres_primary,ceres_shadow,ceres_finalize,ceres_assemble";
+    return "ceres_fused,ceres_primary,ceres_finalize,ceres_assemble";
 }
 
 size_t ceres_tiling_local_rows(size_t height, const ceres_tiling* t) {
@@ -1920,35 +1231,8 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     uint32_t stack4 = 0, not_collapsed = 0;
     if (!rlc && build_shadow_bvh4(pairs, nodes4, stack4, not_collapsed)) return nullptr;
     if (nodes4.empty()) nodes4.emplace_back();
-#if CERES_FOOTPRINT_PAD
-    {   // diagnostic A/B only: every pair record followed by an unused one (2x the primary BVH's
-        // cache footprint, same traversal) -- how sensitive is the kernel to L1/L2 capacity?
-        std::vector<SiblingPair> padded(2 * pairs.size());
-        for (size_t q = 0; q < pairs.size(); ++q) {
-            SiblingPair r = pairs[q];
-            if (r.lcount == 0) r.lfirst *= 2;
-            if (r.rcount == 0) r.rfirst *= 2;
-            padded[2 * q] = r;
-            padded[2 * q + 1] = r;
-        }
-        pairs.swap(padded);
-    }
-#endif
     auto* s = new (std::nothrow) ceres_scene;
     if (!s) { set_error(CERES_ENOMEM, "out of host memory"); return nullptr; }
-#if CERES_DIAG_UNIFORM
-    {
-        std::vector<uint32_t> parent(pairs.size(), 0);
-        for (size_t q = 0; q < pairs.size(); ++q) {
-            if (pairs[q].lcount == 0) parent[pairs[q].lfirst] = uint32_t(q);
-            if (pairs[q].rcount == 0) parent[pairs[q].rfirst] = uint32_t(q);
-        }
-        uint32_t* d = nullptr;
-        if (hipMalloc(&d, parent.size() * 4) == hipSuccess &&
-            hipMemcpy(d, parent.data(), parent.size() * 4, hipMemcpyHostToDevice) == hipSuccess)
-            (void)hipMemcpyToSymbol(HIP_SYMBOL(ceres::dev::g_diag_parent), &d, sizeof(d));
-    }
-#endif
     s->n_nodes4 = nodes4.size();
     s->shadow_stack_entries = std::max<uint32_t>(1, stack4);
     s->device = device; s->flags = flags; s->n_tri = n_tri; s->n_pairs = pairs.size();
@@ -2119,7 +1403,7 @@ int ceres_render_f32(ceres_scene* s, const float basis12[12], const float sun[3]
                      uint8_t* rgb8, size_t W, size_t H, ceres_stats* stats) {
     if (!s) return set_error(CERES_EINVAL, "null scene");
     HIP_TRY(hipSetDevice(s->device));
-    if (int rc = ensure_workspace(s, 0, W * H, pixels != nullptr, rgb8 != nullptr)) return rc;
+    if (int rc = ensure_workspace(s, W * H, pixels != nullptr, rgb8 != nullptr)) return rc;
     hipEvent_t a, b;
     HIP_TRY(hipEventCreate(&a));
     HIP_TRY(hipEventCreate(&b));
@@ -2179,7 +1463,7 @@ int ceres_render_multi_f32(ceres_scene* const* scenes, uint32_t world, uint32_t 
         const size_t rows = local_rows_of(H, row_block, r, world);
         if (hipSetDevice(s->device) != hipSuccess) { rc = set_error(CERES_EHIP, "hipSetDevice(%d)", s->device); break; }
         // rank 0's buffers also hold the assembled frame: size them for the whole frame up front
-        if ((rc = ensure_workspace(s, 0, r == 0 ? W * H : std::max<size_t>(rows, 1) * W, true, true))) break;
+        if ((rc = ensure_workspace(s, r == 0 ? W * H : std::max<size_t>(rows, 1) * W, true, true))) break;
         if ((rc = launch(s, 1, basis12, sun, mode, W, H, &t, pixels ? s->d_pixels : nullptr, s->d_rgb8, s->d_counters,
                          s->stream)))
             break;
@@ -2285,35 +1569,33 @@ int ceres_scene_wave_log(ceres_scene* s, uint64_t* out, size_t max_waves, size_t
     return CERES_OK;
 }
 
-// Per-kernel device timing for the roofline leg of bench.py: while enabled, every render
-// records HIP events around ceres_primary and ceres_shadow (or the one ceres_fused launch, reported
-// as primary_ms with shadow_ms = 0) on the launch stream.
+// Per-launch device timing: while enabled, every render records HIP events around its one
+// kernel launch (ceres_fused or ceres_primary) on the launch stream.
 int ceres_scene_set_timing(ceres_scene* s, int enable) {
     if (!s) return set_error(CERES_EINVAL, "null scene");
     s->timing = enable != 0;
     return CERES_OK;
 }
 
-// Synchronises, sums the recorded kernel durations (ms) and recycles the events.
-int ceres_scene_read_timing(ceres_scene* s, double* primary_ms, double* shadow_ms, uint64_t* renders) {
+// Synchronises, sums the recorded kernel durations (ms) and recycles the events.  Every render
+// is one kernel, so the whole duration is reported as kernel_ms (shadow_ms: always 0, kept for
+// the ABI of the former two-kernel path).
+int ceres_scene_read_timing(ceres_scene* s, double* kernel_ms, double* shadow_ms, uint64_t* renders) {
     if (!s) return set_error(CERES_EINVAL, "null scene");
     HIP_TRY(hipSetDevice(s->device));
-    double p = 0, q = 0;
-    const size_t n = s->ev_used.size() / 3;
+    double p = 0;
+    const size_t n = s->ev_used.size() / 2;
     for (size_t k = 0; k < n; ++k) {
-        hipEvent_t e0 = s->ev_used[3 * k], e1 = s->ev_used[3 * k + 1], e2 = s->ev_used[3 * k + 2];
-        HIP_TRY(hipEventSynchronize(e2));
-        float a = 0.f, b = 0.f;
+        hipEvent_t e0 = s->ev_used[2 * k], e1 = s->ev_used[2 * k + 1];
+        HIP_TRY(hipEventSynchronize(e1));
+        float a = 0.f;
         HIP_TRY(hipEventElapsedTime(&a, e0, e1));
-        HIP_TRY(hipEventElapsedTime(&b, e1, e2));
         p += a;
-        if (!s->ev_fused[k]) q += b;   // fused: e1..e2 brackets no kernel
     }
     for (auto e : s->ev_used) s->ev_pool.push_back(e);
     s->ev_used.clear();
-    s->ev_fused.clear();
-    if (primary_ms) *primary_ms = p;
-    if (shadow_ms) *shadow_ms = q;
+    if (kernel_ms) *kernel_ms = p;
+    if (shadow_ms) *shadow_ms = 0.0;
     if (renders) *renders = n;
     return CERES_OK;
 }

@@ -281,9 +281,23 @@ int relayout_device(const Tri48* d_tris, uint32_t n_tri, const RefNode* d_nodes,
         SD_TRY(hipStreamSynchronize(stream));
         if (perr & kErrPrim) { rc = set_error(CERES_EINVAL, "primitive index out of range"); goto done; }
         if (perr & kErrNode4) {
-            rc = set_error(CERES_EUNSUPPORTED, "shadow BVH4: a leaf of more than %u triangles or an index above 2^27",
-                           kNode4MaxCount);
-            goto done;
+            // a leaf of more than 31 triangles (coincident centroids: the builder could not split
+            // it) does not fit a packed child word; the host collapse turns such leaves into piece
+            // nodes (build_shadow_bvh4).  Rare, one-off scene preparation: the pair records go to
+            // the host and the BVH4 records come back.
+            std::vector<SiblingPair> hp(out.n_pairs);
+            std::vector<Node4> n4;
+            uint32_t st4 = 0, not_collapsed = 0;
+            SD_TRY(hipMemcpyAsync(hp.data(), out.pairs, hp.size() * sizeof(SiblingPair), hipMemcpyDeviceToHost, stream));
+            SD_TRY(hipStreamSynchronize(stream));
+            if ((rc = build_shadow_bvh4(hp, n4, st4, not_collapsed))) goto done;
+            SD_TRY(hipFree(out.nodes4));
+            out.nodes4 = nullptr;
+            SD_TRY(hipMalloc(&out.nodes4, n4.size() * sizeof(Node4)));
+            SD_TRY(hipMemcpyAsync(out.nodes4, n4.data(), n4.size() * sizeof(Node4), hipMemcpyHostToDevice, stream));
+            SD_TRY(hipStreamSynchronize(stream));
+            out.n_nodes4 = uint32_t(n4.size());
+            out.stack4 = st4;
         }
     }
 #undef SD_TRY

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <string>
 #include <vector>
@@ -530,6 +531,13 @@ int relayout_bvh64(const RefNode64* nodes, size_t n_nodes, const uint64_t* prim,
 // it returns).  A child whose grandchildren are not contained (e.g. a box quirk of the builder's
 // quantile fallback) stays an entry of its own, so the equivalence holds unconditionally.
 // stack_bound: the most entries the traversal can ever hold (pushes along any root-leaf path).
+//
+// A child word packs a leaf as (first << 5 | count), so a leaf holds at most 31 triangles.  The
+// reference builder makes bigger leaves when no split separates the centroids (coincident
+// triangles; binned_sah_builder.hpp:179-196 falls back, top_down_builder.hpp:36 caps the depth),
+// so such a leaf becomes a "piece" node: an extra Node4 whose children are runs of <= 31 of the
+// leaf's triangles (or further piece nodes), every one with the leaf's own box.  Equal boxes
+// pass or fail together, so the triangles tested -- and the any-hit answer -- are unchanged.
 int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>& out, uint32_t& stack_bound,
                       uint32_t& not_collapsed) {
     struct Entry { const float* box; uint32_t count, first; };   // count 0: first = pair index
@@ -540,6 +548,36 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
     out.reserve(pairs.size() / 2 + 1);
     stack_bound = 0;
     not_collapsed = 0;
+    auto set_box = [](Node4& rec, int c, const float* b) {
+        rec.lo_x[c] = b[0]; rec.hi_x[c] = b[1]; rec.lo_y[c] = b[2]; rec.hi_y[c] = b[3]; rec.lo_z[c] = b[4]; rec.hi_z[c] = b[5];
+    };
+    // child word of a leaf of `count` triangles from slot `first` reached with `acc` stack entries
+    // held above it; oversized leaves are split into piece nodes (recursively, 4 ways)
+    std::function<int(const float*, uint32_t, uint32_t, uint32_t, uint32_t&)> leaf_word =
+        [&](const float* box, uint32_t count, uint32_t first, uint32_t acc, uint32_t& word) -> int {
+        if (first > kNode4MaxFirst) return set_error(CERES_EUNSUPPORTED, "shadow BVH4: leaf slot %u at or above 2^27", first);
+        if (count <= kNode4MaxCount) { word = node4_child(count, first); return CERES_OK; }
+        if (out.size() > kNode4MaxFirst) return set_error(CERES_EUNSUPPORTED, "shadow BVH4: more than 2^27 records");
+        const uint32_t idx = uint32_t(out.size());
+        out.emplace_back();
+        const uint32_t parts = count <= 4 * kNode4MaxCount ? (count + kNode4MaxCount - 1) / kNode4MaxCount : 4;
+        const uint32_t per = (count + parts - 1) / parts;
+        const uint32_t inner = count <= 4 * kNode4MaxCount ? 0 : parts;      // pieces that are piece nodes again
+        const uint32_t acc2 = acc + (inner > 1 ? inner - 1 : 0);
+        stack_bound = std::max(stack_bound, acc2);
+        Node4 rec{};
+        for (uint32_t c = 0; c < 4; ++c) {
+            const uint32_t lo = c * per, n = c < parts && lo < count ? std::min(per, count - lo) : 0;
+            if (!n) { rec.child[c] = kNode4Empty; continue; }
+            set_box(rec, int(c), box);
+            uint32_t w = 0;
+            if (int rc = leaf_word(box, n, first + lo, acc2, w)) return rc;
+            rec.child[c] = w;
+        }
+        out[idx] = rec;
+        word = node4_child(0, idx);
+        return CERES_OK;
+    };
     struct Item { uint32_t pair, node4, acc; };
     std::vector<Item> st;
     out.emplace_back();
@@ -563,20 +601,17 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
             }
         }
         int inner = 0;
-        for (int c = 0; c < n; ++c) inner += ents[c].count == 0;
+        for (int c = 0; c < n; ++c) inner += ents[c].count == 0 || ents[c].count > kNode4MaxCount;   // piece nodes are inner
         const uint32_t acc = it.acc + uint32_t(std::max(0, inner - 1));
         stack_bound = std::max(stack_bound, acc);
         Node4 rec{};
         for (int c = 0; c < 4; ++c) {
             if (c >= n) { rec.child[c] = kNode4Empty; continue; }
-            rec.lo_x[c] = ents[c].box[0]; rec.hi_x[c] = ents[c].box[1];
-            rec.lo_y[c] = ents[c].box[2]; rec.hi_y[c] = ents[c].box[3];
-            rec.lo_z[c] = ents[c].box[4]; rec.hi_z[c] = ents[c].box[5];
+            set_box(rec, c, ents[c].box);
             if (ents[c].count) {
-                if (ents[c].count > kNode4MaxCount || ents[c].first > kNode4MaxFirst)
-                    return set_error(CERES_EUNSUPPORTED, "shadow BVH4: leaf of %u triangles at slot %u (at most %u "
-                                     "triangles per leaf, slots below 2^27)", ents[c].count, ents[c].first, kNode4MaxCount);
-                rec.child[c] = node4_child(ents[c].count, ents[c].first);
+                uint32_t w = 0;
+                if (int rc = leaf_word(ents[c].box, ents[c].count, ents[c].first, acc, w)) return rc;
+                rec.child[c] = w;
             } else {
                 if (out.size() > pairs.size() || ents[c].first >= pairs.size())   // a tree has fewer records than pairs
                     return set_error(CERES_EINVAL, "build_shadow_bvh4: sibling pairs do not form a tree");

@@ -10,7 +10,7 @@
 #include "ceres_types.hpp"
 
 using ceres::SiblingPair; using ceres::SiblingPair64; using ceres::Node4; using ceres::Tri48; using ceres::Tri96;
-using ceres::Shard; using ceres::ShadowJob;
+using ceres::Shard;
 
 struct ceres_scene {
     int device = 0;
@@ -24,11 +24,12 @@ struct ceres_scene {
     // fused-kernel tile orders, one per (frame size, tiling, batch, tile), never rewritten or
     // freed while a launch that reads them may be in flight (launches on different streams may
     // read different orders concurrently): an evicted order's buffer goes to `retired` and is
-    // freed only once retired buffers exceed kRetiredBytes, after one device synchronise -- no
+    // freed only once retired buffers exceed kRetiredBytes (counted at the allocation granule) or
+    // number kMaxRetired, after one device synchronise -- no
     // per-launch events, and no stall while the working set of shapes fits the cache.
     struct TileOrder {
         size_t W = 0, H = 0;
-        uint32_t row_block = 0, rank = 0, world = 0, frames = 0, tile = 0, cluster = 1;
+        uint32_t row_block = 0, rank = 0, world = 0, frames = 0, tile = 0;
         uint32_t* d = nullptr;
         size_t cap = 0;                // entries allocated at d
         uint64_t used = 0;
@@ -43,8 +44,6 @@ struct ceres_scene {
     Shard* d_shards = nullptr;
     bool shards_dirty = true;          // shards not known to be zero (see ceres_render_batch)
     uint64_t* d_counters = nullptr;
-    ShadowJob* d_jobs = nullptr;
-    size_t jobs_cap = 0;
     float* d_pixels = nullptr;
     uint8_t* d_rgb8 = nullptr;
     size_t px_cap = 0;
@@ -52,11 +51,10 @@ struct ceres_scene {
     int num_cus = 256;
     unsigned long long* d_wave_log = nullptr;   // stats scenes: per-wave diagnostic records
     size_t wave_log_waves = 0, last_grid_waves = 0;
-    // optional per-kernel device timing (bench.py roofline leg)
+    // optional per-launch device timing (ceres_scene_set_timing)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
-    std::vector<hipEvent_t> ev_used;   // triples: start, after primary, after shadow
-    std::vector<char> ev_fused;        // per triple: one ceres_fused launch (no separate shadow kernel)
+    std::vector<hipEvent_t> ev_used;   // pairs: before and after the render's kernel
     // double-precision scene (render<double>, render64.hip): set instead of the float layout
     bool f64 = false;
     SiblingPair64* d_pairs64 = nullptr;
@@ -69,5 +67,10 @@ void scene_release(ceres_scene* s);          // frees every device buffer and th
 // centre-first, XCD-balanced order of one whole frame's tile x tile tiles (render_hip.hip)
 int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out);
 constexpr size_t kMaxTileOrders = 16;         // cached orders per scene before LRU eviction
-constexpr size_t kRetiredBytes = 64u << 20;   // evicted orders kept until they exceed this
+#ifndef CERES_RETIRED_BYTES
+#define CERES_RETIRED_BYTES (64u << 20)
+#endif
+constexpr size_t kRetiredBytes = CERES_RETIRED_BYTES;   // evicted orders kept until they exceed this ...
+constexpr size_t kMaxRetired = 64;                      // ... or number this many buffers
+constexpr size_t kAllocGranule = 4096;                  // bytes of a retired buffer counted per started granule
 }

@@ -143,8 +143,10 @@ int ceres_orbit_cameras_f64(const double eye[3], const double dir[3], const doub
  * may be freed after the call.  Returns NULL on failure (see ceres_last_error).
  * Replaces the (bvh, triangles, tri_norms) arguments of render() (render.hpp:87-88).
  * Limits (CERES_EUNSUPPORTED): below 2^32 triangles and nodes; the shadow-ray BVH4 packs each
- * child in one word, so leaves hold at most 31 triangles (BinnedSahBuilder's hold at most 16)
- * and triangle slots / BVH4 records stay below 2^27. */
+ * child in one word, so triangle slots / BVH4 records stay below 2^27.  Leaves of any size are
+ * accepted: BinnedSahBuilder leaves hold up to 16 triangles, but a node whose centroids cannot be
+ * split (coincident triangles, the depth cap) stays one bigger leaf; the shadow BVH4 stores a
+ * leaf of more than 31 triangles as a node of equal-box pieces. */
 ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* norm36,
                                 const void* nodes32, size_t n_nodes, const uint64_t* prim64,
                                 int device, uint32_t flags);
@@ -235,17 +237,18 @@ int ceres_render_records_f64(ceres_scene* scene, const double basis12[12], const
                              size_t width, size_t height, int32_t* prim, double* tuv, int8_t* shadow,
                              ceres_stats* stats);
 
-/* Per-kernel device timing (bench.py roofline leg): while enabled, every render records HIP
- * events around ceres_primary and ceres_shadow on the stream it was launched on.
- * ceres_scene_read_timing synchronises, returns the summed durations (ms) and the number of
- * renders since the last read, and resets. */
+/* Per-launch device timing: while enabled, every render records HIP events around its one
+ * kernel (ceres_fused, or ceres_primary in primary-only mode) on the stream it was launched on.
+ * ceres_scene_read_timing synchronises, returns the summed kernel durations (ms; shadow_ms is
+ * always 0: primary and shadow rays run in the same kernel) and the number of renders since the
+ * last read, and resets. */
 int ceres_scene_set_timing(ceres_scene* scene, int enable);
-int ceres_scene_read_timing(ceres_scene* scene, double* primary_ms, double* shadow_ms, uint64_t* renders);
+int ceres_scene_read_timing(ceres_scene* scene, double* kernel_ms, double* shadow_ms, uint64_t* renders);
 
-/* Diagnostic: per-wavefront records of the last persistent-kernel render of a
- * CERES_SCENE_STATS scene, 8 x u64 each: {start, end (s_memrealtime, 100 MHz), chunks fetched,
- * full shadow batches, shader clocks spent fetching, node pairs, xcc_id << 32 | hw_id,
- * shadow rays traced}.  Synchronises the device. */
+/* Diagnostic: per-wavefront records of the last full-mode render of a CERES_SCENE_STATS scene
+ * (one 8x8 tile per wavefront), 8 x u64 each: {start, after the primary rays, end
+ * (s_memrealtime, 100 MHz), longest primary chain (node pairs), shadow-loop trips, primary hits,
+ * the wavefront's primary node pairs, its shadow node pairs}.  Synchronises the device. */
 int ceres_scene_wave_log(ceres_scene* scene, uint64_t* out, size_t max_waves, size_t* n_waves);
 
 /* Launch-geometry introspection for the roofline accounting in bench.py (kernel names as

@@ -82,7 +82,7 @@ def test_frame_matches_reference(gpu, name):
 
 
 @pytest.mark.parametrize("name", ["bunny_640", "dragon_640", "proc_101", "dragon_333x217", "bunny_97x61_primary",
-                                  "tri1", "quad", "degenerate", "dragon_1080", "dragon_orbit3_333x217"])
+                                  "tri1", "quad", "degenerate", "dragon_1080", "dragon_orbit3_333x217", "dupleaf"])
 def test_hit_records_match_reference(gpu, name):
     """prim / t / u / v / shadow per pixel, bit-exact vs the reference records (all pixels when small)."""
     pkg = gpu

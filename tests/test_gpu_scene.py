@@ -52,7 +52,7 @@ def device_scene(pkg, d_tri, n, d_norm):
 
 
 @pytest.mark.parametrize("name", ["dragon_1080", "bunny_640", "bunny_1080_primary", "degenerate", "tri1", "quad",
-                                  "proc_101", "dragon_orbit3_333x217", "dragon_4096"])
+                                  "proc_101", "dragon_orbit3_333x217", "dragon_4096", "dupleaf"])
 def test_device_scene_renders_reference_frame(gpu, name):
     import torch
     pkg = gpu
