@@ -5,10 +5,13 @@ Workload (default): C3 = dragon.obj 1920x1080, primary + shadow rays, static.cpp
 (static.cpp:38-47,72-73) -- the configuration BASELINE.json's metric is quoted on.
 
 A step renders F frames (F = --frames, default = 16 per GPU): views of the anim.cpp:76-88 orbit
-of the C3 camera + sun about z, frame 0 = C3 exactly.  At N = 1 a step is sixteen C3-size frames
-(the full orbit in 22.5-degree steps); at N GPUs it is 16N distinct frames over the same orbit,
-22.5/N degrees apart (step_views) -- WEAK scaling, sixteen frames' work per GPU from the same
-orbit at every N (one batch launch per 64 frames).
+of the C3 camera + sun about z, frame f rotated once by f x 360 / F degrees (frame 0 = C3
+exactly).  At N = 1 a step is sixteen C3-size frames 22.5 degrees apart; at N GPUs it is 16N
+distinct frames over the same turn, 22.5/N degrees apart (pkg.bench_views) -- WEAK scaling,
+sixteen frames' work per GPU from the same orbit at every N (one batch launch per 64 frames).
+Every one of those views has its reference PPM sha256 and rays/hits in
+tests/golden/orbit/<config>.json (made by the reference's own render(), make_golden.py --orbit),
+and every frame the validation step assembles is checked against it.
 Every frame's rows are interleaved over the ranks in blocks of --row-block rows (balanced
 load); each rank renders its rows of all F frames with one ceres_render_batch_device launch,
 RGB8 + float framebuffers in HBM, then ONE RCCL collective per step: by default each frame is
@@ -25,13 +28,20 @@ Scene upload, OBJ load and BVH build are outside the timed region, as in the ref
 Also reported (rank 0):
   roofline      dominant kernel's algorithmic bytes per launch (pinned reference statistics,
                 SURVEY.md §8(d): 64 B per node-pair visit + 56 B per triangle test) / its mean
-                device duration from HIP events around back-to-back launches on their stream, vs 8 TB/s HBM peak, for
-                one full C3 frame on one GPU; traffic = rocprofv3 --pmc FETCH_SIZE (gfx950 x2
-                correction) per launch from profiles/pmc_summary.json.
+                device duration from HIP events around back-to-back launches on their stream, for
+                one full frame on one GPU.  `bound` is chosen from the measured counters
+                (profiles/pmc_summary.json, rocprofv3 --pmc of the same solo launch): "hbm" when the
+                DRAM bytes are at least half the algorithmic bytes, else "l2" (the bytes are
+                served on-die; priced against the ~34.5 TB/s aggregate L2); `limiter` names what
+                the counters say stalls the kernel; `hbm_frac_algorithmic` keeps SURVEY §8(d)'s
+                algorithmic-bytes-vs-8-TB/s figure as a secondary field.
+  c3_only       the same timed loop with all F frames = the C3 view itself (the orbit mix is
+                lighter: fewer shadow rays per frame), value + shadow-ray fractions of both.
   cpu_baseline  the REFERENCE hot path (oracle/_ref/ref_render, reference CMake flags) timed
                 on this host's cores on a bounded sample of the same workload (N = 1 only);
                 falls back to the oracle restatement if the reference binary is absent.
-  parity        sha256 of frame 0's PPM vs the reference fixture, rays/hits vs the fixture.
+  parity        sha256 of frame 0's PPM vs the reference fixture, rays/hits vs the fixture, and
+                every assembled frame of the step vs the reference orbit fixtures.
 """
 import argparse
 import hashlib
@@ -77,26 +87,26 @@ def pinned_basis(meta, cfg, cam):
     return np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
 
 
-def step_views(pkg, cfg, meta, cam, F, V):
-    """Cameras (basis12 [F,12], sun3 [F,3]) of one bench step of F frames: V orbit views
-    (BENCH_ORBIT: v x 45 degrees about z, v = 0 is C3 with the fixture's basis bits) when F <= V;
-    for F = V N (N GPUs) the SAME arc sampled N times finer, frame f at f x 45 / N degrees.  So
-    every GPU's share of a step covers the same arc at every N (views differ in cost),
-    and all F views are distinct (near-copies of one view in one launch run slower:
-    tools/partition_probe.py)."""
-    W, H = cfg["W"], cfg["H"]
-    axis, step_deg = pkg.configs.BENCH_ORBIT
-    V = max(1, min(F, V))
-    b12, s3 = pkg.orbit_cameras(cam, cfg["sun"], W, H, V, axis=axis, step_deg=step_deg, rotate_first=False)
-    if F > V:
-        b12, s3 = np.zeros((F, 12), np.float32), np.zeros((F, 3), np.float32)
-        for f in range(1, F):
-            b, s = pkg.orbit_cameras(cam, cfg["sun"], W, H, 2, axis=axis, step_deg=f * float(step_deg) * V / F,
-                                     rotate_first=False)
-            b12[f], s3[f] = b[1], s[1]
-    b12[0] = pinned_basis(meta, cfg, cam)          # frame 0 = C3 (fixture bits)
-    s3[0] = np.asarray(cfg["sun"], np.float32)
+def step_views(pkg, cfg, meta, cam, F, V=None):
+    """Cameras (basis12 [F,12], sun3 [F,3]) of one bench step of F frames (pkg.bench_views: frame f
+    rotated once by f x 360 / F degrees about z, frame 0 = C3 with the fixture's basis bits).
+    `V` is accepted for older tools and ignored."""
+    b12, s3, _ = pkg.bench_views(cam, cfg["sun"], cfg["W"], cfg["H"], F, basis0=pinned_basis(meta, cfg, cam))
     return b12, s3
+
+
+def load_orbit_fixture(name):
+    """tests/golden/orbit/<name>.json: reference sha256 / rays / hits per orbit view, keyed by the
+    float32 step's hex bits (tests/golden/make_golden.py --orbit), or None."""
+    p = os.path.join(REPO, "tests", "golden", "orbit", name + ".json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)["by_step_bits"]
+
+
+def step_key(step):
+    return "%08x" % int(np.asarray(step, np.float32).view(np.uint32))
 
 
 def cpu_baseline(cfg_name, cfg, rays_per_frame, budget_s=3.0):
@@ -147,17 +157,63 @@ def _cpu_model():
     return "unknown"
 
 
-def pmc_traffic(cfg_name, kernel):
-    """Per-launch HBM bytes of `kernel` from a committed rocprofv3 --pmc summary, or None."""
+def pmc_entry(cfg_name, kernel):
+    """rocprofv3 --pmc summary of `kernel`'s solo launch for a config (profiles/pmc_summary.json,
+    tools/pmc_summary.py), or None."""
     p = os.path.join(REPO, "profiles", "pmc_summary.json")
     if not os.path.exists(p):
         return None
     try:
-        d = json.load(open(p))
-        e = d.get(cfg_name, {}).get(kernel)
-        return None if e is None else e.get("hbm_bytes_per_launch")
+        with open(p) as f:
+            return json.load(f).get(cfg_name, {}).get(kernel)
     except Exception:  # noqa: BLE001
         return None
+
+
+def roofline_block(name, nbytes, ms, pmc, scene_bytes):
+    """The roofline object for the dominant kernel (one launch = one frame).
+
+    achieved = ALGORITHMIC bytes per launch / the launch's mean duration.  The
+    bound is picked from the measured counters: DRAM bytes (FETCH_SIZE x2 + WRITE_SIZE, the gfx950
+    correction) per launch >= half the algorithmic bytes -> "hbm" (8 TB/s); otherwise the bytes
+    are served on-die and the ceiling they are priced against is the aggregate L2 (~34.5 TB/s,
+    MI355X_MICROARCH.md §L2) -- an upper bound on L2 use, since L1 / scalar-cache hits count
+    too.  `limiter` reads the counters: wave cycles parked on s_waitcnt, TA busy, and whether the
+    L2 fabric reads exceed the scene (the scene streams from MALL/DRAM) or not."""
+    achieved = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    traffic = None if pmc is None else pmc.get("hbm_bytes_per_launch")
+    dram_gbs = traffic / (ms * 1e-3) / 1e9 if traffic and ms > 0 else None
+    bound = "hbm" if traffic and traffic >= 0.5 * nbytes else "l2"
+    peak = HBM_PEAK_GBS if bound == "hbm" else L2_PEAK_GBS
+    out = {"bound": bound, "kernel": name, "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
+           "frac": round(achieved / peak, 4), "traffic": traffic,
+           "algorithmic_bytes_per_launch": nbytes, "mean_launch_ms": round(ms, 5),
+           "hbm_frac_algorithmic": round(achieved / HBM_PEAK_GBS, 4),
+           "dram_gbs": None if dram_gbs is None else round(dram_gbs, 1),
+           "dram_frac": None if dram_gbs is None else round(dram_gbs / HBM_PEAK_GBS, 4),
+           "scene_device_bytes": scene_bytes}
+    if pmc is None:
+        out["limiter"] = "unmeasured (no rocprofv3 --pmc summary for this config)"
+        return out
+    wait = pmc.get("waitcnt_parked_frac")
+    ta = pmc.get("ta_busy_frac")
+    rd = pmc.get("hbm_read_bytes_per_launch")
+    out.update({k: pmc.get(k) for k in ("waitcnt_parked_frac", "issue_stall_frac", "ta_busy_frac", "td_busy_frac",
+                                        "l2_hit_rate", "valu_lane_utilisation", "hbm_read_bytes_per_launch",
+                                        "hbm_write_bytes_per_launch") if pmc.get(k) is not None})
+    out["pmc_source"] = "profiles/pmc_summary.json (rocprofv3 --pmc, solo launches of this config)"
+    if bound == "hbm" and dram_gbs and dram_gbs >= 0.5 * HBM_PEAK_GBS:
+        lim = "HBM bandwidth"
+    elif wait is not None and wait >= 0.45:
+        where = "MALL/DRAM" if rd and scene_bytes and rd >= scene_bytes else "L2"
+        lim = f"{where} latency of dependent loads (waves parked on s_waitcnt {wait:.2f} of cycles"
+        lim += f", fabric reads {rd / 1e6:.0f} MB/launch vs scene {scene_bytes / 1e6:.0f} MB)" if rd and scene_bytes else ")"
+    elif ta is not None and ta >= 0.5:
+        lim = f"vector-memory issue (TA busy {ta:.2f}) + dependent L2 latency (s_waitcnt {wait:.2f})"
+    else:
+        lim = "dependent-load latency" + (f" (s_waitcnt {wait:.2f})" if wait is not None else "")
+    out["limiter"] = lim
+    return out
 
 
 def main():
@@ -173,6 +229,8 @@ def main():
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-view0-only", action="store_true",
+                    help="skip the second timed loop with every frame = frame 0's view (C3 itself)")
     ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
     ap.add_argument("--collect", choices=("exchange", "gather"), default="exchange",
                     help="N > 1: every frame of a step to one owner rank in one all-to-all (exchange; frames a "
@@ -190,6 +248,7 @@ def main():
     import ceres_raytracer_amd.distributed as D
     cfg = pkg.configs.CONFIGS[args.config]
     meta = load_golden(args.config)
+    orbit_fx = load_orbit_fixture(args.config)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -215,17 +274,14 @@ def main():
     F = args.frames or args.frames_per_gpu * world
     mesh, bvh, cam = pkg.prepare(cfg)
     scene = pkg.Scene(mesh, bvh, device=local_rank)
-    # explicit --frames: F distinct orbit views spread over the ranks; default: --frames-per-gpu views
-    # the orbit is 8 views 45 degrees apart (BENCH_ORBIT, a full turn); a step of F frames samples
-    # it F / 8 times finer (frame f at f x 360 / F degrees), at every N
-    b12, s3 = step_views(pkg, cfg, meta, cam, F, max(1, F // world) if args.frames else min(8, F))
+    # F views of the orbit, frame f rotated once by f x 360 / F degrees (frame 0 = C3, fixture bits)
+    b12, s3, steps_deg = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=pinned_basis(meta, cfg, cam))
     exchange = world > 1 and args.collect == "exchange" and F % world == 0
     if exchange:
         # batch order for the all-to-all: rank q owns batch frames q*k .. q*k+k-1, which are orbit
         # frames q, q + N, q + 2N, ... (batch frame 0 = orbit frame 0 = C3)
-        k = F // world
-        order = np.asarray([m * world + q for q in range(world) for m in range(k)])
-        b12, s3 = b12[order], s3[order]
+        order = D.exchange_order(F, world)
+        b12, s3, steps_deg = b12[order], s3[order], steps_deg[order]
     mode = pkg.cfg_mode(cfg)
     row_block = args.row_block if world > 1 else H
     tiling = pkg.Tiling(row_block, rank, world)
@@ -249,14 +305,16 @@ def main():
 
     MAXF = 64                                    # frames per ceres_render_batch_device launch (kMaxFrames)
     chunk_counters = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range((F + MAXF - 1) // MAXF)]
+    views = {"b12": b12, "s3": s3, "steps": steps_deg}      # what every step renders
 
     def render(slot, st, with_counters=False):
         # one launch per (at most) 64 frames of the step; frame f's rows at f * 3 * W * rows
         px = d_px[slot % S]
         fb = 3 * W * max(rows, 1)
+        vb, vs = views["b12"], views["s3"]
         for c, f0 in enumerate(range(0, F, MAXF)):
             f1 = min(F, f0 + MAXF)
-            scene.render_batch_device(b12[f0:f1], s3[f0:f1], W, H, mode=mode, tiling=tiling,
+            scene.render_batch_device(vb[f0:f1], vs[f0:f1], W, H, mode=mode, tiling=tiling,
                                       d_pixels=0 if px is None else px.data_ptr() + 4 * fb * f0,
                                       d_rgb8=gather.local_ptr(slot) + fb * f0,
                                       d_counters=chunk_counters[c].data_ptr() if with_counters else 0,
@@ -290,98 +348,129 @@ def main():
                 pending[k_] = False
         gather.wait_assembled()
 
-    # validation step (not timed): exact counts of the F-frame batch + frame-0 PPM parity on rank 0
-    render(0, stream, with_counters=True)
-    gather.start(0)
-    full = gather.finish(0)
-    gather.wait_assembled()
-    torch.cuda.synchronize(dev)
-    c = counters.clone()
-    if world > 1:
-        dist.all_reduce(c)
-    c = c.cpu().numpy()
-    if c[6]:
-        # ceres_finalize's error word: a traversal stack overflowed (single_ray_traverser.hpp:29
-        # asserts instead), so some frame of the batch is wrong -- never time a wrong render
-        sys.stderr.write(f"bench.py: traversal stack overflow in the validation batch (error word {int(c[6]):#x})\n")
-        return 3
-    rays_step, hits_step = int(c[0]), int(c[1])
-    parity = None
-    if rank == 0:
-        body = b"P6 %d %d 255\n" % (W, H) + full[0].cpu().numpy().tobytes()
-        sha = hashlib.sha256(body).hexdigest()
-        if meta is not None:
-            parity = {"frame0_ppm_sha256_matches_reference": sha == meta["ppm_sha256"]["exact"]}
-            # frame 0's ray / hit counts (render.hpp:155) from a counted whole-frame render
-            c0 = torch.zeros(8, dtype=torch.int64, device=dev)
-            scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=pkg.Tiling(H, 0, 1),
-                                d_counters=c0.data_ptr(), stream=sh)
-            torch.cuda.synchronize(dev)
-            c0 = c0.cpu().numpy()
-            parity.update(rays_match=int(c0[0]) == meta["exact"]["rays"], hits_match=int(c0[1]) == meta["exact"]["hits"])
-    if True:  # placeholder-free: see below
-        # every assembled frame (this rank's k frames with the exchange, all F on rank 0 with
-        # the gather or at N = 1) == the same frame rendered whole, alone, on this GPU.  Every
-        # timed step renders these same F views, so with the stack-overflow check above this
-        # validates what the timed steps compute (the render is deterministic).
+    def validate():
+        """Untimed: one counted step of the current views.  Returns (rays, hits, checks) where checks
+        compares every frame this rank assembled with the REFERENCE's PPM of the same view
+        (tests/golden/orbit/<config>.json; sha256 of "P6 W H 255\n" + body, static.cpp:135-147)
+        and the step's rays / hits with the reference's per-view counts (render.hpp:155)."""
+        render(0, stream, with_counters=True)
+        gather.start(0)
+        full = gather.finish(0)
+        gather.wait_assembled()
+        torch.cuda.synchronize(dev)
+        c = counters.clone()
+        if world > 1:
+            dist.all_reduce(c)
+        c = c.cpu().numpy()
+        if c[6]:
+            # ceres_finalize's error word: a traversal stack overflowed (single_ray_traverser.hpp:29
+            # asserts instead), so some frame of the batch is wrong -- never time a wrong render
+            raise SystemExit(f"bench.py: traversal stack overflow in the validation batch (error word {int(c[6]):#x})")
         mine = (list(zip(gather.owned_frames(), full)) if exchange
                 else ([(f, full[f]) for f in range(F)] if rank == 0 else []))
-        solo_rgb = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
-        same = True
+        head = b"P6 %d %d 255\n" % (W, H)
+        n = [0, 0, 0]                                            # [checked, matched, unpinned]
         for f, body in mine:
-            scene.render_device(b12[f], s3[f], W, H, mode=mode, tiling=pkg.Tiling(H, 0, 1),
-                                d_rgb8=solo_rgb.data_ptr(), stream=sh)
-            torch.cuda.synchronize(dev)
-            same &= bool(torch.equal(solo_rgb.view(H, 3 * W), body))
-        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=dev)
+            e = None if orbit_fx is None else orbit_fx.get(step_key(views["steps"][f]))
+            if e is None:
+                n[2] += 1
+                continue
+            n[0] += 1
+            n[1] += int(hashlib.sha256(head + body.cpu().numpy().tobytes()).hexdigest() == e["sha256"])
+        stat = torch.tensor(n, dtype=torch.int64, device=dev)
         if world > 1:
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if rank == 0 and parity is not None:
-            parity["all_frames_match_one_gpu_render"] = bool(flag.item())
+            dist.all_reduce(stat)
+        stat = stat.cpu().numpy()
+        keys = [None if orbit_fx is None else orbit_fx.get(step_key(x)) for x in views["steps"]]
+        ref_rays = sum(e["rays"] for e in keys) if all(keys) else None
+        ref_hits = sum(e["hits"] for e in keys) if all(keys) else None
+        checks = {"frames": F, "frames_checked": int(stat[0]), "frames_unpinned": int(stat[2]),
+                  "all_frames_match_reference": bool(stat[2] == 0 and stat[1] == stat[0] == F),
+                  "step_rays_match_reference": None if ref_rays is None else int(c[0]) == ref_rays,
+                  "step_hits_match_reference": None if ref_hits is None else int(c[1]) == ref_hits}
+        return int(c[0]), int(c[1]), checks
 
-    # setup (untimed, before the W warmup steps): steps over every stream and collective slot for
-    # at least --prime-s seconds, so no stream's first launch lands in the timed region when
-    # W < S and the GPU has left its idle clock state (measured: K = 20 after W = 5 from a cold
-    # start ran 6 % below the same K after W = 200; after this priming they agree)
-    t_prime = time.perf_counter()
-    for k in range(slots):
-        step(k)
-    drain()
-    torch.cuda.synchronize(dev)
-    per_step = max((time.perf_counter() - t_prime) / slots, 1e-5)
-    # the same number of steps on every rank (each step is a collective)
-    more = torch.tensor([min(20000, max(0, int(args.prime_s / per_step) - slots))], dtype=torch.int64, device=dev)
-    if world > 1:
-        dist.all_reduce(more, op=dist.ReduceOp.MAX)
-    for k in range(int(more.item())):
-        step(slots + k)
-    drain()
-    torch.cuda.synchronize(dev)
-    for k in range(args.warmup):
-        step(k)
-    drain()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    drain()
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    T = float(elapsed.item())
+    def timed(prime):
+        """W warmup steps (after >= --prime-s of untimed steps when `prime`), then exactly K steps
+        between barrier + device synchronise; returns the max-over-ranks wall time."""
+        if prime:
+            # untimed setup before the W warmup steps: steps over every stream and collective slot
+            # for at least --prime-s seconds, so no stream's first launch lands in the timed region
+            # when W < S and the GPU has left its idle clock state (measured: K = 20 after W = 5
+            # from a cold start ran 6 % below the same K after W = 200; after this priming they agree)
+            t_prime = time.perf_counter()
+            for k in range(slots):
+                step(k)
+            drain()
+            torch.cuda.synchronize(dev)
+            per_step = max((time.perf_counter() - t_prime) / slots, 1e-5)
+            # the same number of steps on every rank (each step is a collective)
+            more = torch.tensor([min(20000, max(0, int(args.prime_s / per_step) - slots))], dtype=torch.int64,
+                                device=dev)
+            if world > 1:
+                dist.all_reduce(more, op=dist.ReduceOp.MAX)
+            for k in range(int(more.item())):
+                step(slots + k)
+            drain()
+            torch.cuda.synchronize(dev)
+        for k in range(args.warmup):
+            step(k)
+        drain()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(k)
+        drain()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        return float(elapsed.item())
+
+    # validation step of the orbit views (not timed): exact counts + every frame vs the reference
+    rays_step, hits_step, orbit_checks = validate()
+    parity = None
+    if rank == 0 and meta is not None:
+        parity = {}
+        # frame 0's ray / hit counts (render.hpp:155) from a counted whole-frame render
+        c0 = torch.zeros(8, dtype=torch.int64, device=dev)
+        rgb0 = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
+        scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=pkg.Tiling(H, 0, 1), d_rgb8=rgb0.data_ptr(),
+                            d_counters=c0.data_ptr(), stream=sh)
+        torch.cuda.synchronize(dev)
+        c0 = c0.cpu().numpy()
+        body = b"P6 %d %d 255\n" % (W, H) + rgb0.view(H, 3 * W).cpu().numpy().tobytes()
+        parity.update(frame0_ppm_sha256_matches_reference=hashlib.sha256(body).hexdigest() == meta["ppm_sha256"]["exact"],
+                      rays_match=int(c0[0]) == meta["exact"]["rays"], hits_match=int(c0[1]) == meta["exact"]["hits"])
+    if parity is not None:
+        parity.update(orbit_checks)
+
+    T = timed(prime=True)
     value = rays_step * args.steps / T / 1e6
+    primary_step = F * W * H
+    view0 = None
+    if not args.no_view0_only:
+        # the same loop with every frame = frame 0's view (C3 itself for dragon_1080): the orbit mix
+        # has fewer shadow rays per frame than C3, so report both
+        views.update(b12=np.repeat(b12[:1], F, 0), s3=np.repeat(s3[:1], F, 0),
+                     steps=np.repeat(steps_deg[:1], F))
+        rays0, hits0, checks0 = validate()
+        T0 = timed(prime=False)
+        view0 = {"value": round(rays0 * args.steps / T0 / 1e6, 3), "unit": "Mrays/s",
+                 "ms_per_step": round(T0 / args.steps * 1e3, 5), "rays_per_step": rays0, "hits_per_step": hits0,
+                 "shadow_ray_frac": round((rays0 - primary_step) / rays0, 4) if mode == pkg.MODE_FULL else 0.0,
+                 "parity": checks0}
 
     roofline = None
     cpu = None
     if rank == 0 and not args.no_roofline and meta is not None:
-        # dominant kernel, timed live with HIP events on the launch stream (one full C3 frame, this GPU)
+        # dominant kernel, timed live with HIP events on the launch stream (one full frame, this GPU)
         solo = pkg.Tiling(H, 0, 1)
         solo_rgb = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
         solo_px = torch.empty(3 * W * H, dtype=torch.float32, device=dev)
@@ -403,30 +492,8 @@ def main():
         b_p = 64 * ex["primary_pairs"] + 56 * ex["primary_tests"]
         b_s = 64 * ex["shadow_pairs"] + 56 * ex["shadow_tests"]
         # one kernel per frame: ceres_fused (primary + shadow + shading) or ceres_primary (primary only)
-        kern = {"ceres_fused": (mean_ms, b_p + b_s)} if mode == pkg.MODE_FULL else {"ceres_primary": (mean_ms, b_p)}
-        name = max(kern, key=lambda k: kern[k][0])
-        ms, nbytes = kern[name]
-        achieved = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        frame_bytes = sum(v[1] for v in kern.values())
-        frame_ms = sum(v[0] for v in kern.values())
-        traffic = pmc_traffic(args.config, name)
-        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": traffic,
-                    # `frac` prices ALGORITHMIC bytes (the contract's roofline); what actually limits the
-                    # kernel is stated here: DRAM bytes measured by rocprofv3 PMC over the same launch
-                    # time against the same peak, and the limiter DESIGN.md derives from the PMC + wave
-                    # timeline (scene cache-resident -> dependent-load latency, not HBM bandwidth)
-                    "dram_frac": None if not traffic or ms <= 0 else round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "limiter": "latency (dependent L2 loads; scene cache-resident)"
-                    if traffic and traffic < 0.25 * nbytes else "hbm",
-                    "algorithmic_bytes_per_launch": nbytes, "mean_launch_ms": round(ms, 5),
-                    "kernels_ms": {k: round(v[0], 5) for k, v in kern.items()},
-                    "frame_algorithmic_bytes": frame_bytes,
-                    "frame_frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                    # a scene that fits the XCD L2s (dragon 3.8 MB, bunny 0.8 MB) is served from L2, not HBM
-                    # (traffic << algorithmic bytes): the same bytes against the L2 ceiling
-                    "l2_peak": L2_PEAK_GBS, "l2_frac": round(achieved / L2_PEAK_GBS, 4)}
+        name, nbytes = ("ceres_fused", b_p + b_s) if mode == pkg.MODE_FULL else ("ceres_primary", b_p)
+        roofline = roofline_block(name, nbytes, mean_ms, pmc_entry(args.config, name), scene.info()["device_bytes"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, cfg, rays_step if F == 1 else meta["exact"]["rays"])
 
@@ -437,18 +504,25 @@ def main():
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(T / args.steps * 1e3, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "real mesh from the reference repo (data/%s); frame 0 = static.cpp camera, frames 1.. = "
-                    "anim.cpp-style orbit about z" % (cfg["obj"] or "procedural"),
+            "data": ("real mesh from the reference repo (data/%s)" % cfg["obj"] if cfg["obj"] else
+                     "procedural %dx%d-vertex heightfield generated in-process (SURVEY.md §8(d) C5 definition)"
+                     % (cfg["proc"], cfg["proc"]))
+                    + "; frame 0 = the config camera, frames 1.. = the anim.cpp-style orbit about z",
             "config": {"workload": f"{args.config}: {cfg['obj'] or 'proc'} {W}x{H} "
                                    f"{'primary+shadow' if mode == pkg.MODE_FULL else 'primary only'}, "
                                    f"{F} orbit frame(s) per step",
                        "W": W, "H": H, "frames_per_step": F, "rays_per_step": rays_step, "hits_per_step": hits_step,
+                       "shadow_ray_frac": round((rays_step - primary_step) / rays_step, 4)
+                       if mode == pkg.MODE_FULL else 0.0,
                        "row_block": row_block, "parallelism": f"row-interleaved frames x{world}"
                        + ((" + one RCCL all-to-all per step: frame f gathered to rank f (pipelined)" if exchange
                            else " + one RCCL gather per step to rank 0 (pipelined)") if world > 1 else ""),
                        "float_framebuffer": d_px[0] is not None, "streams": S},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
         }
+        if view0 is not None:
+            line["c3_only_value" if args.config == "dragon_1080" else "view0_only_value"] = view0["value"]
+            line["view0_only"] = view0
         print(json.dumps(line), flush=True)
     scene.close()
     if world > 1:

@@ -474,6 +474,25 @@ def orbit_cameras(camera, sun, W, H, n_frames, axis=(0, 1, 0), step_deg=None, ro
     return (b, s3, d3) if want_dirs else (b, s3)
 
 
+def bench_views(camera, sun, W, H, F, basis0=None):
+    """The F views of one bench.py step: frame f = the camera + sun rotated once by
+    configs.orbit_step(f, F) degrees about configs.BENCH_AXIS (anim.cpp:76-88, Transform::rotate
+    transform.hpp:67-112); frame 0 unrotated, with `basis0` (the fixture's pinned basis12) when
+    given.  Returns (basis12 [F,12] f32, sun3 [F,3] f32, step_deg [F] f32); the reference PPM of
+    every such view is pinned in tests/golden/orbit/<cfg>.json by its step bits."""
+    F = int(F)
+    b12 = np.zeros((F, 12), np.float32)
+    s3 = np.zeros((F, 3), np.float32)
+    steps = np.asarray([configs.orbit_step(f, F) for f in range(F)], np.float32)
+    b12[0] = camera.basis(W, H) if basis0 is None else np.asarray(basis0, np.float32)
+    s3[0] = np.asarray(sun, np.float32)
+    for f in range(1, F):
+        b, s = orbit_cameras(camera, sun, W, H, 2, axis=configs.BENCH_AXIS, step_deg=float(steps[f]),
+                             rotate_first=False)
+        b12[f], s3[f] = b[1], s[1]
+    return b12, s3, steps
+
+
 def pose(cfg, frame=0):
     """(Camera, sun) of a config: configs with "orbit": (axis, step_deg, count) are the anim.cpp
     orbit pose after count + frame rotations; otherwise the config's camera rotated `frame`

@@ -78,8 +78,20 @@ CONFIGS = {
     "dragon_1080_robust": _cfg(_DRAGON, W=1920, H=1080, robust=True),
 }
 
-# bench.py weak scaling: frame k of a step is the C3 pose rotated k times by 45 degrees about z
+# pose(cfg, frame) / tests: the config pose rotated `frame` times by 45 degrees about z
 BENCH_ORBIT = ((0.0, 0.0, 1.0), 45.0)
+# bench.py: frame f of an F-frame step is the config pose rotated ONCE by orbit_step(f, F) degrees
+# about BENCH_AXIS (anim.cpp:76-88's Transform) -- F views over the full turn; every view of every
+# F = 16N (N = 1, 2, 4, 8) is among the 128 pinned by tests/golden/orbit/<cfg>.json
+BENCH_AXIS = (0.0, 0.0, 1.0)
+ORBIT_FIXTURE_VIEWS = 128
+
+
+def orbit_step(f, F):
+    """Float32 rotation (degrees) of frame f of an F-frame bench step: f x 360 / F, rounded once to
+    double then to float32 (so equal fractions f / F give identical bits)."""
+    import numpy as np
+    return np.float32(f * 360.0 / F)
 
 
 def obj_path(cfg):

@@ -228,7 +228,7 @@ int run(const Opts& o, const Num<S>& v) {
     std::vector<uint8_t> rgb(3 * o.W * o.H);
     ceres_stats st{};
     unsigned long long tot_rays = 0;
-    std::vector<double> ms;
+    std::vector<double> ms, e2e;
     for (int k = 0; k < o.frames; ++k) {
         const S* basis = bases.data() + 12 * size_t(o.orbit_count + k);
         const S* sun = suns.data() + 3 * size_t(o.orbit_count + k);
@@ -243,7 +243,9 @@ int run(const Opts& o, const Num<S>& v) {
         tot_rays += st.rays;
         for (int r = 0; r < o.bench; ++r) {
             ceres_stats s2{};
+            const double b1 = now_s();
             rc = render(basis, sun, rgb.data(), &s2);
+            e2e.push_back((now_s() - b1) * 1e3);          // the whole call: launch + kernel + RGB8 copy to the host
             if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); destroy(); return 1; }
             ms.push_back(s2.ms);
         }
@@ -268,12 +270,13 @@ int run(const Opts& o, const Num<S>& v) {
     }
     if (o.frames > 1) std::printf("Total Rays: %llu\n", tot_rays);   // anim.cpp:127
     if (o.json) {
-        double med = 0;
+        double med = 0, e2e_med = 0;
         if (!ms.empty()) { std::sort(ms.begin(), ms.end()); med = ms[ms.size() / 2]; }
+        if (!e2e.empty()) { std::sort(e2e.begin(), e2e.end()); e2e_med = e2e[e2e.size() / 2]; }
         std::printf("{\"rays\": %llu, \"hits\": %llu, \"W\": %zu, \"H\": %zu, \"device_ms\": %.4f, \"bench_median_ms\": %.4f, "
-                    "\"mrays_per_s\": %.3f}\n",
+                    "\"mrays_per_s\": %.3f, \"e2e_ms\": %.4f}\n",
                     (unsigned long long)st.rays, (unsigned long long)st.hits, o.W, o.H, st.ms, med,
-                    med > 0 ? double(st.rays) / (med * 1e3) : 0.0);
+                    med > 0 ? double(st.rays) / (med * 1e3) : 0.0, e2e_med);
     }
     destroy();
     return 0;

@@ -28,6 +28,14 @@ def row_map(H, row_block, world):
     return out
 
 
+def exchange_order(frames, world):
+    """Batch order of an F-frame step for FrameExchange (F = k * world): batch frame q*k + m is
+    orbit frame m*world + q, so rank q owns the consecutive batch frames q*k .. q*k+k-1 (orbit
+    frames q, q + N, q + 2N, ...; batch frame 0 = orbit frame 0)."""
+    k = frames // world
+    return np.asarray([m * world + q for q in range(world) for m in range(k)], np.int64)
+
+
 def rank_rows(H, row_block, rank, world):
     """Closed form of len(row_map(...)[rank]) -- the formula ceres_assemble uses on the device."""
     nb = (H + row_block - 1) // row_block

@@ -20,6 +20,9 @@
 //                  overload (single_ray_traverser.hpp:132-135,161-163)
 //   --orbit ax ay az step count   apply anim.cpp:76-88's camera/sun Transform (transform.hpp)
 //                  `count` times before rendering (eye, dir, sun rotate; up does not)
+//   --orbit-views s1,s2,...   one render per listed step (degrees, applied once to the base
+//                  camera + sun about --orbit's axis): bench.py's timed orbit frames; with --out f
+//                  the PPMs are f.<k>.ppm and every view prints its own JSON line
 //   --dump p       write p.tri48 (rotated Triangle[]), p.norm36, p.nodes32, p.prim64
 //   --primary-only render.hpp:123-125 (commented-out normal visualisation) as the
 //                  primary-rays-only mode: pixel = |normalize(tri.n)|
@@ -77,6 +80,7 @@ struct Args {
     int proc = 0;  // >0: procedural heightfield with proc x proc vertices instead of an OBJ
     Vector3 orbit_axis{0.f, 1.f, 0.f};
     Scalar orbit_step = 0.f; int orbit_count = 0;   // --orbit: anim.cpp camera/sun rotations
+    std::vector<std::string> orbit_views;             // --orbit-views: one render per listed step_deg
 };
 
 static Vector3 v3(char** a) { return Vector3(num(a[0]), num(a[1]), num(a[2])); }
@@ -101,6 +105,8 @@ static bool parse(int argc, char** argv, Args& a) {
         else if (s == "--robust") a.robust = true;
         else if (s == "--primary-only") a.primary_only = true;
         else if (s == "--proc") { need(1); a.proc = std::atoi(argv[++i]); }
+        else if (s == "--orbit-views") { need(1); std::stringstream ss(argv[++i]); std::string t;
+                                          while (std::getline(ss, t, ',')) if (!t.empty()) a.orbit_views.push_back(t); }
         else if (s == "--orbit") { need(5); a.orbit_axis = v3(argv + i + 1); a.orbit_step = num(argv[i + 4]); a.orbit_count = std::atoi(argv[i + 5]); i += 5; }
         else if (s[0] == '-') { std::fprintf(stderr, "unknown flag %s\n", s.c_str()); return false; }
         else a.obj = s;
@@ -184,6 +190,17 @@ int main(int argc, char** argv) {
         wr(".prim64", pi.data(), pi.size() * 8);
     }
 
+    // --orbit-views s1,s2,...: one render per view, the base camera + sun rotated ONCE by s_k degrees
+    // about the orbit axis (bench.py's step_views frames); PPMs go to <out>.<k>.ppm, one JSON line each.
+    const Vector3 base_sun = a.sun;
+    const std::string base_out = a.out;
+    const size_t n_views = a.orbit_views.empty() ? 1 : a.orbit_views.size();
+    for (size_t view_k = 0; view_k < n_views; ++view_k) {
+    a.sun = base_sun;
+    if (!a.orbit_views.empty()) {
+        a.orbit_step = num(a.orbit_views[view_k].c_str()); a.orbit_count = 1;
+        if (!base_out.empty()) a.out = base_out + "." + std::to_string(view_k) + ".ppm";
+    }
     Camera<Scalar> camera{a.eye, a.dir, a.up, a.fov};
     if (a.orbit_count > 0) {
         // anim.cpp:76-88: the reference's own Transform applied orbit_count times
@@ -343,5 +360,7 @@ int main(int argc, char** argv) {
                     "\"primary_pairs\": %zu, \"primary_tests\": %zu, \"shadow_rays\": %zu, \"shadow_pairs\": %zu, \"shadow_tests\": %zu",
                     loop_rays, loop_hits, mismatch, prim_pairs, prim_tests, n_sh, sh_pairs, sh_tests);
     std::printf("}\n");
+    std::fflush(stdout);
+    }   // views
     return 0;
 }

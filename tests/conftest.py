@@ -51,6 +51,13 @@ def load_golden(name):
     return meta, rec, ppm
 
 
+def load_orbit(name):
+    """tests/golden/orbit/<name>.json (make_golden.py --orbit): the reference's PPM sha256 and
+    rays / hits of every bench orbit view, keyed by the float32 step's hex bits."""
+    with open(os.path.join(GOLDEN, "orbit", name + ".json")) as f:
+        return json.load(f)
+
+
 def hexbits(a):
     return ["0x%08x" % int(x) for x in np.asarray(a, np.float32).view(np.uint32)]
 

@@ -19,6 +19,7 @@ config in ceres-raytracer_amd/configs.py and commits only small artefacts:
 
 Must run in the build container (needs /root/reference); the GPU box only reads the outputs.
 Usage: python tests/golden/make_golden.py [cfg ...]
+       python tests/golden/make_golden.py --orbit cfg ...   (orbit/<cfg>.json: every bench view)
 """
 import gzip
 import hashlib
@@ -188,7 +189,55 @@ def add_scene_hashes(name):
     print(name, "scene hashes added", flush=True)
 
 
+ORBIT_VIEWS = 128          # bench.step_views: frame f of an F-frame step is ONE rotation by f x 360 / F degrees;
+                          # F = 16N frames at N = 1, 2, 4, 8 GPUs are all among k x 360 / 128, k = 0..127
+
+
+def orbit_step_deg(f, F):
+    """Float32 step (degrees) of frame f of an F-frame bench step -- the same expression as
+    bench.step_views (an exactly rounded double, then float32)."""
+    return np.float32(f * 360.0 / F)
+
+
+def make_orbit(name, views=ORBIT_VIEWS):
+    """Reference PPM sha256 + rays/hits (render.hpp:155) of every orbit view bench.py can time
+    for config `name` (anim.cpp:76-110: the camera and sun rotated about z by the reference's own
+    Transform, transform.hpp:67-112), from the contraction-free reference build.  Only hashes and
+    counts are stored: tests/golden/orbit/<name>.json, keyed by the float32 step's hex bits."""
+    cfg = configs.CONFIGS[name]
+    (ax, ay, az), _ = configs.BENCH_ORBIT
+    os.makedirs(SCRATCH, exist_ok=True)
+    os.makedirs(os.path.join(HERE, "orbit"), exist_ok=True)
+    steps = [orbit_step_deg(k, views) for k in range(views)]
+    out = os.path.join(SCRATCH, name + ".orbit")
+    cmd = ([REF_EXACT] + configs.cli_args(cfg) + ["--orbit", repr(ax), repr(ay), repr(az), "0", "0",
+           "--orbit-views", ",".join(repr(float(s)) for s in steps), "--out", out])
+    lines = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout.strip().splitlines()
+    assert len(lines) == views, (name, len(lines))
+    entries = {}
+    for k, (s, line) in enumerate(zip(steps, lines)):
+        j = json.loads(line)
+        ppm = out + ".%d.ppm" % k
+        key = "%08x" % int(np.asarray(s, np.float32).view(np.uint32))
+        entries[key] = {"k": k, "step_deg": float(s), "sha256": sha(ppm), "rays": j["rays"], "hits": j["hits"],
+                        "eye": j["eye"], "sun": j["sun"]}
+        os.remove(ppm)
+    meta = {"config": name, "axis": [ax, ay, az], "views": views,
+            "generator": "oracle/_ref/ref_render_exact --orbit-views via tests/golden/make_golden.py --orbit",
+            "rule": "view k = the config camera + sun rotated once by float32(k * 360 / views) degrees about "
+                    "axis (Transform::rotate, transform.hpp:67-112; anim.cpp:76-88); PPM as static.cpp:135-147",
+            "by_step_bits": entries}
+    with open(os.path.join(HERE, "orbit", name + ".json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+        f.write("\n")
+    print(name, "orbit views", views, flush=True)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["--orbit"]:
+        for n in sys.argv[2:]:
+            make_orbit(n)
+        sys.exit(0)
     if sys.argv[1:2] == ["--scene-hashes"]:
         for n in sys.argv[2:]:
             add_scene_hashes(n)

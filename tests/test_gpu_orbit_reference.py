@@ -1,0 +1,95 @@
+"""The frames bench.py times, against the REFERENCE: every view of a bench step (pkg.bench_views:
+the config camera + sun rotated once by f x 360 / F degrees about z, anim.cpp:76-110 /
+transform.hpp:67-112) rendered the way bench.py renders it -- one ceres_render_batch_device
+launch per 64 frames per rank, each rank its interleaved 8-row blocks, frames in the
+FrameExchange batch order at N > 1 -- reassembled, and compared by PPM sha256 with the
+reference's own render() of the same view (tests/golden/orbit/<cfg>.json, made by
+oracle/_ref/ref_render_exact --orbit-views).  The step's rays / hits equal the sum of the
+reference's per-view counts (render.hpp:155).  N = 1 is the bench step on one GPU; N = 2, 4, 8
+are the weak-scaling steps (16N views, 22.5/N degrees apart), every rank's share rendered here
+in turn on the one GPU."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden, load_orbit
+
+import configs
+
+pytestmark = pytest.mark.gpu
+
+MAXF = 64          # frames per batch launch (kMaxFrames)
+
+
+def _basis0(meta, cfg):
+    bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
+    return np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
+
+
+_scenes = {}
+
+
+def _scene(pkg, name):
+    if name not in _scenes:
+        _scenes.clear()                     # one big scene resident at a time
+        cfg = configs.CONFIGS[name]
+        mesh, bvh, cam = pkg.prepare(cfg)
+        _scenes[name] = (pkg.Scene(mesh, bvh, device=0), cam)
+    return _scenes[name]
+
+
+@pytest.mark.parametrize("name,world", [("dragon_1080", 1), ("dragon_1080", 2), ("dragon_1080", 4),
+                                        ("dragon_1080", 8), ("bunny_1080", 1), ("bunny_1080_primary", 1),
+                                        ("dragon_4096", 1), ("dragon_4096", 8), ("proc_c5", 1), ("proc_c5", 8)])
+def test_bench_step_frames_match_reference(pkg, name, world):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device (no CPU fallback exists)")
+    import ceres_raytracer_amd.distributed as D
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    meta, _, _ = load_golden(name)
+    fx = load_orbit(name)["by_step_bits"]
+    scene, cam = _scene(pkg, name)
+    F = 16 * world
+    b12, s3, steps = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=_basis0(meta, cfg))
+    if world > 1:
+        order = D.exchange_order(F, world)
+        b12, s3, steps = b12[order], s3[order], steps[order]
+    row_block = 8 if world > 1 else H
+    mode = pkg.cfg_mode(cfg)
+    st = torch.cuda.current_stream().cuda_stream
+    _, maxrows = D.ppm_row_permutation(H, row_block, world)
+    idx = torch.as_tensor(D.ppm_row_permutation(H, row_block, world)[0], device="cuda")
+    per_rank = []
+    rays = hits = 0
+    counters = torch.zeros(8, dtype=torch.int64, device="cuda")
+    for r in range(world):
+        til = pkg.Tiling(row_block, r, world)
+        rows = pkg.local_rows(H, til)
+        tight = torch.zeros((F, rows, 3 * W), dtype=torch.uint8, device="cuda")
+        for f0 in range(0, F, MAXF):
+            f1 = min(F, f0 + MAXF)
+            counters.zero_()
+            scene.render_batch_device(b12[f0:f1], s3[f0:f1], W, H, mode=mode, tiling=til,
+                                      d_rgb8=tight[f0].data_ptr(), d_counters=counters.data_ptr(), stream=st)
+            torch.cuda.synchronize()
+            c = counters.cpu().numpy()
+            assert c[6] == 0, "traversal stack overflow"
+            rays += int(c[0]); hits += int(c[1])
+        buf = torch.zeros((F, maxrows, 3 * W), dtype=torch.uint8, device="cuda")
+        buf[:, :rows] = tight
+        del tight
+        per_rank.append(buf)
+    head = b"P6 %d %d 255\n" % (W, H)
+    bad = []
+    ref_rays = ref_hits = 0
+    for f in range(F):
+        e = fx["%08x" % int(np.asarray(steps[f], np.float32).view(np.uint32))]
+        ref_rays += e["rays"]; ref_hits += e["hits"]
+        full = torch.cat([b[f] for b in per_rank])[idx].cpu().numpy()
+        if hashlib.sha256(head + full.tobytes()).hexdigest() != e["sha256"]:
+            bad.append((f, e["k"]))
+    assert not bad, f"frames differing from the reference (batch frame, orbit view k): {bad}"
+    assert (rays, hits) == (ref_rays, ref_hits)

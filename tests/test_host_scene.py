@@ -125,3 +125,28 @@ def test_obj_long_line_stops_reading(pkg, oracle_mod, tmp_path):
 def test_golden_tiny_meshes_exist():
     for f in ("tri1.obj", "quad.obj", "degenerate.obj"):
         assert os.path.exists(os.path.join(GOLDEN, f))
+
+
+@pytest.mark.parametrize("name", ["dragon_1080", "bunny_1080", "bunny_1080_primary", "dragon_4096", "proc_c5"])
+def test_bench_views_are_the_pinned_reference_poses(pkg, name):
+    """Every view bench.py can time at N = 1, 2, 4, 8 (pkg.bench_views, F = 16N) is pinned in
+    tests/golden/orbit/<cfg>.json, and the host's orbit pose (ceres_orbit_cameras, eye and sun)
+    equals the reference Transform's bits for it (anim.cpp:76-88, transform.hpp:67-112)."""
+    from conftest import load_orbit
+    fx = load_orbit(name)
+    by = fx["by_step_bits"]
+    assert len(by) == fx["views"] == pkg.configs.ORBIT_FIXTURE_VIEWS
+    cfg = pkg.configs.CONFIGS[name]
+    meta, _, _ = load_golden(name)
+    cam = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    v0 = [e for e in by.values() if e["k"] == 0][0]
+    assert v0["sha256"] == meta["ppm_sha256"]["exact"] and v0["rays"] == meta["exact"]["rays"]
+    for n in (1, 2, 4, 8):
+        F = 16 * n
+        b12, s3, steps = pkg.bench_views(cam, cfg["sun"], cfg["W"], cfg["H"], F)
+        for f in range(F):
+            e = by["%08x" % int(np.asarray(steps[f], np.float32).view(np.uint32))]
+            assert e["k"] == f * 128 // F
+            if f:
+                assert hexbits(b12[f, :3]) == e["eye"], (n, f)
+                assert hexbits(s3[f]) == e["sun"], (n, f)

@@ -15,7 +15,7 @@ import os
 import sys
 from collections import defaultdict
 
-SHORT = {k: k for k in ("ceres_fused", "ceres_primary", "ceres_shadow", "ceres_finalize", "ceres_assemble")}
+SHORT = {k: k for k in ("ceres_fused", "ceres_primary", "ceres_finalize", "ceres_assemble")}
 
 
 def short(name):
@@ -62,6 +62,17 @@ def main():
             e["l2_hit_rate"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
         if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_ACTIVE_INST_VALU", 0) > 0:
             e["valu_lane_utilisation"] = round(c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64), 4)
+        g = c.get("GRBM_GUI_ACTIVE", 0)
+        if g > 0:
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs, the TA / TD / TCP sums over the 256 CUs'
+            # instances: busy fraction = sum / (256 x GRBM / 8)
+            for n, key in (("TA_TA_BUSY_sum", "ta_busy_frac"), ("TD_TD_BUSY_sum", "td_busy_frac")):
+                if n in c:
+                    e[key] = round(c[n] / (32.0 * g), 4)
+        if "TCC_REQ_sum" in c:
+            e["l2_requests_per_launch"] = int(c["TCC_REQ_sum"])
+        if "TCP_TCC_READ_REQ_sum" in c and c.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0) > 0:
+            e["l1_to_l2_read_frac"] = round(c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"], 4)
         if c.get("SQ_WAVE_CYCLES", 0) > 0:
             for n, key in (("SQ_WAIT_INST_ANY", "issue_stall_frac"), ("SQ_WAIT_ANY", "waitcnt_parked_frac"),
                            ("SQ_ACTIVE_INST_ANY", "active_inst_frac")):
