@@ -928,6 +928,11 @@ void ceres::scene_release(ceres_scene* s) {
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
     for (auto e : s->ev_used) (void)hipEventDestroy(e);
     s->ev_pool.clear(); s->ev_used.clear();
+    for (auto e : s->band_events) (void)hipEventDestroy(e);
+    s->band_events.clear();
+    dfree(s->d_band_counters);
+    if (s->copy_stream) (void)hipStreamDestroy(s->copy_stream);
+    s->copy_stream = nullptr;
     if (s->stream) (void)hipStreamDestroy(s->stream);
     s->stream = nullptr;
 }
@@ -1399,28 +1404,75 @@ int ceres_assemble_rgb8_packed(const uint8_t* d_gathered, uint8_t* d_out, uint32
     return CERES_OK;
 }
 
+// Row bands of a host-buffer render (ceres_render_f32).  The call's length is set by the copy of
+// the framebuffer over the host link (C3: 24.9 MB of floats, ~0.45 ms at ~55 GB/s, against a
+// 0.17-ms kernel), so the frame is rendered as `bands` launches of contiguous row bands on the
+// scene stream and each band's rows are copied out on a second stream as soon as its kernel
+// ends: the copies start after the first band instead of after the whole frame.  Each pixel is
+// computed alone (render.hpp:104-153), so the bytes are those of one launch.  Measured on one
+// MI355X (profiles/r03/e2e): dragon 4096^2 float frame 4.04 -> 3.73 ms per call, RGB8 (./render)
+// 1.32 -> 1.04 ms with 4 bands; at 1080p the bands' own tails cost what the overlap saves (floats
+// +-2 %, RGB8 +60 %), so frames under kBandMinBytes stay one launch.  CERES_HOST_BANDS overrides
+// the count (1 = one launch, then the copy).
+constexpr uint32_t kMaxHostBands = 16;
+constexpr size_t kBandMinBytes = size_t(32) << 20;     // below this a frame is one launch (measured: 1080p floats ±2 %, 1080p RGB8 +60 %)
+
+static uint32_t host_bands(size_t W, size_t H, bool pixels, bool rgb8) {
+    uint32_t b = 4;
+    if (const char* e = std::getenv("CERES_HOST_BANDS")) b = uint32_t(std::max(1, std::atoi(e)));
+    const size_t bytes = W * H * 3 * ((pixels ? sizeof(float) : 0) + (rgb8 ? 1 : 0));
+    if (bytes < kBandMinBytes) b = 1;
+    return uint32_t(std::min<size_t>({size_t(b), size_t(kMaxHostBands), H}));
+}
+
 int ceres_render_f32(ceres_scene* s, const float basis12[12], const float sun[3], int mode, float* pixels,
                      uint8_t* rgb8, size_t W, size_t H, ceres_stats* stats) {
     if (!s) return set_error(CERES_EINVAL, "null scene");
     HIP_TRY(hipSetDevice(s->device));
     if (int rc = ensure_workspace(s, W * H, pixels != nullptr, rgb8 != nullptr)) return rc;
-    hipEvent_t a, b;
-    HIP_TRY(hipEventCreate(&a));
-    HIP_TRY(hipEventCreate(&b));
+    const uint32_t want = host_bands(W, H, pixels != nullptr, rgb8 != nullptr);
+    const uint32_t rb = uint32_t((H + want - 1) / want);
+    const uint32_t bands = uint32_t((H + rb - 1) / rb);
+    if (!s->d_band_counters) HIP_TRY(hipMalloc(&s->d_band_counters, kMaxHostBands * 8 * sizeof(uint64_t)));
+    if (bands > 1 && !s->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking));
+    while (s->band_events.size() < kMaxHostBands + 2) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        s->band_events.push_back(e);
+    }
+    hipEvent_t a = s->band_events[kMaxHostBands], b = s->band_events[kMaxHostBands + 1];
     HIP_TRY(hipEventRecord(a, s->stream));
-    int rc = launch(s, 1, basis12, sun, mode, W, H, nullptr, pixels ? s->d_pixels : nullptr, rgb8 ? s->d_rgb8 : nullptr,
-                    s->d_counters, s->stream);
-    if (rc) { (void)hipEventDestroy(a); (void)hipEventDestroy(b); return rc; }
+    for (uint32_t k = 0; k < bands; ++k) {
+        // band k = global rows [j0, j1): one block of the tiling {rb, k, bands}; its float rows sit
+        // at row j0 of the framebuffer (row 0 at the bottom), its PPM rows (flipped) at H - j1
+        const size_t j0 = size_t(k) * rb, j1 = std::min<size_t>(H, j0 + rb);
+        const ceres_tiling t{rb, k, bands};
+        if (int rc = launch(s, 1, basis12, sun, mode, W, H, &t, pixels ? s->d_pixels + 3 * W * j0 : nullptr,
+                            rgb8 ? s->d_rgb8 + 3 * W * (H - j1) : nullptr, s->d_band_counters + 8 * k, s->stream))
+            return rc;
+        HIP_TRY(hipEventRecord(s->band_events[k], s->stream));
+    }
     HIP_TRY(hipEventRecord(b, s->stream));
-    uint64_t c[8] = {0};
-    HIP_TRY(hipMemcpyAsync(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost, s->stream));
-    if (pixels) HIP_TRY(hipMemcpyAsync(pixels, s->d_pixels, W * H * 3 * sizeof(float), hipMemcpyDeviceToHost, s->stream));
-    if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, s->d_rgb8, W * H * 3, hipMemcpyDeviceToHost, s->stream));
+    hipStream_t cs = bands > 1 ? s->copy_stream : s->stream;
+    for (uint32_t k = 0; k < bands; ++k) {
+        const size_t j0 = size_t(k) * rb, j1 = std::min<size_t>(H, j0 + rb);
+        if (bands > 1) HIP_TRY(hipStreamWaitEvent(cs, s->band_events[k], 0));
+        if (pixels)
+            HIP_TRY(hipMemcpyAsync(pixels + 3 * W * j0, s->d_pixels + 3 * W * j0, 3 * W * (j1 - j0) * sizeof(float),
+                                   hipMemcpyDeviceToHost, cs));
+        if (rgb8)
+            HIP_TRY(hipMemcpyAsync(rgb8 + 3 * W * (H - j1), s->d_rgb8 + 3 * W * (H - j1), 3 * W * (j1 - j0),
+                                   hipMemcpyDeviceToHost, cs));
+    }
+    uint64_t cb[kMaxHostBands * 8] = {0};
+    HIP_TRY(hipMemcpyAsync(cb, s->d_band_counters, bands * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    if (bands > 1) HIP_TRY(hipStreamSynchronize(cs));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, a, b));
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
+    uint64_t c[8] = {0};
+    for (uint32_t k = 0; k < bands; ++k)
+        for (int i = 0; i < 8; ++i) c[i] = i == 6 ? std::max(c[i], cb[8 * k + i]) : c[i] + cb[8 * k + i];
     fill_stats(stats, c, ms);
     if (c[6]) return set_error(CERES_ESTACK, "traversal stack overflow");
     return CERES_OK;

@@ -48,6 +48,12 @@ struct ceres_scene {
     uint8_t* d_rgb8 = nullptr;
     size_t px_cap = 0;
     hipStream_t stream = nullptr;
+    // host-buffer renders (ceres_render_f32): row bands rendered one after another on `stream`,
+    // each band's D2H copy on `copy_stream` as soon as its kernel ends (the copy over the host
+    // link, not the kernel, sets the call's length); counters per band
+    hipStream_t copy_stream = nullptr;
+    uint64_t* d_band_counters = nullptr;
+    std::vector<hipEvent_t> band_events;
     int num_cus = 256;
     unsigned long long* d_wave_log = nullptr;   // stats scenes: per-wave diagnostic records
     size_t wave_log_waves = 0, last_grid_waves = 0;
