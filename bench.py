@@ -518,6 +518,14 @@ def main():
                        + ((" + one RCCL all-to-all per step: frame f gathered to rank f (pipelined)" if exchange
                            else " + one RCCL gather per step to rank 0 (pipelined)") if world > 1 else ""),
                        "float_framebuffer": d_px[0] is not None, "streams": S},
+            # the step's one collective against the xGMI budget (DESIGN.md "Multi-GPU"): bytes one rank
+            # receives per step, 1/N of them from each peer over that peer's direct link (one link per
+            # peer in a fully connected 8-GPU node) at 76.8 GB/s per link and direction
+            "collective": None if world == 1 else {
+                "kind": "all_to_all" if exchange else "gather",
+                "recv_bytes_per_rank_step": (world - 1) * (F // world if exchange else F) * H * 3 * W // world,
+                "xgmi_link_ms_est": round((F // world if exchange else F) * H * 3 * W / world / 76.8e6, 4),
+                "ms_per_step": round(T / args.steps * 1e3, 5)},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
         }
         if view0 is not None:

@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
 """Weak-scaling rehearsal on ONE MI355X: the per-rank work of bench.py at N = 1, 2, 4, 8 GPUs.
 
-At N GPUs a bench step is F = k*N orbit frames (k = frames per GPU, bench.py's default 8), each frame's rows dealt in blocks of 8 over the
+At N GPUs a bench step is F = k*N orbit frames (k = frames per GPU, bench.py's default 16), each frame's rows dealt in blocks of 8 over the
 N ranks; rank r renders its rows of all F frames with one ceres_render_batch_device launch,
 and rank 0 un-interleaves the gathered buffers with ceres_assemble_rgb8.  This tool runs,
 on the one GPU it has, exactly the launch every rank would run (Tiling(8, r, N)) and the
 rank-0 assembly, timed with HIP events on the launch stream.  The slowest rank's launch is
 the predicted device time of a step, serialised (tail-bound) and in the bench's regime
-(launches rotated over 8 streams, wall time per launch); the RCCL collective is NOT modelled (one GPU has no xGMI
-peer) -- it is pipelined behind the next step's render in bench.py (distributed.BatchGather).
+(launches rotated over 8 streams, wall time per launch).  One GPU has no xGMI peer, so the RCCL
+all-to-all itself cannot run; its on-device cost is EMULATED in a third regime: after each
+pipelined launch, a copy of the rank's receive volume (bench.py's FrameExchange: (N-1)/N of its k
+frames' RGB8 rows, the bytes RCCL's copy kernels move into this GPU's HBM, read from the render's
+output) plus the un-interleave of its k frames (ceres_assemble_rgb8_packed) run on a separate
+"collective" stream, as in bench.py -- so the predicted efficiency pays the exchange's HBM
+traffic and CU time.  The link time is budgeted separately: 1/N of the rank's k frames from each
+peer over its own xGMI link at XGMI_GBS per link and direction (default 76.8 GB/s: 153.6 GB/s
+bidirectional).
 
     python tools/scaling_rehearsal.py [config] [reps] [frames per GPU] [row block] > gpurun_out/scaling_rehearsal.json
 """
@@ -21,6 +28,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+XGMI_GBS = float(os.environ.get("XGMI_GBS", "76.8"))     # per link and direction
 
 
 def main():
@@ -31,7 +39,7 @@ def main():
         pkg.LIB_PATH = os.path.abspath(os.environ["CERES_LIB"])
     name = sys.argv[1] if len(sys.argv) > 1 else "dragon_1080"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
-    k = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    k = int(sys.argv[3]) if len(sys.argv) > 3 else 16
     rb = int(sys.argv[4]) if len(sys.argv) > 4 else 8            # bench.py --row-block
     cfg = pkg.configs.CONFIGS[name]
     meta = load_golden(name)
@@ -60,23 +68,38 @@ def main():
         spx = [torch.empty(F * 3 * W * maxrows, dtype=torch.float32, device=dev) for _ in range(S)]
         srgb = [torch.empty(F * 3 * W * maxrows, dtype=torch.uint8, device=dev) for _ in range(S)]
         piped = []
-        counters = torch.zeros(8, dtype=torch.int64, device=dev)
+        piped_x = []
+        # exchange emulation: per step, the receive volume of one rank ((N-1)/N of k frames) copied on a
+        # collective stream out of the render's output, then the assembly of its k frames
+        recv_bytes = (N - 1) * k * H * 3 * W // N
+        coll = torch.cuda.Stream(device=dev)
+        xrecv = [torch.empty(max(recv_bytes, 1), dtype=torch.uint8, device=dev) for _ in range(2)]
+        xfull = torch.empty((k, H, 3 * W), dtype=torch.uint8, device=dev)
+        xpack = torch.zeros((k * H, 3 * W), dtype=torch.uint8, device=dev)
+        copied = [None] * S
+        counters = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range((F + 63) // 64)]
+
+        def launch(til, d_px, d_rgb, st, with_counters=False):
+            # as bench.py: one ceres_render_batch_device launch per (at most) 64 frames of the step
+            fb = 3 * W * max(pkg.local_rows(H, til), 1)
+            for c, f0 in enumerate(range(0, F, 64)):
+                f1 = min(F, f0 + 64)
+                scene.render_batch_device(b12[f0:f1], s3[f0:f1], W, H, mode=mode, tiling=til, d_pixels=d_px + 4 * fb * f0,
+                                          d_rgb8=d_rgb + fb * f0,
+                                          d_counters=counters[c].data_ptr() if with_counters else 0, stream=st)
+
         for r in range(N):
             til = pkg.Tiling(row_block, r, N)
-            counters.zero_()
-            scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=til, d_pixels=px.data_ptr(),
-                                      d_rgb8=rgb.data_ptr(), d_counters=counters.data_ptr(), stream=stream.cuda_stream)
+            launch(til, px.data_ptr(), rgb.data_ptr(), stream.cuda_stream, with_counters=True)
             torch.cuda.synchronize(dev)
-            rank_rays.append(int(counters[0].item()))
+            rank_rays.append(sum(int(c[0].item()) for c in counters))
             rays += rank_rays[-1]
             for _ in range(5):
-                scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=til, d_pixels=px.data_ptr(),
-                                          d_rgb8=rgb.data_ptr(), stream=stream.cuda_stream)
+                launch(til, px.data_ptr(), rgb.data_ptr(), stream.cuda_stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(reps):
-                scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=til, d_pixels=px.data_ptr(),
-                                          d_rgb8=rgb.data_ptr(), stream=stream.cuda_stream)
+                launch(til, px.data_ptr(), rgb.data_ptr(), stream.cuda_stream)
             e1.record(stream)
             e1.synchronize()
             per_rank.append(e0.elapsed_time(e1) / reps)
@@ -84,10 +107,30 @@ def main():
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
                 for q in range(reps * S // 2):
-                    scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=til, d_pixels=spx[q % S].data_ptr(),
-                                              d_rgb8=srgb[q % S].data_ptr(), stream=streams[q % S].cuda_stream)
+                    launch(til, spx[q % S].data_ptr(), srgb[q % S].data_ptr(), streams[q % S].cuda_stream)
                 torch.cuda.synchronize(dev)
             piped.append((time.perf_counter() - t0) * 1e3 / (reps * S // 2))
+            if N > 1:
+                for it in range(2):                      # warm, then timed
+                    torch.cuda.synchronize(dev)
+                    t0 = time.perf_counter()
+                    for q in range(reps * S // 2):
+                        st = streams[q % S]
+                        if copied[q % S] is not None:
+                            st.wait_event(copied[q % S])  # the slot's rows were read by the exchange
+                        launch(til, spx[q % S].data_ptr(), srgb[q % S].data_ptr(), st.cuda_stream)
+                        done = torch.cuda.Event()
+                        done.record(st)
+                        coll.wait_event(done)
+                        with torch.cuda.stream(coll):
+                            xrecv[q % 2].copy_(srgb[q % S][:recv_bytes])
+                            pkg.assemble_rgb8_packed(xpack.data_ptr(), xfull.data_ptr(), k, W, H, row_block, N,
+                                                     coll.cuda_stream)
+                            ev = torch.cuda.Event()
+                            ev.record(coll)
+                        copied[q % S] = ev
+                    torch.cuda.synchronize(dev)
+                piped_x.append((time.perf_counter() - t0) * 1e3 / (reps * S // 2))
         asm_ms = 0.0
         if N > 1:
             recv = torch.zeros((N, F * maxrows, 3 * W), dtype=torch.uint8, device=dev)
@@ -107,6 +150,8 @@ def main():
         mrays = rays / (step_ms * 1e3)
         pipe_ms = max(piped)
         mrays_p = rays / (pipe_ms * 1e3)
+        pipe_x_ms = max(piped_x) if piped_x else pipe_ms
+        mrays_x = rays / (pipe_x_ms * 1e3)
         if base is None:
             base, base_p = mrays, mrays_p
         del spx, srgb
@@ -118,7 +163,12 @@ def main():
                           "predicted_weak_efficiency": round(mrays / (N * base), 3),
                           "pipelined_rank_ms": [round(x, 5) for x in piped], "pipelined_streams": S,
                           "predicted_mrays_s_pipelined": round(mrays_p, 1),
-                          "predicted_weak_efficiency_pipelined": round(mrays_p / (N * base_p), 3)}
+                          "predicted_weak_efficiency_pipelined": round(mrays_p / (N * base_p), 3),
+                          "exchange_recv_bytes_per_rank_step": recv_bytes,
+                          "xgmi_link_ms_per_step": round(k * H * 3 * W / N / (XGMI_GBS * 1e6), 4),
+                          "pipelined_with_exchange_rank_ms": [round(x, 5) for x in piped_x],
+                          "predicted_mrays_s_pipelined_with_exchange": round(mrays_x, 1),
+                          "predicted_weak_efficiency_pipelined_with_exchange": round(mrays_x / (N * base_p), 3)}
         print(json.dumps({"N": N, **out["by_n"][N]}), file=sys.stderr, flush=True)
     scene.close()
     print(json.dumps(out))
