@@ -202,16 +202,25 @@ def roofline_block(name, nbytes, ms, pmc, scene_bytes):
                                         "l2_hit_rate", "valu_lane_utilisation", "hbm_read_bytes_per_launch",
                                         "hbm_write_bytes_per_launch") if pmc.get(k) is not None})
     out["pmc_source"] = "profiles/pmc_summary.json (rocprofv3 --pmc, solo launches of this config)"
+    hit = pmc.get("l2_hit_rate")
     if bound == "hbm" and dram_gbs and dram_gbs >= 0.5 * HBM_PEAK_GBS:
         lim = "HBM bandwidth"
-    elif wait is not None and wait >= 0.45:
-        where = "MALL/DRAM" if rd and scene_bytes and rd >= scene_bytes else "L2"
-        lim = f"{where} latency of dependent loads (waves parked on s_waitcnt {wait:.2f} of cycles"
-        lim += f", fabric reads {rd / 1e6:.0f} MB/launch vs scene {scene_bytes / 1e6:.0f} MB)" if rd and scene_bytes else ")"
-    elif ta is not None and ta >= 0.5:
-        lim = f"vector-memory issue (TA busy {ta:.2f}) + dependent L2 latency (s_waitcnt {wait:.2f})"
     else:
-        lim = "dependent-load latency" + (f" (s_waitcnt {wait:.2f})" if wait is not None else "")
+        # the counters say latency or issue, not bandwidth (dram_frac, frac << 1); where the L2 misses
+        # are served follows from the scene's size against the 8 x 4 MiB L2s and the 256-MiB MALL
+        where = ("DRAM (scene larger than the 256-MiB Infinity Cache)" if scene_bytes and scene_bytes > 256 << 20
+                 else "MALL (scene larger than the L2s)" if scene_bytes and scene_bytes > 32 << 20
+                 else "MALL (scene L2-resident; misses are each XCD's first touches)")
+        kind = "dependent-load latency" if wait is not None and wait >= 0.45 else \
+            "vector-memory issue + dependent-load latency" if ta is not None and ta >= 0.5 else \
+            "dependent-load latency and issue"
+        lim = f"{kind}: waves parked on s_waitcnt {wait:.2f} of cycles" if wait is not None else kind
+        if ta is not None:
+            lim += f", TA busy {ta:.2f}"
+        if hit is not None:
+            lim += f"; L2 hit {hit:.2f}, misses to {where}"
+        if rd:
+            lim += f", fabric reads {rd / 1e6:.0f} MB/launch"
     out["limiter"] = lim
     return out
 

@@ -46,6 +46,15 @@
 #ifndef CERES_FRAME_MAJOR_PIXELS
 #define CERES_FRAME_MAJOR_PIXELS (1u << 22)    // batches of frames of >= this many pixels: frame after frame (0: never)
 #endif
+#ifndef CERES_LOCAL_ORDER
+#define CERES_LOCAL_ORDER 1                    // XCD-local Morton tile order (ensure_tile_order); 0: never
+#endif
+#ifndef CERES_LOCAL_CHUNK_BATCH
+#define CERES_LOCAL_CHUNK_BATCH 64             // tiles per XCD block: frame-major batches ...
+#endif
+#ifndef CERES_LOCAL_CHUNK_SOLO
+#define CERES_LOCAL_CHUNK_SOLO 16              // ... and single large frames of a DRAM-resident scene
+#endif
 
 namespace ceres {
 
@@ -1042,6 +1051,44 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     // of four; the left half of a mesh).  Shuffling each window of 64 (fixed seed) keeps the order
     // centre-first at that granularity and gives every XCD an unbiased sample: solo bunny 1080p
     // -9.5 %, dragon 4096^2 -5.5 %; one rank of a 2-GPU split 40 % -> 0 % apart.
+    // XCD-local order for large views: each frame's tiles along a Morton curve, every run of 8 x c
+    // tiles dealt so that XCD x (workgroups w = x mod 8) takes the x-th block of c consecutive
+    // curve tiles -- the waves of one XCD render one compact image region at a time, so the BVH
+    // nodes and triangles that region's rays share stay in that XCD's L2.  Used for frame-major
+    // batches (A/B, 16-frame batches x 8 streams: dragon 4096^2 -3.2 %, C5 -1.7..-1.9 %) and for
+    // single frames of a scene that does not fit the L2s (C5 solo frame 3.11 -> 2.66 ms, -14 %); a
+    // single frame of an L2-resident scene keeps the centre-first order (dragon 4096^2: local
+    // +9 %: its expensive centre tiles must start first).  profiles/r03/local_order/.
+    const size_t scene_bytes = s->n_pairs * sizeof(SiblingPair) + s->n_nodes4 * sizeof(Node4) +
+                               s->n_tri * (sizeof(Tri48) + 4 + 36);
+    const size_t lchunk = !CERES_LOCAL_ORDER || !frame_major ? 0
+                          : frames > 1 ? size_t(CERES_LOCAL_CHUNK_BATCH)
+                          : scene_bytes >= kDramSceneBytes ? size_t(CERES_LOCAL_CHUNK_SOLO) : 0;
+    if (lchunk) {
+        auto morton = [](uint32_t x, uint32_t y) {
+            uint64_t m = 0;
+            for (int b = 0; b < 16; ++b) m |= (uint64_t((x >> b) & 1) << (2 * b)) | (uint64_t((y >> b) & 1) << (2 * b + 1));
+            return m;
+        };
+        std::vector<std::pair<uint64_t, uint32_t>> mk(n);
+        for (uint32_t id = 0; id < n; ++id) {
+            const uint32_t f = id / per_frame, rem = id - f * per_frame, y = rem / bx, x = rem - y * bx;
+            mk[id] = {(uint64_t(f) << 40) | morton(x, y), id};
+        }
+        std::sort(mk.begin(), mk.end());
+        const uint32_t tpw = frames == 1 ? 1u : uint32_t(CERES_TILES_PER_WAVE);
+        const size_t c = std::max<size_t>(tpw, lchunk / tpw * tpw), cw = c / tpw, grp = 8 * c;
+        const size_t full = n / grp * grp;
+        for (size_t p = 0; p < n; ++p) {
+            size_t src = p;
+            if (p < full) {
+                const size_t w = p / tpw, i = p % tpw, g = w / (8 * cw), wl = w % (8 * cw);
+                src = g * grp + (wl % 8) * c + (wl / 8) * tpw + i;
+            }
+            order[p] = mk[src].second;
+        }
+        return upload_tile_order(s, W, H, t, frames, tile, order, stream, out);
+    }
     uint64_t st = 0x9e3779b97f4a7c15ull;
     for (size_t b0 = 0; b0 < n; b0 += dev::kTileShuffleWindow) {
         const size_t len = std::min<size_t>(dev::kTileShuffleWindow, n - b0);

@@ -73,6 +73,7 @@ void scene_release(ceres_scene* s);          // frees every device buffer and th
 // centre-first, XCD-balanced order of one whole frame's tile x tile tiles (render_hip.hip)
 int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out);
 constexpr size_t kMaxTileOrders = 16;         // cached orders per scene before LRU eviction
+constexpr size_t kDramSceneBytes = size_t(64) << 20;   // a scene this large does not stay in the 8 x 4 MB L2s
 #ifndef CERES_RETIRED_BYTES
 #define CERES_RETIRED_BYTES (64u << 20)
 #endif

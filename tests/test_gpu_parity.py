@@ -378,6 +378,30 @@ def test_c5_procedural_10m_triangles(gpu):
     scene.close()
 
 
+def test_c5_single_launch_xcd_local_order(gpu):
+    """C5 as ONE whole-frame launch (ceres_render_device, the launch bench.py's roofline times): a
+    DRAM-resident scene's large frame takes the XCD-local Morton tile order (ensure_tile_order);
+    the PPM and the counts still equal the reference's."""
+    import torch
+    pkg = gpu
+    meta, _, _ = load_golden("proc_c5")
+    cfg = configs.CONFIGS["proc_c5"]
+    W, H = cfg["W"], cfg["H"]
+    mesh, bvh, cam = pkg.prepare(cfg)
+    scene = pkg.Scene(mesh, bvh)
+    del mesh, bvh
+    assert scene.info()["device_bytes"] >= 64 << 20          # kDramSceneBytes: the local order applies
+    rgb = torch.empty(3 * W * H, dtype=torch.uint8, device="cuda")
+    c = torch.zeros(8, dtype=torch.int64, device="cuda")
+    scene.render_device(pinned_basis(meta, cfg), cfg["sun"], W, H, d_rgb8=rgb.data_ptr(), d_counters=c.data_ptr(),
+                        stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    c = c.cpu().numpy()
+    assert (int(c[0]), int(c[1])) == (meta["exact"]["rays"], meta["exact"]["hits"]) and c[6] == 0
+    assert hashlib.sha256(pkg.ppm(W, H, rgb.cpu().numpy())).hexdigest() == meta["ppm_sha256"]["exact"]
+    scene.close()
+
+
 @pytest.mark.parametrize("gpu_bvh", [False, True])
 def test_cli_writes_reference_ppm(gpu, tmp_path, gpu_bvh):
     pkg = gpu

@@ -32,6 +32,9 @@ def load_build(path, tag):
 
 
 def main():
+    # kernel A/B: a host-buffer render is ONE launch (ceres_render_f32 splits frames of >= 32 MB into
+    # row bands whose copies overlap later bands; their device time would include the bands' tails)
+    os.environ.setdefault("CERES_HOST_BANDS", "1")
     import torch  # noqa: F401  (one HIP runtime for every build)
     name = sys.argv[1] if len(sys.argv) > 1 else "dragon_1080"
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 20
@@ -66,10 +69,11 @@ def main():
         s3 = np.asarray(cfg["sun"], np.float32)[None, :]
         nb = int(os.environ.get("AB_BATCH", "1"))      # frames per launch (bench.py's --frames-per-gpu)
         if nb > 1:
-            axis, step_deg = first.configs.BENCH_ORBIT
-            b12, s3 = first.orbit_cameras(cam, cfg["sun"], W, H, nb, axis=axis, step_deg=step_deg, rotate_first=False)
-            b12[0] = basis
-            s3[0] = np.asarray(cfg["sun"], np.float32)
+            # bench.py's step views (pkg.bench_views); AB_VIEW0=1: nb copies of frame 0 (the C5 orbit
+            # turns away from the heightfield for half of its views)
+            b12, s3, _ = first.bench_views(cam, cfg["sun"], W, H, nb, basis0=basis)
+            if os.environ.get("AB_VIEW0") == "1":
+                b12, s3 = np.repeat(b12[:1], nb, 0), np.repeat(s3[:1], nb, 0)
             px = [torch.empty(nb * 3 * W * H, dtype=torch.float32, device="cuda") for _ in range(n_streams)]
             rgb = [torch.empty(nb * 3 * W * H, dtype=torch.uint8, device="cuda") for _ in range(n_streams)]
         for _ in range(rounds):
