@@ -32,6 +32,7 @@ import configs  # noqa: E402,F401  (re-exported)
 
 MODE_FULL, MODE_PRIMARY = 0, 1
 MODE_ROBUST = 0x10          # OR-ed: RobustNodeIntersector traversal (node_intersectors.hpp:54-79)
+MODE_QBVH4 = 0x20           # OR-ed: compressed shadow BVH4 (8-bit child bounds; budget-gated, not exact)
 
 
 def cfg_mode(cfg):

@@ -78,6 +78,20 @@ __host__ __device__
 #endif
 inline uint32_t node4_child(uint32_t count, uint32_t first) { return first << kNode4CountBits | count; }
 
+// Compressed shadow BVH4 record (CERES_MODE_QBVH4; quantize_nodes4 in render_hip.hip): the node's
+// box origin and a power-of-two scale per axis, each child bound as one byte (4 children's lo_x
+// bytes in one word, ...), and the same packed child words as Node4.  Bound = fma(byte, scale,
+// origin), rounded outwards on the host (the decoded box always contains the exact one).
+// 64 B = four 16-B loads per step instead of seven.
+struct alignas(64) QNode4 {
+    float ox, oy, oz, sx;
+    float sy, sz;
+    uint32_t qlx, qhx;           // byte c = child c
+    uint32_t qly, qhy, qlz, qhz;
+    uint32_t child[4];
+};
+static_assert(sizeof(QNode4) == 64, "QNode4");
+
 constexpr int kShards = 32;    // counter shards (one 128-B line each), wavefront w adds to shard w % 32
 struct alignas(128) Shard {
     uint32_t queued;           // shadow rays traced
@@ -108,6 +122,7 @@ struct KParams {
     const uint32_t* tile_order;                  // fused kernel: block -> batch tile (centre first)
     const SiblingPair* pairs;
     const Node4* nodes4;                         // shadow-ray BVH4 over the same leaf slots
+    const QNode4* qnodes4;                       // its compressed copy (CERES_MODE_QBVH4 only)
     const Tri48* tris;
     const uint32_t* orig;
     const float* norms;

@@ -9,7 +9,7 @@
 //                [--rotate x|y|z deg] [--size W H] [-o|--out file.ppm] [--primary-only]
 //                [--proc N] [--device D] [--bench reps] [--json]
 //                [--orbit ax ay az step_deg count] [--frames N] [--gpu-bvh] [--double|-d]
-//                [--gpus N] [--row-block R] [--robust]
+//                [--gpus N] [--row-block R] [--robust] [--qbvh]
 //
 // --robust traverses with the library's RobustNodeIntersector (node_intersectors.hpp:54-79,
 // T. Ize's padded-inverse slab test) instead of render()'s FastNodeIntersector.
@@ -67,7 +67,7 @@ int usage() {
                  "usage: render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]\n"
                  "              [--rotate x|y|z deg] [--size W H] [-o out.ppm] [--primary-only] [--proc N]\n"
                  "              [--device D] [--bench reps] [--json] [--orbit ax ay az step_deg count] [--frames N]\n"
-                 "              [--gpu-bvh] [--double] [--gpus N] [--row-block R] [--robust]\n");
+                 "              [--gpu-bvh] [--double] [--gpus N] [--row-block R] [--robust] [--qbvh]\n");
     return 2;
 }
 
@@ -106,6 +106,7 @@ bool parse(int argc, char** argv, Opts& o) {
         } else if (a == "-o" || a == "--out") { if (!have(1)) return false; o.out = argv[++i]; }
         else if (a == "--primary-only") o.mode = (o.mode & CERES_MODE_ROBUST) | CERES_MODE_PRIMARY;
         else if (a == "--robust") o.mode |= CERES_MODE_ROBUST;             // RobustNodeIntersector traversal
+        else if (a == "--qbvh") o.mode |= CERES_MODE_QBVH4;                // compressed shadow BVH4 (not exact)
         else if (a == "--proc") { if (!have(1)) return false; o.proc = std::atoi(argv[++i]); }
         else if (a == "--device") { if (!have(1)) return false; o.device = std::atoi(argv[++i]); }
         else if (a == "--gpus") { if (!have(1)) return false; o.gpus = std::atoi(argv[++i]); if (o.gpus < 1) return false; }

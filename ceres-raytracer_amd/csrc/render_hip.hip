@@ -328,10 +328,37 @@ __device__ __forceinline__ N4 load_n4_u(const Node4* nodes, uint32_t cur) {
     }
     return load_n4(nodes + cur);
 }
+// compressed node (CERES_MODE_QBVH4, ceres_types.hpp QNode4): bound = fma(byte, scale, origin), the
+// formula quantize_nodes4 checks on the host (the decoded box contains the exact one)
+__device__ __forceinline__ float4 qdecode(uint32_t w, float scale, float origin) {
+    return make_float4(__builtin_fmaf(float(w & 0xffu), scale, origin), __builtin_fmaf(float((w >> 8) & 0xffu), scale, origin),
+                       __builtin_fmaf(float((w >> 16) & 0xffu), scale, origin), __builtin_fmaf(float(w >> 24), scale, origin));
+}
+__device__ __forceinline__ N4 load_q4_u(const QNode4* nodes, uint32_t cur) {
+    float4 a, b;
+    uint4 c, d;
+    uint32_t r;
+    if (uniform_id(cur, r)) {
+        const QNode4* q = nodes + r;
+        a = sload_f4(q, 0); b = sload_f4(q, 1); c = sload_u4(q, 2); d = sload_u4(q, 3);
+    } else {
+        const float4* q = reinterpret_cast<const float4*>(nodes + cur);
+        a = q[0]; b = q[1];
+        c = reinterpret_cast<const uint4*>(q)[2]; d = reinterpret_cast<const uint4*>(q)[3];
+    }
+    // a = {ox, oy, oz, sx}, b = {sy, sz, qlx, qhx}, c = {qly, qhy, qlz, qhz}, d = child words
+    return {qdecode(__float_as_uint(b.z), a.w, a.x), qdecode(__float_as_uint(b.w), a.w, a.x),
+            qdecode(c.x, b.x, a.y), qdecode(c.y, b.x, a.y), qdecode(c.z, b.y, a.z), qdecode(c.w, b.y, a.z), d};
+}
+template <bool kQ>
+__device__ __forceinline__ N4 load_shadow_node(const KParams& P, uint32_t cur) {
+    if constexpr (kQ) return load_q4_u(P.qnodes4, cur);
+    else return load_n4_u(P.nodes4, cur);
+}
 __device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 __device__ __forceinline__ uint32_t pick(uint4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 
-template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false>
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, bool kQ = false>
 __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT stk, uint32_t& n_pairs,
                                            uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f, tmax = FLT_MAX;
@@ -343,18 +370,9 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
     uint32_t sp = 0, cur = 0;
     while (true) {
         if (kStats) ++n_pairs;
-        float4 LX, HX, LY, HY, LZ, HZ;
-        uint4 CH;
-        uint32_t rc;
-        if (uniform_id(cur, rc)) {
-            const Node4* q = P.nodes4 + rc;
-            LX = sload_f4(q, 0); HX = sload_f4(q, 1); LY = sload_f4(q, 2); HY = sload_f4(q, 3);
-            LZ = sload_f4(q, 4); HZ = sload_f4(q, 5); CH = sload_u4(q, 6);
-        } else {
-            const float4* q = reinterpret_cast<const float4*>(P.nodes4 + cur);
-            LX = q[0]; HX = q[1]; LY = q[2]; HY = q[3]; LZ = q[4]; HZ = q[5];
-            CH = reinterpret_cast<const uint4*>(q)[6];
-        }
+        const N4 nd = load_shadow_node<kQ>(P, cur);
+        const float4 LX = nd.lx, HX = nd.hx, LY = nd.ly, HY = nd.hy, LZ = nd.lz, HZ = nd.hz;
+        const uint4 CH = nd.ch;
         float e[4], x[4];
         const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
         const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
@@ -567,7 +585,7 @@ struct StealLdsT {
 // Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
 // intra-wavefront work stealing; on return L.blocked[tid] holds the lane's answer.  Must be
 // reached by all 64 lanes of the wavefront (it loops on wavefront ballots).
-template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false>
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, bool kQ = false>
 __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, StkT stk, StealLdsT<kS>& L,
                                                uint32_t tid, uint32_t lane, uint32_t& n_pairs, uint32_t& n_tests,
                                                bool& overflow, uint32_t* n_iters = nullptr) {
@@ -592,7 +610,7 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
         if (active && L.blocked[owner]) active = false;                 // another piece found an occluder
         if (active) {
             if (kStats) ++n_pairs;
-            const N4 n = load_n4_u(P.nodes4, cur);
+            const N4 n = load_shadow_node<kQ>(P, cur);
             float e[4];
             uint32_t leaf_mask = 0, inner_mask = 0;
 #pragma unroll
@@ -719,7 +737,7 @@ __device__ __forceinline__ void finish_pixel(const KParams& P, uint32_t f, uint3
 // whose pixel missed help the others), then shades.  No shadow-ray queue in HBM, no second
 // launch: the shadow work of early tiles overlaps the primary work of later ones.
 constexpr int kFusedB = 64;      // single-wavefront workgroups (LDS is released per workgroup)
-template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal>
+template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ = false>
 __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     constexpr int kB = kFusedB;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -815,9 +833,9 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     // launch is tail-bound); a multi-frame batch is throughput-bound, and there one ray per lane
     // spends fewer instructions per node (the steal bookkeeping runs every iteration)
     if constexpr (kSteal)
-        steal_traverse<kStats, kB, StkT, kRobust>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
+        steal_traverse<kStats, kB, StkT, kRobust, kQ>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
     else
-        L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
+        L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust, kQ>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
@@ -932,7 +950,7 @@ void ceres::scene_release(ceres_scene* s) {
     for (auto& o : s->orders) dfree(o.d);
     for (auto& d : s->retired) dfree(d);
     s->orders.clear(); s->retired.clear(); s->retired_bytes = 0;
-    dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
+    dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_qnodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
     for (auto e : s->ev_used) (void)hipEventDestroy(e);
@@ -1100,6 +1118,70 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     return upload_tile_order(s, W, H, t, frames, tile, order, stream, out);
 }
 
+// CERES_MODE_QBVH4: the exact shadow BVH4 (Node4) -> compressed QNode4 records.  Per node and
+// axis: origin = the smallest child lo, scale = the power of two that puts the children's extent
+// in 250 steps; every child bound becomes a byte q with fma(q, scale, origin) <= lo (resp. >= hi),
+// checked with the kernel's own formula, so each decoded box contains the exact box (and the
+// fast slab test is monotone in the bounds: every box the exact test passes, the decoded one
+// passes too).  Empty slots keep their kNode4Empty child word.
+int quantize_nodes4(const std::vector<Node4>& in, std::vector<QNode4>& out) {
+    out.assign(in.size(), QNode4{});
+    for (size_t k = 0; k < in.size(); ++k) {
+        const Node4& n = in[k];
+        QNode4& q = out[k];
+        const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
+        const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
+        float org[3], scl[3];
+        uint32_t ql[3] = {0, 0, 0}, qh[3] = {0, 0, 0};
+        for (int a = 0; a < 3; ++a) {
+            float mn = INFINITY, mx = -INFINITY;
+            for (int c = 0; c < 4; ++c)
+                if (n.child[c] != kNode4Empty) { mn = std::min(mn, lo[a][c]); mx = std::max(mx, hi[a][c]); }
+            if (mn > mx) { mn = 0.f; mx = 0.f; }                     // no children (cannot happen) or empty
+            if (!std::isfinite(mn) || !std::isfinite(mx))
+                return set_error(CERES_EUNSUPPORTED, "CERES_MODE_QBVH4: non-finite BVH bounds");
+            const double ext = double(mx) - double(mn);
+            int e = ext > 0 ? int(std::ceil(std::log2(ext / 250.0))) : -126;
+            e = std::max(e, -126);
+            float sc = std::ldexp(1.0f, e);
+            org[a] = mn;
+            for (int c = 0; c < 4; ++c) {
+                uint32_t bl = 255, bh = 0;                           // empty slot: never read (child word)
+                if (n.child[c] != kNode4Empty) {
+                    double fl = std::floor((double(lo[a][c]) - double(mn)) / double(sc));
+                    double fh = std::ceil((double(hi[a][c]) - double(mn)) / double(sc));
+                    int il = int(std::max(0.0, std::min(255.0, fl))), ih = int(std::max(0.0, std::min(255.0, fh)));
+                    while (il > 0 && std::fma(float(il), sc, mn) > lo[a][c]) --il;
+                    while (ih < 255 && std::fma(float(ih), sc, mn) < hi[a][c]) ++ih;
+                    if (std::fma(float(il), sc, mn) > lo[a][c] || std::fma(float(ih), sc, mn) < hi[a][c])
+                        return set_error(CERES_EUNSUPPORTED, "CERES_MODE_QBVH4: bound not representable");
+                    bl = uint32_t(il); bh = uint32_t(ih);
+                }
+                ql[a] |= bl << (8 * c);
+                qh[a] |= bh << (8 * c);
+            }
+            scl[a] = sc;
+        }
+        q.ox = org[0]; q.oy = org[1]; q.oz = org[2];
+        q.sx = scl[0]; q.sy = scl[1]; q.sz = scl[2];
+        q.qlx = ql[0]; q.qhx = qh[0]; q.qly = ql[1]; q.qhy = qh[1]; q.qlz = ql[2]; q.qhz = qh[2];
+        for (int c = 0; c < 4; ++c) q.child[c] = n.child[c];
+    }
+    return CERES_OK;
+}
+
+// First QBVH4 render of a scene: read its exact BVH4 back, compress it, upload the copy.
+int build_qnodes4(ceres_scene* s) {
+    if (!s->n_nodes4 || !s->d_nodes4) return CERES_OK;              // root is a leaf: shadow rays use the BVH2 path
+    std::vector<Node4> n4(s->n_nodes4);
+    HIP_TRY(hipMemcpy(n4.data(), s->d_nodes4, n4.size() * sizeof(Node4), hipMemcpyDeviceToHost));
+    std::vector<QNode4> q;
+    if (int rc = quantize_nodes4(n4, q)) return rc;
+    HIP_TRY(hipMalloc(&s->d_qnodes4, q.size() * sizeof(QNode4)));
+    HIP_TRY(hipMemcpy(s->d_qnodes4, q.data(), q.size() * sizeof(QNode4), hipMemcpyHostToDevice));
+    return CERES_OK;
+}
+
 // One batch: `frames` cameras (basis12 = frames x {eye, dir, iu, iv}) and suns (frames x 3).
 int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* sun, int mode, size_t W, size_t H,
            const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream,
@@ -1109,7 +1191,8 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     if (frames == 0 || frames > uint32_t(kMaxFrames))
         return set_error(CERES_EINVAL, "render: %u frames per batch (1..%d)", frames, kMaxFrames);
     const bool robust = (mode & CERES_MODE_ROBUST) != 0;            // RobustNodeIntersector traversal
-    mode &= ~CERES_MODE_ROBUST;
+    const bool qbvh = (mode & CERES_MODE_QBVH4) != 0;              // compressed shadow BVH4 (not exact)
+    mode &= ~(CERES_MODE_ROBUST | CERES_MODE_QBVH4);
     if (mode != CERES_MODE_FULL && mode != CERES_MODE_PRIMARY) return set_error(CERES_EINVAL, "render: bad mode %d", mode);
     if (W == 0 || H == 0 || W > 65535u * 16u || H > 0xffffffu) return set_error(CERES_EINVAL, "render: bad size %zux%zu", W, H);
     ceres_tiling t{uint32_t(H), 0, 1};
@@ -1121,7 +1204,11 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     if (size_t(by) * frames > 65535u) return set_error(CERES_EINVAL, "render: frames x row blocks exceeds the grid limit");
     if ((d_rec_prim != nullptr) != (d_rec_tuv != nullptr) || (d_rec_prim != nullptr) != (d_rec_shadow != nullptr))
         return set_error(CERES_EINVAL, "render: hit records need all three arrays");
+    if (qbvh && (robust || (s->flags & CERES_SCENE_STATS)))
+        return set_error(CERES_EUNSUPPORTED, "render: CERES_MODE_QBVH4 takes neither CERES_MODE_ROBUST nor a stats scene");
     HIP_TRY(hipSetDevice(s->device));
+    if (qbvh && mode == CERES_MODE_FULL && !s->d_qnodes4)
+        if (int rc = build_qnodes4(s)) return rc;
 
     KParams P{};
     for (uint32_t f = 0; f < frames; ++f) {
@@ -1138,6 +1225,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     P.shadow_stack_entries = s->shadow_stack_entries;
     P.root_leaf_count = s->root_leaf_count; P.root_leaf_first = s->root_leaf_first;
     P.pairs = s->d_pairs; P.nodes4 = s->d_nodes4; P.tris = s->d_tris; P.orig = s->d_orig; P.norms = s->d_norms;
+    P.qnodes4 = s->d_qnodes4;
     P.pixels = d_pixels; P.rgb8 = d_rgb8; P.shards = s->d_shards;
     P.rec_prim = d_rec_prim; P.rec_tuv = d_rec_tuv; P.rec_shadow = d_rec_shadow;
 
@@ -1194,6 +1282,14 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             constexpr int w16 = CERES_FUSED_MINW16, w32 = CERES_FUSED_MINW32;
             auto fused = [&](auto rt, auto st) {
                 constexpr bool R = decltype(rt)::value, T = decltype(st)::value;
+                if constexpr (!R) {
+                    if (qbvh) {                                      // compressed shadow BVH4 (non-stats, fast slabs)
+                        if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, false, T, true>), fgrid, fblock, flds, stream, P);
+                        else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, false, T, true>), fgrid, fblock, flds, stream, P);
+                        else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, false, T, true>), fgrid, fblock, flds, stream, P);
+                        return;
+                    }
+                }
                 if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, uint16_t*, 1, R, T>), fgrid, fblock, flds, stream, P);
                 else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
                 else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);

@@ -21,6 +21,7 @@ struct ceres_scene {
     size_t n_nodes4 = 0;
     SiblingPair* d_pairs = nullptr;
     Node4* d_nodes4 = nullptr;
+    ceres::QNode4* d_qnodes4 = nullptr;   // compressed shadow BVH4, built on first CERES_MODE_QBVH4 render
     // fused-kernel tile orders, one per (frame size, tiling, batch, tile), never rewritten or
     // freed while a launch that reads them may be in flight (launches on different streams may
     // read different orders concurrently): an evicted order's buffer goes to `retired` and is

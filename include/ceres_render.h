@@ -44,9 +44,17 @@ typedef enum {
 typedef enum {
     CERES_MODE_FULL = 0,     /* primary + shadow + smooth shading (render.hpp:104-153) */
     CERES_MODE_PRIMARY = 1,  /* primary rays only; pixel = |normalize(tri.n)| (render.hpp:123-125) */
-    CERES_MODE_ROBUST = 0x10 /* OR-ed flag: traverse with the library's RobustNodeIntersector
+    CERES_MODE_ROBUST = 0x10, /* OR-ed flag: traverse with the library's RobustNodeIntersector
                                 (node_intersectors.hpp:54-79) instead of render()'s FastNodeIntersector;
                                 float scenes only */
+    CERES_MODE_QBVH4 = 0x20  /* OR-ed flag (full mode, float, not with ROBUST): shadow rays traverse
+                                a COMPRESSED BVH4 -- 64-B nodes, child boxes quantised to 8 bits per
+                                bound, rounded outwards -- instead of the exact 128-B one.  Not
+                                bit-exact: a box can only grow, so every leaf the reference reaches
+                                is still tested, but a grazing shadow ray may also meet a triangle
+                                the reference's slab tests never reach (a lit pixel turns dark).
+                                Held to the SURVEY section 7 budget (+-1 LSB, <= 1e-5 of pixels),
+                                never the default (node_intersectors.hpp:35-47,83-103). */
 } ceres_mode;
 
 typedef struct ceres_scene ceres_scene;

@@ -40,17 +40,19 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     libs = sys.argv[3:] or [os.path.join(PKG_DIR, "libceres_hip.so")]
     meta, _, _ = load_golden(name)
-    builds = {os.path.basename(p): load_build(p, i) for i, p in enumerate(libs)}
+    # "lib.so@qbvh": the same build rendering with CERES_MODE_QBVH4 (parity then means the budget)
+    builds = {os.path.basename(p): load_build(p.split("@")[0], i) for i, p in enumerate(libs)}
+    qflag = {k: (m.MODE_QBVH4 if k.endswith("@qbvh") else 0) for k, m in builds.items()}
     first = next(iter(builds.values()))
     cfg = first.configs.CONFIGS[name]
     mesh, bvh, cam = first.prepare(cfg)
     bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
     basis = np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
-    mode = first.cfg_mode(cfg)
+    mode0 = first.cfg_mode(cfg)
     scenes = {k: m.Scene(mesh, bvh) for k, m in builds.items()}
     ok = {}
     for k, sc in scenes.items():
-        _, rgb, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=False)
+        _, rgb, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode0 | qflag[k], want_pixels=False)
         ok[k] = hashlib.sha256(builds[k].ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
     want_px = os.environ.get("AB_FLOAT", "1") == "1"
     res = {k: [] for k in scenes}
@@ -82,13 +84,14 @@ def main():
                 t0 = time.perf_counter()
                 for f in range(per):
                     i = f % n_streams
-                    sc.render_batch_device(b12, s3, W, H, mode=mode, d_pixels=px[i].data_ptr() if want_px else 0,
+                    sc.render_batch_device(b12, s3, W, H, mode=mode0 | qflag[k], d_pixels=px[i].data_ptr() if want_px else 0,
                                            d_rgb8=rgb[i].data_ptr(), stream=strs[i].cuda_stream)
                 torch.cuda.synchronize()
                 res[k].append((time.perf_counter() - t0) * 1e3 / (per * nb))
     for _ in range(0 if n_streams else rounds):
         for k, sc in scenes.items():
-            _, _, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode, want_pixels=want_px, want_rgb8=True)
+            _, _, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode0 | qflag[k], want_pixels=want_px,
+                                 want_rgb8=True)
             res[k].append(st["ms"])
     out = {k: {"median_ms": round(float(np.median(r)), 4), "min_ms": round(float(np.min(r)), 4),
                "mrays_s_median": round(meta["exact"]["rays"] / (np.median(r) * 1e3), 1), "parity": ok[k]}
