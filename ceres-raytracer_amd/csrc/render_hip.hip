@@ -46,6 +46,12 @@
 #ifndef CERES_FRAME_MAJOR_PIXELS
 #define CERES_FRAME_MAJOR_PIXELS (1u << 22)    // batches of frames of >= this many pixels: frame after frame (0: never)
 #endif
+#ifndef CERES_SHADOW_NEAREST_BATCH
+#define CERES_SHADOW_NEAREST_BATCH 0           // batch any-hit BVH4 steps: 1 = descend into the nearest passing child,
+#endif                                        // 0 = into the first (A/B: C3 batches -1.6 %, dragon 4096^2 -1.4 %)
+#ifndef CERES_SPLIT_UNIFORM
+#define CERES_SPLIT_UNIFORM 1                  // wave-uniform triangle / BVH4 fetches get their own copy of the test
+#endif
 #ifndef CERES_LOCAL_ORDER
 #define CERES_LOCAL_ORDER 1                    // XCD-local Morton tile order (ensure_tile_order); 0: never
 #endif
@@ -165,6 +171,17 @@ __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin,
         if (t >= tmin && t <= tmax) { t_out = t; u_out = u; v_out = v; return true; }
     }
     return false;
+}
+
+// tri_test on triangle `idx`, the wave-uniform case with its own copy of the test: the test
+// then reads the record from SGPRs instead of first copying the 12 scalar-loaded words into
+// VGPRs to join the vector path (12 v_mov per uniform test; CERES_SPLIT_UNIFORM)
+__device__ __forceinline__ bool tri_test_u(const Tri48* tris, uint32_t idx, F3 o, F3 d, float tmin, float tmax,
+                                           float& t_out, float& u_out, float& v_out) {
+    if (!CERES_SPLIT_UNIFORM) return tri_test(load_tri_u(tris, idx), o, d, tmin, tmax, t_out, u_out, v_out);
+    uint32_t r;
+    if (uniform_id(idx, r)) return tri_test(load_tri_s(tris + r), o, d, tmin, tmax, t_out, u_out, v_out);
+    return tri_test(load_tri(tris + idx), o, d, tmin, tmax, t_out, u_out, v_out);
 }
 
 // Per-ray constants of the ray-box (slab) test and the test of one box.
@@ -293,7 +310,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         while (k < k_end || k2 < k2_end) {
             const uint32_t idx = k < k_end ? k++ : k2++;
             float t, u, v;
-            if (tri_test(load_tri_u(P.tris, idx), o, d, tmin, tmax, t, u, v)) {
+            if (tri_test_u(P.tris, idx, o, d, tmin, tmax, t, u, v)) {
                 best = {idx, t, u, v}; have = true;
                 if (kAnyHit) return true;
                 tmax = t;
@@ -308,8 +325,8 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
 // Any-hit traversal of the shadow BVH4 (build_shadow_bvh4): result-identical to trace<true>
 // (see the equivalence argument there).  Per step: one 128-B record, four slab tests with the
 // same fma/min/max restatement as trace(), the triangles of every passing leaf, then descend
-// into the nearest passing inner child and push the others.  The order only changes how soon
-// an occluder is found, never whether one is.
+// into one passing inner child (the first, CERES_SHADOW_NEAREST_BATCH) and push the others.  The
+// order only changes how soon an occluder is found, never whether one is.
 struct N4 { float4 lx, hx, ly, hy, lz, hz; uint4 ch; };   // ch: packed child words (Node4::child)
 __device__ __forceinline__ N4 load_n4(const Node4* n) {
     const float4* q = reinterpret_cast<const float4*>(n);
@@ -370,24 +387,41 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
     uint32_t sp = 0, cur = 0;
     while (true) {
         if (kStats) ++n_pairs;
-        const N4 nd = load_shadow_node<kQ>(P, cur);
-        const float4 LX = nd.lx, HX = nd.hx, LY = nd.ly, HY = nd.hy, LZ = nd.lz, HZ = nd.hz;
-        const uint4 CH = nd.ch;
-        float e[4], x[4];
-        const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
-        const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
-        const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
-        const uint32_t chw[4] = {CH.x, CH.y, CH.z, CH.w};
+        float e[4];
+        uint32_t leaf_mask = 0, inner_mask = 0;
+        // the four slab tests of a record; the wave-uniform record gets its own copy that reads
+        // the scalar-loaded bounds from SGPRs (CERES_SPLIT_UNIFORM: no 28 v_mov to join the
+        // vector path)
+        auto classify = [&](const float4& LX, const float4& HX, const float4& LY, const float4& HY, const float4& LZ,
+                            const float4& HZ, const uint4& CH) {
+            const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
+            const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
+            const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
+            const uint32_t chw[4] = {CH.x, CH.y, CH.z, CH.w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float x;
+                slab_box<kRobust>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e[c], x);
+                const bool hit = e[c] <= x && chw[c] != kNode4Empty;
+                const bool leaf = n4_count(chw[c]) != 0;
+                leaf_mask |= (hit && leaf) ? (1u << c) : 0u;
+                inner_mask |= (hit && !leaf) ? (1u << c) : 0u;
+            }
+        };
+        uint4 CH;
+        uint32_t rc;
+        if (!kQ && CERES_SPLIT_UNIFORM && uniform_id(cur, rc)) {
+            const Node4* q = P.nodes4 + rc;
+            CH = sload_u4(q, 6);
+            classify(sload_f4(q, 0), sload_f4(q, 1), sload_f4(q, 2), sload_f4(q, 3), sload_f4(q, 4), sload_f4(q, 5), CH);
+            __asm__ volatile("; uniform BVH4 record" ::);               // keeps this copy from being merged with the other
+        } else {
+            const N4 nd = (!kQ && CERES_SPLIT_UNIFORM) ? load_n4(P.nodes4 + cur) : load_shadow_node<kQ>(P, cur);
+            CH = nd.ch;
+            classify(nd.lx, nd.hx, nd.ly, nd.hy, nd.lz, nd.hz, CH);
+        }
         const uint32_t cnt[4] = {n4_count(CH.x), n4_count(CH.y), n4_count(CH.z), n4_count(CH.w)};
         const uint32_t fst[4] = {n4_first(CH.x), n4_first(CH.y), n4_first(CH.z), n4_first(CH.w)};
-        uint32_t leaf_mask = 0, inner_mask = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            slab_box<kRobust>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e[c], x[c]);
-            const bool hit = e[c] <= x[c] && chw[c] != kNode4Empty;
-            leaf_mask |= (hit && cnt[c] != 0) ? (1u << c) : 0u;
-            inner_mask |= (hit && cnt[c] == 0) ? (1u << c) : 0u;
-        }
         // triangles of every passing leaf child, as one flattened loop (wave-coherent trip count)
         uint32_t k = 0, k_end = 0;
         while (true) {
@@ -400,17 +434,21 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
                 if (kStats) n_tests += k_end - k;
             }
             float t, u, v;
-            if (tri_test(load_tri_u(P.tris, k), o, d, tmin, tmax, t, u, v)) return true;
+            if (tri_test_u(P.tris, k, o, d, tmin, tmax, t, u, v)) return true;
             ++k;
         }
         if (inner_mask) {
-            // nearest passing inner child next; the others go on the stack
+            // one passing inner child next; the others go on the stack
+            // (any order gives the same answer; the nearest-first choice costs its selects in every
+            // step and the batch regime is issue-bound, so batches take the first passing child)
             uint32_t best = __builtin_ctz(inner_mask);
-            float be = e[0];
-            be = best == 1 ? e[1] : best == 2 ? e[2] : best == 3 ? e[3] : be;
+            if (CERES_SHADOW_NEAREST_BATCH) {
+                float be = e[0];
+                be = best == 1 ? e[1] : best == 2 ? e[2] : best == 3 ? e[3] : be;
 #pragma unroll
-            for (int c = 1; c < 4; ++c)
-                if ((inner_mask >> c & 1u) && e[c] < be) { be = e[c]; best = c; }
+                for (int c = 1; c < 4; ++c)
+                    if ((inner_mask >> c & 1u) && e[c] < be) { be = e[c]; best = c; }
+            }
             uint32_t rest = inner_mask & ~(1u << best);
             if (sp + __builtin_popcount(rest) > P.shadow_stack_entries) { overflow = true; return false; }
             while (rest) {
@@ -610,18 +648,31 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
         if (active && L.blocked[owner]) active = false;                 // another piece found an occluder
         if (active) {
             if (kStats) ++n_pairs;
-            const N4 n = load_shadow_node<kQ>(P, cur);
             float e[4];
             uint32_t leaf_mask = 0, inner_mask = 0;
+            auto classify = [&](const N4& n) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                float x;
-                slab_box<kRobust>(slab_of<kRobust>(w), pick(n.lx, c), pick(n.hx, c), pick(n.ly, c), pick(n.hy, c),
-                                  pick(n.lz, c), pick(n.hz, c), tmin, tmax, e[c], x);
-                const uint32_t w = pick(n.ch, c), cn = n4_count(w);
-                const bool hit = e[c] <= x && w != kNode4Empty;
-                leaf_mask |= (hit && cn != 0) ? (1u << c) : 0u;
-                inner_mask |= (hit && cn == 0) ? (1u << c) : 0u;
+                for (int c = 0; c < 4; ++c) {
+                    float x;
+                    slab_box<kRobust>(slab_of<kRobust>(w), pick(n.lx, c), pick(n.hx, c), pick(n.ly, c), pick(n.hy, c),
+                                      pick(n.lz, c), pick(n.hz, c), tmin, tmax, e[c], x);
+                    const uint32_t cw = pick(n.ch, c), cn = n4_count(cw);
+                    const bool hit = e[c] <= x && cw != kNode4Empty;
+                    leaf_mask |= (hit && cn != 0) ? (1u << c) : 0u;
+                    inner_mask |= (hit && cn == 0) ? (1u << c) : 0u;
+                }
+            };
+            N4 n;
+            uint32_t rc;
+            if (!kQ && CERES_SPLIT_UNIFORM && uniform_id(cur, rc)) {   // own copy: bounds read from SGPRs
+                const Node4* q = P.nodes4 + rc;
+                n = {sload_f4(q, 0), sload_f4(q, 1), sload_f4(q, 2), sload_f4(q, 3), sload_f4(q, 4), sload_f4(q, 5),
+                     sload_u4(q, 6)};
+                classify(n);
+                __asm__ volatile("; uniform BVH4 record" ::);
+            } else {
+                n = (!kQ && CERES_SPLIT_UNIFORM) ? load_n4(P.nodes4 + cur) : load_shadow_node<kQ>(P, cur);
+                classify(n);
             }
             bool found = false;
             uint32_t k = 0, k_end = 0;
@@ -635,13 +686,14 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
                     if (kStats) n_tests += k_end - k;
                 }
                 float t, u, v;
-                if (tri_test(load_tri_u(P.tris, k), w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
+                if (tri_test_u(P.tris, k, w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
                 ++k;
             }
             if (found) {
                 L.blocked[owner] = 1u;
                 active = false;
             } else if (inner_mask) {
+                // nearest first here: with work stealing it pays (first-child order: bunny solo +20 %)
                 uint32_t best = __builtin_ctz(inner_mask);
                 float be = best == 0 ? e[0] : best == 1 ? e[1] : best == 2 ? e[2] : e[3];
 #pragma unroll
