@@ -116,6 +116,8 @@ struct KParams {
     uint32_t row_blocks_per_frame;               // 16-row blocks of local rows per frame (primary grid.y)
     uint32_t stack_entries;
     uint32_t root_leaf_count, root_leaf_first;   // root is a leaf (single_ray_traverser.hpp:72-73)
+    float root_box[6];                           // the root node's bounds (bvh.hpp:25-30 order) ...
+    uint32_t root_box_ok;                        // ... and whether both root children lie inside it
     uint32_t shadow_stack_entries;               // BVH4 traversal stack (shadow rays)
     uint32_t tiles_x;                            // tile columns per row (fused kernel)
     uint32_t lds_entries;                        // fused kernel: LDS stack slots per lane (24-bit planes)
@@ -140,6 +142,7 @@ static_assert(sizeof(KParams) <= 4096, "KParams must fit the 4 KB kernel-argumen
 
 // device: reference BVH in HBM -> GPU layout (scene_device.hip); buffers hipMalloc'd
 struct DeviceLayout {
+    float root_box[6] = {0, 0, 0, 0, 0, 0};      // the reference root node's bounds
     SiblingPair* pairs = nullptr;
     Node4* nodes4 = nullptr;
     Tri48* tris = nullptr;

@@ -52,6 +52,9 @@
 #ifndef CERES_SPLIT_UNIFORM
 #define CERES_SPLIT_UNIFORM 1                  // wave-uniform triangle / BVH4 fetches get their own copy of the test
 #endif
+#ifndef CERES_ROOT_TEST
+#define CERES_ROOT_TEST 1                      // primary rays test the root box before the first record (set_root_box)
+#endif
 #ifndef CERES_LOCAL_ORDER
 #define CERES_LOCAL_ORDER 1                    // XCD-local Morton tile order (ensure_tile_order); 0: never
 #endif
@@ -268,6 +271,15 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         return have;
     }
     const Slab<kRobust> sl = make_slab<kRobust>(o, d);
+    if (P.root_box_ok) {                                              // exact early miss (set_root_box)
+        float e, x;
+        slab_box<kRobust>(sl, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
+                          P.root_box[5], tmin, tmax, e, x);
+        if (!(e <= x)) {
+            if (kStats) ++n_pairs;                                    // the reference's first step, both children missed
+            return false;
+        }
+    }
     uint32_t sp = 0;
     // Software-pipelined steps: the next record (near child or stack top) follows from this
     // step's box tests alone (the leaf hits only lower tmax for LATER steps, :89-121), so its
@@ -1234,6 +1246,19 @@ int build_qnodes4(ceres_scene* s) {
     return CERES_OK;
 }
 
+// The root box pre-test of primary rays (trace()): the reference never tests the root's own box
+// (single_ray_traverser.hpp:81 starts at its children), but when both children's boxes lie inside
+// it (exact float compare) a child box can pass the slab test only if the root box does -- the
+// test is monotone in the bounds (see build_shadow_bvh4) -- so a ray failing the root box would
+// fail both children in the reference's first step: same result, no record fetch.
+void set_root_box(ceres_scene* s, const float root[6], const SiblingPair& p0) {
+    for (int k = 0; k < 6; ++k) s->root_box[k] = root[k];
+    auto inside = [&](const float* c) {
+        return c[0] >= root[0] && c[1] <= root[1] && c[2] >= root[2] && c[3] <= root[3] && c[4] >= root[4] && c[5] <= root[5];
+    };
+    s->root_box_ok = (!s->root_leaf_count && inside(p0.lb) && inside(p0.rb)) ? 1u : 0u;
+}
+
 // One batch: `frames` cameras (basis12 = frames x {eye, dir, iu, iv}) and suns (frames x 3).
 int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* sun, int mode, size_t W, size_t H,
            const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream,
@@ -1276,6 +1301,8 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     P.stack_entries = s->stack_entries;
     P.shadow_stack_entries = s->shadow_stack_entries;
     P.root_leaf_count = s->root_leaf_count; P.root_leaf_first = s->root_leaf_first;
+    for (int k = 0; k < 6; ++k) P.root_box[k] = s->root_box[k];
+    P.root_box_ok = CERES_ROOT_TEST ? s->root_box_ok : 0u;
     P.pairs = s->d_pairs; P.nodes4 = s->d_nodes4; P.tris = s->d_tris; P.orig = s->d_orig; P.norms = s->d_norms;
     P.qnodes4 = s->d_qnodes4;
     P.pixels = d_pixels; P.rgb8 = d_rgb8; P.shards = s->d_shards;
@@ -1438,6 +1465,7 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     s->device = device; s->flags = flags; s->n_tri = n_tri; s->n_pairs = pairs.size();
     s->depth = depth; s->root_leaf_count = rlc; s->root_leaf_first = rlf;
     s->stack_entries = std::max<uint32_t>(1, depth);                 // stack <= depth - 1 entries
+    set_root_box(s, static_cast<const RefNode*>(nodes32)[0].bounds, pairs[0]);
     auto fail = [&]() -> ceres_scene* { scene_release(s); delete s; return nullptr; };
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { set_error(CERES_EHIP, "no HIP device available"); return fail(); }
@@ -1510,6 +1538,12 @@ ceres_scene* ceres_scene_create_device(const float* d_tri48, size_t n_tri, const
         s->depth = L.depth; s->root_leaf_count = L.root_leaf_count; s->root_leaf_first = L.root_leaf_first;
         s->stack_entries = std::max<uint32_t>(1, L.depth);           // stack <= depth - 1 entries
         s->shadow_stack_entries = std::max<uint32_t>(1, L.stack4);
+        if (!L.root_leaf_count) {
+            SiblingPair p0;
+            HIP_TRY(hipMemcpyAsync(&p0, L.pairs, sizeof p0, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            set_root_box(s, L.root_box, p0);
+        }
         L = DeviceLayout{};                                          // owned by the scene now
         HIP_TRY(hipMalloc(&s->d_norms, n_tri * 36));
         HIP_TRY(hipMemcpyAsync(s->d_norms, d_norm36, n_tri * 36, hipMemcpyDeviceToDevice, st));

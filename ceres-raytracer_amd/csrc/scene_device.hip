@@ -219,6 +219,7 @@ int relayout_device(const Tri48* d_tris, uint32_t n_tri, const RefNode* d_nodes,
         RefNode root;
         SD_TRY(hipMemcpyAsync(&root, d_nodes, sizeof root, hipMemcpyDeviceToHost, stream));
         SD_TRY(hipStreamSynchronize(stream));
+        for (int k = 0; k < 6; ++k) out.root_box[k] = root.bounds[k];
         out.root_leaf_count = out.root_leaf_first = 0;
         if (root.primitive_count) {                                  // the root is a leaf (single_ray_traverser.hpp:72-73)
             if (uint64_t(root.first_child_or_primitive) + root.primitive_count > n_tri) { rc = set_error(CERES_EINVAL, "root leaf range out of bounds"); goto done; }

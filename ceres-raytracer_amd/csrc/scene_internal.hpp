@@ -17,6 +17,8 @@ struct ceres_scene {
     uint32_t flags = 0;
     size_t n_tri = 0, n_pairs = 0;
     uint32_t depth = 0, stack_entries = 1, root_leaf_count = 0, root_leaf_first = 0;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};   // root node bounds; root_box_ok: both children inside it
+    uint32_t root_box_ok = 0;
     uint32_t shadow_stack_entries = 1;
     size_t n_nodes4 = 0;
     SiblingPair* d_pairs = nullptr;
