@@ -552,8 +552,10 @@ def test_concurrent_streams_render_identical_frames(gpu):
 def test_tile_order_eviction_under_concurrent_streams(gpu):
     """More distinct batch shapes than the scene caches tile orders for (kMaxTileOrders = 16,
     scene_internal.hpp), launched round-robin on four streams and repeated, so least-recently-used
-    orders are evicted and their buffers reused while other streams' launches are in flight --
-    every output still equals the same render done alone."""
+    orders are evicted -- their buffers RETIRED, not rewritten, while other streams' launches may
+    still read them -- and, after more than kMaxRetired (64) evictions, freed in bulk behind one
+    device synchronise while work is queued on the streams: every output still equals the same
+    render done alone."""
     import torch
     pkg = gpu
     name = "dragon_333x217"
@@ -579,7 +581,7 @@ def test_tile_order_eviction_under_concurrent_streams(gpu):
         refs.append(ref.cpu())
     streams = [torch.cuda.Stream() for _ in range(4)]
     outs = [torch.zeros_like(r, device="cuda") for r in refs]
-    for rep in range(3):
+    for rep in range(6):                       # ~110 evictions: the bulk free path runs at least once
         order = list(range(len(jobs))) if rep % 2 == 0 else list(reversed(range(len(jobs))))
         for q, j in enumerate(order):
             b, s, t = jobs[j]
