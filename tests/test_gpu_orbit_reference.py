@@ -39,7 +39,7 @@ def _scene(pkg, name):
     return _scenes[name]
 
 
-@pytest.mark.parametrize("name,world", [("dragon_1080", 1), ("dragon_1080", 2), ("dragon_1080", 4),
+@pytest.mark.parametrize("name,world", [("bunny_640", 1), ("dragon_1080", 1), ("dragon_1080", 2), ("dragon_1080", 4),
                                         ("dragon_1080", 8), ("bunny_1080", 1), ("bunny_1080_primary", 1),
                                         ("dragon_4096", 1), ("dragon_4096", 8), ("proc_c5", 1), ("proc_c5", 8)])
 def test_bench_step_frames_match_reference(pkg, name, world):

@@ -127,7 +127,7 @@ def test_golden_tiny_meshes_exist():
         assert os.path.exists(os.path.join(GOLDEN, f))
 
 
-@pytest.mark.parametrize("name", ["dragon_1080", "bunny_1080", "bunny_1080_primary", "dragon_4096", "proc_c5"])
+@pytest.mark.parametrize("name", ["bunny_640", "dragon_1080", "bunny_1080", "bunny_1080_primary", "dragon_4096", "proc_c5"])
 def test_bench_views_are_the_pinned_reference_poses(pkg, name):
     """Every view bench.py can time at N = 1, 2, 4, 8 (pkg.bench_views, F = 16N) is pinned in
     tests/golden/orbit/<cfg>.json, and the host's orbit pose (ceres_orbit_cameras, eye and sun)
