@@ -55,6 +55,9 @@
 #ifndef CERES_ROOT_TEST
 #define CERES_ROOT_TEST 1                      // primary rays test the root box before the first record (set_root_box)
 #endif
+#ifndef CERES_TRUST_STACK_BOUND
+#define CERES_TRUST_STACK_BOUND 1              // BVH2 steps of non-stats kernels: no stack clamps / overflow flag
+#endif
 #ifndef CERES_LOCAL_ORDER
 #define CERES_LOCAL_ORDER 1                    // XCD-local Morton tile order (ensure_tile_order); 0: never
 #endif
@@ -301,12 +304,20 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         // read at the start of the step, only the exit branches
         const bool both = go_l && go_r, none = !go_l && !go_r;
         const bool swap = le > re;                                    // near first, ties left (:109-115)
-        overflow |= both && sp >= P.stack_entries;
-        stk[(sp < P.stack_entries ? sp : P.stack_entries) * kS] = swap ? L.y : L.w;
         const bool done = none && sp == 0;                            // :118-121
         const uint32_t near = both ? (swap ? L.w : L.y) : (go_l ? L.y : L.w);   // :115-117
         const uint32_t nxt = none ? top : near;
-        sp = both ? (sp < P.stack_entries ? sp + 1 : sp) : (none ? (sp ? sp - 1 : 0) : sp);
+        if (kStats || !CERES_TRUST_STACK_BOUND) {
+            overflow |= both && sp >= P.stack_entries;
+            stk[(sp < P.stack_entries ? sp : P.stack_entries) * kS] = swap ? L.y : L.w;
+            sp = both ? (sp < P.stack_entries ? sp + 1 : sp) : (none ? (sp ? sp - 1 : 0) : sp);
+        } else {
+            // the scene's stack bound is exact (a push per level descended: at most depth - 1
+            // entries, stack_entries = depth), so the production kernels skip the clamps; the
+            // stats kernels (records, statistics: every parity test config) keep the check
+            stk[sp * kS] = swap ? L.y : L.w;
+            sp = sp + (both ? 1u : 0u) - (none ? 1u : 0u);            // none && sp == 0 exits (done)
+        }
         // leaves of this step, left then right (intersect_leaf on each, :89-107), one loop so a
         // wavefront runs max(left + right) trips rather than max(left) + max(right)
         uint32_t k = 0, k_end = 0, k2 = 0, k2_end = 0;
