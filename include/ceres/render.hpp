@@ -76,7 +76,7 @@ using HostBvh64 = BasicHostBvh<double>;
 namespace detail {
 
 struct SceneCache {
-    const void *bvh = nullptr, *tris = nullptr, *norms = nullptr;
+    const void *bvh = nullptr, *tris = nullptr, *norms = nullptr, *nodes = nullptr;
     size_t node_count = 0, n_tri = 0;
     bool f64 = false;
     uint64_t fingerprint = 0;
@@ -140,14 +140,25 @@ std::pair<int, int> render(const Camera<Scalar>& camera, const Vec& sun_position
     const auto* nodes = bvh.nodes.get();
     const size_t n_nodes = bvh.node_count;
     static_assert(sizeof(*nodes) == 8 * sizeof(Scalar), "bvh node must be bvh::Bvh<Scalar>::Node layout");
-    // triangle count = end of the furthest leaf (the reference never passes it explicitly)
-    size_t n_tri = 0;
-    for (size_t k = 0; k < n_nodes; ++k)
-        if (nodes[k].primitive_count)
-            n_tri = std::max<size_t>(n_tri, size_t(nodes[k].first_child_or_primitive) + size_t(nodes[k].primitive_count));
+    // triangle count = end of the furthest leaf (the reference never passes it explicitly): a scan
+    // of every node, done again only when the cached scene's BVH identity or fingerprint changes
+    // (a 10M-triangle BVH has 20M nodes: the scan alone would cost tens of ms per call)
+    auto scan_n_tri = [&] {
+        size_t n = 0;
+        for (size_t k = 0; k < n_nodes; ++k)
+            if (nodes[k].primitive_count)
+                n = std::max<size_t>(n, size_t(nodes[k].first_child_or_primitive) + size_t(nodes[k].primitive_count));
+        return n;
+    };
     auto& c = ceres::detail::cache();
     std::lock_guard<std::mutex> lock(c.mu);
-    const uint64_t fp = ceres::detail::fingerprint(nodes, n_nodes, sizeof(*nodes), triangles, n_tri, sizeof(TriT));
+    const bool same_bvh = c.scene && c.bvh == &bvh && c.nodes == nodes && c.node_count == n_nodes && c.f64 == kF64;
+    size_t n_tri = same_bvh ? c.n_tri : scan_n_tri();
+    uint64_t fp = ceres::detail::fingerprint(nodes, n_nodes, sizeof(*nodes), triangles, n_tri, sizeof(TriT));
+    if (same_bvh && fp != c.fingerprint) {                            // edited in place: full rescan
+        n_tri = scan_n_tri();
+        fp = ceres::detail::fingerprint(nodes, n_nodes, sizeof(*nodes), triangles, n_tri, sizeof(TriT));
+    }
     if (!c.scene || c.bvh != &bvh || c.tris != triangles || c.norms != tri_norms || c.node_count != n_nodes ||
         c.n_tri != n_tri || c.fingerprint != fp || c.f64 != kF64) {
         if (c.scene) ceres_scene_destroy(c.scene);
@@ -157,7 +168,8 @@ std::pair<int, int> render(const Camera<Scalar>& camera, const Vec& sun_position
                        : ceres_scene_create(reinterpret_cast<const float*>(triangles), n_tri,
                                             reinterpret_cast<const float*>(tri_norms), nodes, n_nodes, prim, 0, 0);
         if (!c.scene) ceres::detail::fail("ceres_scene_create");
-        c.bvh = &bvh; c.tris = triangles; c.norms = tri_norms; c.node_count = n_nodes; c.n_tri = n_tri; c.fingerprint = fp;
+        c.bvh = &bvh; c.nodes = nodes; c.tris = triangles; c.norms = tri_norms; c.node_count = n_nodes; c.n_tri = n_tri;
+        c.fingerprint = fp;
         c.f64 = kF64;
     }
     Scalar eye[3] = {Scalar(camera.eye[0]), Scalar(camera.eye[1]), Scalar(camera.eye[2])};
