@@ -7,19 +7,22 @@
 // plus the PPM quantiser of static.cpp:135-147.
 //
 // Full mode: ONE kernel per batch of frames, ceres_fused (DESIGN.md "Kernels"): one 64-thread
-// workgroup per 8x8 pixel tile (coherent primary rays), tiles walked centre-first; closest-hit
-// BVH2 traversal per pixel (software-pipelined: the next record is loaded before the step's
-// triangle tests), then the tile's shadow rays over an exact BVH4 collapse (any-hit: only the
-// boolean matters, render.hpp:139; one-frame launches share the rays' work among the lanes),
-// then shading of the lit pixels.  Primary-only mode (C2): ceres_primary.
+// workgroup per 8x8 pixel tile (coherent primary rays), tiles walked centre-first (views of
+// >= 4 Mpixel: frame after frame, XCD-local Morton order for batches and DRAM-resident scenes);
+// an exact root-box pre-test, then closest-hit BVH2 traversal per pixel (software-pipelined: the
+// next record is loaded before the step's triangle tests), then the tile's shadow rays over an
+// exact BVH4 collapse (any-hit: only the boolean matters, render.hpp:139; one-frame launches
+// share the rays' work among the lanes), then shading of the lit pixels.  Primary-only mode
+// (C2): ceres_primary.  CERES_MODE_QBVH4: shadow rays over a compressed BVH4 (not exact).
 // A batch is 1..kMaxFrames frames (own camera + sun each, e.g. the anim.cpp:93-110 orbit),
 // each restricted to this rank's rows (ceres_tiling).
 // Traversal stacks live in LDS ([entries][lanes], lane-contiguous = bank-conflict free),
 // sized from the BVH at scene creation, 16-bit entries when every node index fits.
 //
 // Numerics: compiled with -ffp-contract=off and correctly rounded f32 div/sqrt, explicit
-// fmaf only where the reference calls fast_multiply_add, x^24 in double-double for std::pow
-// (pow24.hpp) -- every float matches the reference compiled without contraction bit for bit.
+// fmaf only where the reference calls fast_multiply_add, x^24 in double for std::pow (pow24.hpp,
+// exhaustively equal to glibc for every float) -- every float matches the reference compiled
+// without contraction bit for bit.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,6 +57,9 @@
 #endif
 #ifndef CERES_ROOT_TEST
 #define CERES_ROOT_TEST 1                      // primary rays test the root box before the first record (set_root_box)
+#endif
+#ifndef CERES_STEAL_BATCH
+#define CERES_STEAL_BATCH 0                    // 1: batches use the work-stealing shadow pass too (A/B only)
 #endif
 #ifndef CERES_TRUST_STACK_BOUND
 #define CERES_TRUST_STACK_BOUND 1              // BVH2 steps of non-stats kernels: no stack clamps / overflow flag
@@ -1352,7 +1358,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
             // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
-            const bool steal = frames == 1;
+            const bool steal = frames == 1 || CERES_STEAL_BATCH;
             const uint32_t tpw = (!stats && !steal) ? CERES_TILES_PER_WAVE : 1;   // = kTPW
             const uint32_t n_tiles = fbx * fby * frames;
             const dim3 fgrid((n_tiles + tpw - 1) / tpw), fblock(dev::kFusedB);
