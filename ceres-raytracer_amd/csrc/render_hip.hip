@@ -58,9 +58,6 @@
 #ifndef CERES_ROOT_TEST
 #define CERES_ROOT_TEST 1                      // primary rays test the root box before the first record (set_root_box)
 #endif
-#ifndef CERES_STEAL_BATCH
-#define CERES_STEAL_BATCH 0                    // 1: batches use the work-stealing shadow pass too (A/B only)
-#endif
 #ifndef CERES_TRUST_STACK_BOUND
 #define CERES_TRUST_STACK_BOUND 1              // BVH2 steps of non-stats kernels: no stack clamps / overflow flag
 #endif
@@ -609,7 +606,10 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 }
 
 #ifndef CERES_FUSED_MINW16
-#define CERES_FUSED_MINW16 6     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes (no-SLP build: 6 waves / 80 VGPRs beat 7 / 72 with spills: bench +0.7 %)
+#define CERES_FUSED_MINW16 6     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes, batch kernel (no-SLP build: 6 waves / 80 VGPRs beat 7 / 72 with spills: bench +0.7 %)
+#endif
+#ifndef CERES_FUSED_MINW16_SOLO
+#define CERES_FUSED_MINW16_SOLO 6  // ... and the work-stealing single-frame kernel
 #endif
 #ifndef CERES_FUSED_MINW32
 #define CERES_FUSED_MINW32 1     // ... and 32-bit-stack scenes (1 = no constraint)
@@ -1358,7 +1358,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
             // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
-            const bool steal = frames == 1 || CERES_STEAL_BATCH;
+            const bool steal = frames == 1;
             const uint32_t tpw = (!stats && !steal) ? CERES_TILES_PER_WAVE : 1;   // = kTPW
             const uint32_t n_tiles = fbx * fby * frames;
             const dim3 fgrid((n_tiles + tpw - 1) / tpw), fblock(dev::kFusedB);
@@ -1375,9 +1375,10 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             }
             // VGPR budgets: 16-bit-stack scenes (LDS for 7+ waves/SIMD) are compiled for 6 waves,
             // C5-size scenes keep the unconstrained allocation
-            constexpr int w16 = CERES_FUSED_MINW16, w32 = CERES_FUSED_MINW32;
+            constexpr int w32 = CERES_FUSED_MINW32;
             auto fused = [&](auto rt, auto st) {
                 constexpr bool R = decltype(rt)::value, T = decltype(st)::value;
+                constexpr int w16 = T ? CERES_FUSED_MINW16_SOLO : CERES_FUSED_MINW16;
                 if constexpr (!R) {
                     if (qbvh) {                                      // compressed shadow BVH4 (non-stats, fast slabs)
                         if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, false, T, true>), fgrid, fblock, flds, stream, P);
