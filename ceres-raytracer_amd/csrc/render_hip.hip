@@ -609,7 +609,7 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 #define CERES_FUSED_MINW16 6     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes, batch kernel (no-SLP build: 6 waves / 80 VGPRs beat 7 / 72 with spills: bench +0.7 %)
 #endif
 #ifndef CERES_FUSED_MINW16_SOLO
-#define CERES_FUSED_MINW16_SOLO 6  // ... and the work-stealing single-frame kernel
+#define CERES_FUSED_MINW16_SOLO 7  // ... and the work-stealing single-frame kernel (72 VGPRs, no VGPR spill: dragon 4096^2 -4 %, bunny -1.5 %, C3 +-1 %)
 #endif
 #ifndef CERES_FUSED_MINW32
 #define CERES_FUSED_MINW32 1     // ... and 32-bit-stack scenes (1 = no constraint)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B kernel builds in ONE process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
 
-usage: python tools/ab.py [config] [rounds] [lib.so ...]
+usage: python tools/ab.py [config] [rounds] [lib.so[@qbvh][#tag] ...]
 Each argument is a build of libceres_hip.so (default: the in-tree one), e.g. one made with
 `make -C ceres-raytracer_amd/csrc variant VARIANT=x DEFS=-DFOO`.  Every build is loaded as its
 own module instance (own ctypes handle, own HIP code object) and renders the config
@@ -40,9 +40,11 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     libs = sys.argv[3:] or [os.path.join(PKG_DIR, "libceres_hip.so")]
     meta, _, _ = load_golden(name)
-    # "lib.so@qbvh": the same build rendering with CERES_MODE_QBVH4 (parity then means the budget)
-    builds = {os.path.basename(p): load_build(p.split("@")[0], i) for i, p in enumerate(libs)}
-    qflag = {k: (m.MODE_QBVH4 if k.endswith("@qbvh") else 0) for k, m in builds.items()}
+    # "lib.so@qbvh": the same build rendering with CERES_MODE_QBVH4 (parity then means the budget);
+    # "lib.so#2": a second instance of the same build (own scene copy: an A/A check of how much the
+    # scene's placement in memory moves the timings)
+    builds = {os.path.basename(p): load_build(p.split("#")[0].split("@")[0], i) for i, p in enumerate(libs)}
+    qflag = {k: (m.MODE_QBVH4 if "@qbvh" in k else 0) for k, m in builds.items()}
     first = next(iter(builds.values()))
     cfg = first.configs.CONFIGS[name]
     mesh, bvh, cam = first.prepare(cfg)

@@ -3,7 +3,7 @@
 # session stops at the first failure.  Outputs under gpurun_out/$TAG/.
 #   TAG=name  AB="cfg ..." (configs for tools/ab.py, solo and 16-frame batches x 8 streams)
 #   AB_LIBS="ceres-raytracer_amd/libceres_hip.so ceres-raytracer_amd/variants/libceres_hip_x.so"
-#   SKIP_TESTS=1  BENCH_ARGS="--steps 20 --warmup 5"  EXTRA="cmd" (one more command, 300 s)
+#   AB_MODES="solo batch" (default both)  SKIP_TESTS=1  BENCH_ARGS="--steps 20 --warmup 5"  EXTRA="cmd" (one more command, 300 s)
 set -u
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-check}; mkdir -p "$OUT"
@@ -14,9 +14,10 @@ if [ -z "${SKIP_TESTS:-}" ]; then
   step 300 smoke python -c "import __graft_entry__ as g; g.smoke()"
   step 600 pytest_gpu python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread
 fi
+M="${AB_MODES:-solo batch}"
 for c in ${AB:-}; do
-  step 300 ab_solo_$c python tools/ab.py $c ${AB_ROUNDS:-20} ${AB_LIBS:-}
-  AB_STREAMS=8 AB_FRAMES=16 AB_BATCH=16 step 300 ab_batch_$c python tools/ab.py $c ${AB_ROUNDS:-8} ${AB_LIBS:-}
+  [ "$M" != "${M/solo/}" ] && step 300 ab_solo_$c python tools/ab.py $c ${AB_ROUNDS:-20} ${AB_LIBS:-}
+  [ "$M" != "${M/batch/}" ] && AB_STREAMS=8 AB_FRAMES=16 AB_BATCH=16 step 300 ab_batch_$c python tools/ab.py $c ${AB_ROUNDS:-8} ${AB_LIBS:-}
 done
 if [ -n "${EXTRA:-}" ]; then step 300 extra bash -c "$EXTRA"; fi
 if [ -z "${NO_BENCH:-}" ]; then step 300 bench python bench.py ${BENCH_ARGS:-}; fi
