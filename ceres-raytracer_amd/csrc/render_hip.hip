@@ -58,6 +58,10 @@
 #ifndef CERES_ROOT_TEST
 #define CERES_ROOT_TEST 1                      // primary rays test the root box before the first record (set_root_box)
 #endif
+#ifndef CERES_OCTANT_SLAB
+#define CERES_OCTANT_SLAB 3                    // traversal loops specialised per wave-uniform ray octant:
+                                               // 1 BVH2, 2 shadow BVH4 (multi-frame kernel), 4 also in the single-frame kernel
+#endif
 #ifndef CERES_TRUST_STACK_BOUND
 #define CERES_TRUST_STACK_BOUND 1              // BVH2 steps of non-stats kernels: no stack clamps / overflow flag
 #endif
@@ -225,11 +229,21 @@ __device__ __forceinline__ Slab<kRobust> make_slab(F3 o, F3 d) {
     s.o = o;
     return s;
 }
-// entry / exit distances of one box (bounds lo, hi per axis); hit iff e <= x
-template <bool kRobust>
+// entry / exit distances of one box (bounds lo, hi per axis); hit iff e <= x.
+// kOct >= 0 (fast test only): the ray octant is known at compile time -- bit a set when axis a's
+// inverse direction is negative -- and each axis's entry / exit bound is picked by it, as the
+// reference's NodeIntersector does (node_intersectors.hpp:35-47): three fmas per side and no
+// per-axis min / max (16 -> 10 VALU per box).
+template <bool kRobust, int kOct = -1>
 __device__ __forceinline__ void slab_box(const Slab<kRobust>& s, float lox, float hix, float loy, float hiy, float loz,
                                          float hiz, float tmin, float tmax, float& e, float& x) {
-    if constexpr (kRobust) {
+    if constexpr (!kRobust && kOct >= 0) {
+        const float nx = (kOct & 1) ? hix : lox, fx = (kOct & 1) ? lox : hix;
+        const float ny = (kOct & 2) ? hiy : loy, fy = (kOct & 2) ? loy : hiy;
+        const float nz = (kOct & 4) ? hiz : loz, fz = (kOct & 4) ? loz : hiz;
+        e = fmaxf(__builtin_fmaf(nx, s.ix, s.sx), fmaxf(__builtin_fmaf(ny, s.iy, s.sy), fmaxf(__builtin_fmaf(nz, s.iz, s.sz), tmin)));
+        x = fminf(__builtin_fmaf(fx, s.ix, s.sx), fminf(__builtin_fmaf(fy, s.iy, s.sy), fminf(__builtin_fmaf(fz, s.iz, s.sz), tmax)));
+    } else if constexpr (kRobust) {
         const bool nx = __float_as_uint(s.ix) >> 31, ny = __float_as_uint(s.iy) >> 31, nz = __float_as_uint(s.iz) >> 31;
         const float ex = ((nx ? hix : lox) - s.o.x) * s.ix, xx = ((nx ? lox : hix) - s.o.x) * s.sx;
         const float ey = ((ny ? hiy : loy) - s.o.y) * s.iy, xy = ((ny ? loy : hiy) - s.o.y) * s.sy;
@@ -245,6 +259,27 @@ __device__ __forceinline__ void slab_box(const Slab<kRobust>& s, float lox, floa
     }
 }
 
+// The octant of a fast slab (see slab_box) and, when every active lane of the wavefront shares it,
+// fn(std::integral_constant<int, octant>) -- the traversal loop instantiated for that octant; else
+// false.  Primary rays of an 8x8 tile and the shadow rays of its hits nearly always share one.
+template <typename Fn>
+__device__ __forceinline__ bool with_uniform_octant(const Slab<false>& s, Fn&& fn) {
+    const uint32_t oct = (__float_as_uint(s.ix) >> 31) | (__float_as_uint(s.iy) >> 31) << 1 | (__float_as_uint(s.iz) >> 31) << 2;
+    uint32_t r;
+    if (!uniform_id(oct, r)) return false;
+    switch (r) {
+        case 0: fn(std::integral_constant<int, 0>{}); break;
+        case 1: fn(std::integral_constant<int, 1>{}); break;
+        case 2: fn(std::integral_constant<int, 2>{}); break;
+        case 3: fn(std::integral_constant<int, 3>{}); break;
+        case 4: fn(std::integral_constant<int, 4>{}); break;
+        case 5: fn(std::integral_constant<int, 5>{}); break;
+        case 6: fn(std::integral_constant<int, 6>{}); break;
+        default: fn(std::integral_constant<int, 7>{}); break;
+    }
+    return true;
+}
+
 // Eager BVH2 traversal, single_ray_traverser.hpp:68-126 with FastNodeIntersector
 // (node_intersectors.hpp:35-47,83-103).  Exactly the reference's visiting order: both
 // children's slab tests use the tmax from before this step's leaves; left leaf triangles,
@@ -258,7 +293,7 @@ __device__ __forceinline__ void slab_box(const Slab<kRobust>& s, float lox, floa
 // whenever y is not NaN (y is tmin / tmax / a previous robust_max -- never NaN) up to the
 // sign of zero, which no comparison below can observe; likewise robust_min and fminf.  The
 // slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
-template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false>
+template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, int kOct = -1>
 __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hit& best,
                                       uint32_t& n_pairs, uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f;
@@ -277,9 +312,16 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         return have;
     }
     const Slab<kRobust> sl = make_slab<kRobust>(o, d);
+    if constexpr (!kRobust && kOct == -1 && (CERES_OCTANT_SLAB & 1)) {
+        bool r = false;
+        if (with_uniform_octant(sl, [&](auto k) {
+                r = trace<kAnyHit, kStats, kS, StkT, kRobust, decltype(k)::value>(P, o, d, stk, best, n_pairs, n_tests, overflow);
+            }))
+            return r;
+    }
     if (P.root_box_ok) {                                              // exact early miss (set_root_box)
         float e, x;
-        slab_box<kRobust>(sl, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
+        slab_box<kRobust, kOct>(sl, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
                           P.root_box[5], tmin, tmax, e, x);
         if (!(e <= x)) {
             if (kStats) ++n_pairs;                                    // the reference's first step, both children missed
@@ -298,8 +340,8 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];             // popped if this step descends nowhere
         // left bounds A.x A.y | A.z A.w | B.x B.y ; right bounds B.z B.w | C.x C.y | C.z C.w
         float le, lx, re, rx;
-        slab_box<kRobust>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
-        slab_box<kRobust>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
+        slab_box<kRobust, kOct>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
+        slab_box<kRobust, kOct>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
         const bool hit_l = le <= lx, hit_r = re <= rx;
         const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
         // the three cases as selects: the far child is written to slot sp every step (a free slot
@@ -401,7 +443,7 @@ __device__ __forceinline__ N4 load_shadow_node(const KParams& P, uint32_t cur) {
 __device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 __device__ __forceinline__ uint32_t pick(uint4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 
-template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, bool kQ = false>
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, bool kQ = false, int kOct = -1>
 __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT stk, uint32_t& n_pairs,
                                            uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f, tmax = FLT_MAX;
@@ -410,6 +452,13 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
         return trace<true, kStats, kS, StkT, kRobust>(P, o, d, stk, h, n_pairs, n_tests, overflow);
     }
     const Slab<kRobust> sl = make_slab<kRobust>(o, d);
+    if constexpr (!kRobust && kOct == -1 && (CERES_OCTANT_SLAB & 2)) {
+        bool r = false;
+        if (with_uniform_octant(sl, [&](auto k) {
+                r = trace_any4<kStats, kS, StkT, kRobust, kQ, decltype(k)::value>(P, o, d, stk, n_pairs, n_tests, overflow);
+            }))
+            return r;
+    }
     uint32_t sp = 0, cur = 0;
     while (true) {
         if (kStats) ++n_pairs;
@@ -427,7 +476,7 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 float x;
-                slab_box<kRobust>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e[c], x);
+                slab_box<kRobust, kOct>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e[c], x);
                 const bool hit = e[c] <= x && chw[c] != kNode4Empty;
                 const bool leaf = n4_count(chw[c]) != 0;
                 leaf_mask |= (hit && leaf) ? (1u << c) : 0u;
@@ -885,7 +934,9 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
     if (active) {
         const F3 view = primary_dir(P, f, i, global_row(P, lr));
-        hit = trace<false, kStats, kB, StkT, kRobust>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
+        // kOct -1: the traversal dispatches on a wave-uniform octant; -2: generic loop only
+        constexpr int kOctMode = (!kSteal || (CERES_OCTANT_SLAB & 4)) ? -1 : -2;
+        hit = trace<false, kStats, kB, StkT, kRobust, kOctMode>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
             P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
