@@ -119,6 +119,7 @@ struct KParams {
     float root_box[6];                           // the root node's bounds (bvh.hpp:25-30 order) ...
     uint32_t root_box_ok;                        // ... and whether both root children lie inside it
     uint32_t shadow_stack_entries;               // BVH4 traversal stack (shadow rays)
+    uint32_t packets;                            // batch kernel: wave-wide packets (L2-resident scenes, render_hip.hip)
     uint32_t tiles_x;                            // tile columns per row (fused kernel)
     uint32_t lds_entries;                        // fused kernel: LDS stack slots per lane (24-bit planes)
     const uint32_t* tile_order;                  // fused kernel: block -> batch tile (centre first)

@@ -62,6 +62,15 @@
 #define CERES_OCTANT_SLAB 3                    // traversal loops specialised per wave-uniform ray octant:
                                                // 1 BVH2, 2 shadow BVH4 (multi-frame kernel), 4 also in the single-frame kernel
 #endif
+#ifndef CERES_SHADOW_PACKET
+#define CERES_SHADOW_PACKET 1                  // batch kernel: a tile's shadow rays as one wave-wide masked packet (packet_any4)
+#endif
+#ifndef CERES_SHADOW_PACKET_SOLO
+#define CERES_SHADOW_PACKET_SOLO 0             // ... in the single-frame (work-stealing) kernel too
+#endif
+#ifndef CERES_PACKET_ORDER
+#define CERES_PACKET_ORDER 0                   // packet_any4: 0 = first passing inner child next, 1 = the one with most lanes
+#endif
 #ifndef CERES_TRUST_STACK_BOUND
 #define CERES_TRUST_STACK_BOUND 1              // BVH2 steps of non-stats kernels: no stack clamps / overflow flag
 #endif
@@ -542,6 +551,100 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
     return false;
 }
 
+// Any-hit of a whole wavefront's shadow rays as ONE masked packet over the shadow BVH4 (batch
+// kernel).  The 8x8 tile's shadow rays start at neighbouring hit points and run to the same sun,
+// so they reach nearly the same nodes: the wavefront walks the union of their paths once, every
+// record and triangle read through the scalar cache (one wave-uniform s_load, no vector-memory
+// traffic), each lane testing its own ray, and the lane masks (a v_cmp result IS the mask)
+// decide where to go.  A ray's answer is "some leaf triangle it reaches is hit" -- every leaf
+// whose box chain its ray passes is still tested for it (its lane is in the mask of every node
+// on that chain, the slab test being the same per-lane arithmetic as trace_any4's) and the order
+// of the tests never changes an any-hit result (render.hpp:137-139 uses only the boolean), so the
+// occluded set equals trace_any4's bit for bit.  A lane leaves the masks once it is occluded.
+// The stack of (node, mask) entries is wave-uniform: entry k lives in lane k of three VGPRs
+// (a select on lane == sp / v_readlane, no memory); it holds at most shadow_stack_entries (the most pushes
+// along any root-leaf path, build_shadow_bvh4) -- the host only takes this path when <= 64.
+// `act`: lanes with a shadow ray; their o / slab in every lane (others: copies of an active one).
+template <int kOct>
+__device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<false>& sl, F3 o, F3 d, uint64_t act,
+                                                uint32_t lane) {
+    constexpr float tmin = 0.0f, tmax = FLT_MAX;
+    uint64_t occ = 0, m = act;
+    uint32_t cur = 0, sp = 0;
+    int s_node = 0, s_lo = 0, s_hi = 0;                               // stack entry k in lane k
+    while (true) {
+        const Node4* q = P.nodes4 + cur;
+        const float4 LX = sload_f4(q, 0), HX = sload_f4(q, 1), LY = sload_f4(q, 2), HY = sload_f4(q, 3);
+        const float4 LZ = sload_f4(q, 4), HZ = sload_f4(q, 5);
+        const uint4 CH = sload_u4(q, 6);
+        const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
+        const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
+        const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
+        const uint32_t chw[4] = {CH.x, CH.y, CH.z, CH.w};
+        uint64_t cm[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float e, x;
+            slab_box<false, kOct>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e, x);
+            cm[c] = chw[c] != kNode4Empty ? (__ballot(e <= x) & m) : 0;
+        }
+        // triangles of every passing leaf child, for the lanes that reach it and are not yet occluded
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t n = n4_count(chw[c]);
+            uint64_t lm = cm[c] & ~occ;
+            if (!n || !lm) continue;
+            for (uint32_t k = n4_first(chw[c]), ke = k + n; k < ke && lm; ++k) {
+                float t, u, v;
+                const Tri48* tp = P.tris + k;
+                const float4 a = sload_f4(tp, 0), b = sload_f4(tp, 1), g = sload_f4(tp, 2);
+                // all 48 B in flight before the first use (one scalar-load wait per triangle, not two)
+                __asm__ volatile("" ::"s"(a.x), "s"(b.x), "s"(g.x));
+                const TriV tr{{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, g.x}, {g.y, g.z, g.w}};
+                const bool h = tri_test(tr, o, d, tmin, tmax, t, u, v);
+                occ |= __ballot(h) & lm;
+                lm &= ~occ;
+            }
+        }
+        // one passing inner child next (the first), the others onto the stack with their masks
+        int nxt = -1;
+        uint64_t nm = 0;
+        if (CERES_PACKET_ORDER) {
+            int most = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint64_t mm = n4_count(chw[c]) ? 0 : cm[c] & ~occ;
+                const int pc = __builtin_popcountll(mm);
+                if (pc > most) { most = pc; nxt = c; nm = mm; }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint64_t mm = n4_count(chw[c]) ? 0 : cm[c] & ~occ;
+            if (!mm || c == nxt) continue;
+            if (nxt < 0) { nxt = c; nm = mm; continue; }
+            const bool mine = lane == sp;                              // a write into lane sp
+            s_node = mine ? int(n4_first(chw[c])) : s_node;
+            s_lo = mine ? int(uint32_t(mm)) : s_lo;
+            s_hi = mine ? int(uint32_t(mm >> 32)) : s_hi;
+            ++sp;
+        }
+        if (nxt >= 0) {
+            cur = n4_first(chw[nxt]);
+            m = nm;
+            continue;
+        }
+        m = 0;
+        while (sp) {                                                    // pop until a mask has live lanes
+            --sp;
+            m = (uint64_t(uint32_t(__builtin_amdgcn_readlane(s_hi, int(sp)))) << 32 |
+                 uint32_t(__builtin_amdgcn_readlane(s_lo, int(sp)))) & ~occ;
+            if (m) { cur = uint32_t(__builtin_amdgcn_readlane(s_node, int(sp))); break; }
+        }
+        if (!m) return occ;
+    }
+}
+
 __device__ __forceinline__ uint8_t quantize(float x) {               // static.cpp:141-143
     const float a = x * 255;
     const float m = (255.0f < a) ? 255.0f : a;                       // std::min(a, 255)
@@ -844,6 +947,40 @@ __device__ __forceinline__ RayWork make_shadow_ray(F3 o, F3 sun) {
     return w;
 }
 
+// A tile's shadow rays as one packet_any4 when every lane with a shadow ray shares one ray octant
+// (nearly every tile), the scene is L2-resident (P.packets) and the packet stack fits the 64
+// lanes: returns true and this lane's answer in `blocked`; false (nothing traced) otherwise.
+template <typename StkT, bool kRobust, bool kQ>
+__device__ __forceinline__ bool shadow_packet(const KParams& P, bool hit, const RayWork& w, uint32_t lane, bool& blocked) {
+    if constexpr (!kRobust && !kQ && CERES_SHADOW_PACKET && std::is_same<StkT, uint16_t*>::value) {
+        const uint64_t act = __ballot(hit);
+        if (!act) { blocked = false; return true; }
+        const uint32_t oct = (__float_as_uint(w.ix) >> 31) | (__float_as_uint(w.iy) >> 31) << 1 |
+                             (__float_as_uint(w.iz) >> 31) << 2;
+        const int first = __builtin_ctzll(act);
+        const uint32_t oct0 = uint32_t(__builtin_amdgcn_readlane(int(oct), first));
+        if (!P.packets || P.shadow_stack_entries > 64 || P.root_leaf_count || __ballot(hit && oct != oct0)) return false;
+        // lanes without a shadow ray take a copy of the first one's (masked out, but finite)
+        auto bc = [&](float x) { return hit ? x : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), first)); };
+        const F3 o{bc(w.o.x), bc(w.o.y), bc(w.o.z)}, d{bc(w.d.x), bc(w.d.y), bc(w.d.z)};
+        const Slab<false> sl{bc(w.ix), bc(w.iy), bc(w.iz), bc(w.sx), bc(w.sy), bc(w.sz), o};
+        uint64_t occ = 0;
+        switch (oct0) {
+            case 0: occ = packet_any4<0>(P, sl, o, d, act, lane); break;
+            case 1: occ = packet_any4<1>(P, sl, o, d, act, lane); break;
+            case 2: occ = packet_any4<2>(P, sl, o, d, act, lane); break;
+            case 3: occ = packet_any4<3>(P, sl, o, d, act, lane); break;
+            case 4: occ = packet_any4<4>(P, sl, o, d, act, lane); break;
+            case 5: occ = packet_any4<5>(P, sl, o, d, act, lane); break;
+            case 6: occ = packet_any4<6>(P, sl, o, d, act, lane); break;
+            default: occ = packet_any4<7>(P, sl, o, d, act, lane); break;
+        }
+        blocked = (occ >> lane) & 1u;
+        return true;
+    }
+    return false;
+}
+
 // Shading / store of a lit or occluded pixel (render.hpp:139-150).
 __device__ __forceinline__ void finish_pixel(const KParams& P, uint32_t f, uint32_t lr, uint32_t i, uint32_t pix,
                                              bool blocked, F3 sun_line, uint32_t slot, float hu, float hv,
@@ -870,6 +1007,8 @@ constexpr int kFusedB = 64;      // single-wavefront workgroups (LDS 
 template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ = false>
 __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     constexpr int kB = kFusedB;
+    // kernels that trace shadow packets keep only the generic per-lane any-hit loop as fallback
+    constexpr bool kPacketsCompiled = !kStats && !kRobust && !kQ && CERES_SHADOW_PACKET && std::is_same<StkT, uint16_t*>::value;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ StealLdsT<kB> L;
     const uint32_t lane = threadIdx.x, tid = lane;
@@ -964,10 +1103,17 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     // shadow phase: intra-wavefront work stealing shortens a frame's longest tiles (a one-frame
     // launch is tail-bound); a multi-frame batch is throughput-bound, and there one ray per lane
     // spends fewer instructions per node (the steal bookkeeping runs every iteration)
-    if constexpr (kSteal)
+    // (the stats kernels keep one ray per lane: their counters are the per-ray traversal's)
+    bool pk_blocked = false;
+    const bool pk = !kStats && (!kSteal || CERES_SHADOW_PACKET_SOLO) &&
+                    shadow_packet<StkT, kRobust, kQ>(P, hit, w, lane, pk_blocked);
+    if (pk)
+        L.blocked[tid] = pk_blocked ? 1u : 0u;
+    else if constexpr (kSteal)
         steal_traverse<kStats, kB, StkT, kRobust, kQ>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
     else
-        L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust, kQ>(P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
+        L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust, kQ, kPacketsCompiled ? -2 : -1>(
+                                    P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
     if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
@@ -1368,6 +1514,11 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     P.row_blocks_per_frame = by;
     P.stack_entries = s->stack_entries;
     P.shadow_stack_entries = s->shadow_stack_entries;
+    // wave-wide packets read every record through the scalar cache, one dependent miss at a time:
+    // for a scene that streams from DRAM (C5) that latency is exposed and the per-lane loops are
+    // faster (A/B, 16-frame batches: C5 +10 % with packets, L2-resident scenes -3..-5 %)
+    P.packets = (s->n_pairs * sizeof(SiblingPair) + s->n_nodes4 * sizeof(Node4) + s->n_tri * sizeof(Tri48)) <
+                kDramSceneBytes ? 1u : 0u;
     P.root_leaf_count = s->root_leaf_count; P.root_leaf_first = s->root_leaf_first;
     for (int k = 0; k < 6; ++k) P.root_box[k] = s->root_box[k];
     P.root_box_ok = CERES_ROOT_TEST ? s->root_box_ok : 0u;
