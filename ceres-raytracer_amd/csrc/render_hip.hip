@@ -65,12 +65,6 @@
 #ifndef CERES_SHADOW_PACKET
 #define CERES_SHADOW_PACKET 1                  // batch kernel: a tile's shadow rays as one wave-wide masked packet (packet_any4)
 #endif
-#ifndef CERES_SHADOW_PACKET_SOLO
-#define CERES_SHADOW_PACKET_SOLO 0             // ... in the single-frame (work-stealing) kernel too
-#endif
-#ifndef CERES_PACKET_ORDER
-#define CERES_PACKET_ORDER 0                   // packet_any4: 0 = first passing inner child next, 1 = the one with most lanes
-#endif
 #ifndef CERES_TRUST_STACK_BOUND
 #define CERES_TRUST_STACK_BOUND 1              // BVH2 steps of non-stats kernels: no stack clamps / overflow flag
 #endif
@@ -607,21 +601,13 @@ __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<fal
             }
         }
         // one passing inner child next (the first), the others onto the stack with their masks
+        // (the child with the most lanes first measured +4.5 % in batches)
         int nxt = -1;
         uint64_t nm = 0;
-        if (CERES_PACKET_ORDER) {
-            int most = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const uint64_t mm = n4_count(chw[c]) ? 0 : cm[c] & ~occ;
-                const int pc = __builtin_popcountll(mm);
-                if (pc > most) { most = pc; nxt = c; nm = mm; }
-            }
-        }
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const uint64_t mm = n4_count(chw[c]) ? 0 : cm[c] & ~occ;
-            if (!mm || c == nxt) continue;
+            if (!mm) continue;
             if (nxt < 0) { nxt = c; nm = mm; continue; }
             const bool mine = lane == sp;                              // a write into lane sp
             s_node = mine ? int(n4_first(chw[c])) : s_node;
@@ -1008,7 +994,7 @@ template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool
 __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     constexpr int kB = kFusedB;
     // kernels that trace shadow packets keep only the generic per-lane any-hit loop as fallback
-    constexpr bool kPacketsCompiled = !kStats && !kRobust && !kQ && CERES_SHADOW_PACKET && std::is_same<StkT, uint16_t*>::value;
+    constexpr bool kPacketsCompiled = !kStats && !kSteal && !kRobust && !kQ && CERES_SHADOW_PACKET && std::is_same<StkT, uint16_t*>::value;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ StealLdsT<kB> L;
     const uint32_t lane = threadIdx.x, tid = lane;
@@ -1103,10 +1089,11 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     // shadow phase: intra-wavefront work stealing shortens a frame's longest tiles (a one-frame
     // launch is tail-bound); a multi-frame batch is throughput-bound, and there one ray per lane
     // spends fewer instructions per node (the steal bookkeeping runs every iteration)
-    // (the stats kernels keep one ray per lane: their counters are the per-ray traversal's)
+    // (the stats kernels keep one ray per lane: their counters are the per-ray traversal's; the
+    // single-frame kernel keeps work stealing: with packets compiled in, its spills cost solo C3
+    // +3 % whether or not a tile takes them -- docs/EXPERIMENTS.md)
     bool pk_blocked = false;
-    const bool pk = !kStats && (!kSteal || CERES_SHADOW_PACKET_SOLO) &&
-                    shadow_packet<StkT, kRobust, kQ>(P, hit, w, lane, pk_blocked);
+    const bool pk = !kStats && !kSteal && shadow_packet<StkT, kRobust, kQ>(P, hit, w, lane, pk_blocked);
     if (pk)
         L.blocked[tid] = pk_blocked ? 1u : 0u;
     else if constexpr (kSteal)

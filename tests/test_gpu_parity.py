@@ -268,6 +268,34 @@ def test_assemble_packed_kernel_matches_permutation(gpu, W, H, row_block, world,
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("name", ALL)
+def test_batch_kernel_frame_matches_reference(gpu, name):
+    """The multi-frame kernel on every fixture (edge cases included: one triangle, root leaf,
+    degenerate and duplicated-leaf meshes, odd sizes, robust mode): a 3-frame batch of the fixture
+    view -- the batch kernel traces a tile's shadow rays as one wave-wide packet when its rays
+    share an octant (packet_any4), else one ray per lane -- gives the reference's PPM for every
+    frame and 3x its rays / hits."""
+    import torch
+    pkg = gpu
+    meta, _, _ = load_golden(name)
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    scene, _, _, _ = scene_for(pkg, name)
+    b12 = np.repeat(pinned_basis(meta, cfg)[None, :], 3, 0).astype(np.float32)
+    s3 = np.repeat(np.asarray(pinned_sun(meta, cfg), np.float32)[None, :], 3, 0)
+    rgb = torch.zeros((3, H, 3 * W), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+    scene.render_batch_device(b12, s3, W, H, mode=pkg.cfg_mode(cfg), d_rgb8=rgb.data_ptr(), d_counters=cnt.data_ptr(),
+                              stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    c = cnt.cpu().numpy()
+    assert (int(c[0]), int(c[1])) == (3 * meta["exact"]["rays"], 3 * meta["exact"]["hits"])
+    assert int(c[6]) == 0
+    head = b"P6 %d %d 255\n" % (W, H)
+    for f in range(3):
+        assert hashlib.sha256(head + rgb[f].cpu().numpy().tobytes()).hexdigest() == meta["ppm_sha256"]["exact"], f
+
+
 def test_batch_of_64_frames_matches_single_frames(gpu):
     """The largest batch (64 frames, cameras inline in the kernel arguments): every frame's PPM
     body == a one-frame render of the same camera, whole frames and one rank of a 3-way split."""
