@@ -744,7 +744,7 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 }
 
 #ifndef CERES_FUSED_MINW16
-#define CERES_FUSED_MINW16 6     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes, batch kernel (no-SLP build: 6 waves / 80 VGPRs beat 7 / 72 with spills: bench +0.7 %)
+#define CERES_FUSED_MINW16 7     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes, batch kernel (with shadow packets, A/A/B/B: 7 waves / 72 VGPRs beat 6 / 80 by 2.6 % on C3, bunny -0.5 %, dragon 4096^2 +-0)
 #endif
 #ifndef CERES_FUSED_MINW16_SOLO
 #define CERES_FUSED_MINW16_SOLO 7  // ... and the work-stealing single-frame kernel (72 VGPRs, no VGPR spill: dragon 4096^2 -4 %, bunny -1.5 %, C3 +-1 %)
@@ -1562,7 +1562,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
                 P.wave_log = s->d_wave_log;
                 s->last_grid_waves = waves;
             }
-            // VGPR budgets: 16-bit-stack scenes (LDS for 7+ waves/SIMD) are compiled for 6 waves,
+            // VGPR budgets: 16-bit-stack scenes (LDS for 7+ waves/SIMD) are compiled for 7 waves,
             // C5-size scenes keep the unconstrained allocation
             constexpr int w32 = CERES_FUSED_MINW32;
             auto fused = [&](auto rt, auto st) {
