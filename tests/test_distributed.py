@@ -219,11 +219,12 @@ def _exchange_worker(rank, world, port, W, H, row_block, slots, q, k=1):
 
 
 @pytest.mark.parametrize("world,row_block,slots,k", [(2, 16, 2, 1), (3, 7, 4, 1), (4, 8, 2, 4), (5, 3, 3, 2),
-                                                     (2, 8, 4, 4)])
+                                                     (2, 8, 4, 4), (8, 8, 8, 16)])
 def test_frame_exchange_alltoall(world, row_block, slots, k):
     """bench.py's default N > 1 collective: each of the step's k*N frames is gathered to its owner
     rank (one all-to-all; rank q owns batch frames q*k .. q*k+k-1), `slots` steps in flight,
-    gloo on CPU; ragged row counts per rank."""
+    gloo on CPU; ragged row counts per rank.  (8, 8, 8, 16) is the driver's N = 8 bench shape:
+    8-row blocks, 8 step slots, 16 owned frames per rank (128 per step), on small frames."""
     import_package()
     W, H = 97, 61
     ctx = mp.get_context("spawn")
