@@ -33,11 +33,16 @@ import configs  # noqa: E402,F401  (re-exported)
 MODE_FULL, MODE_PRIMARY = 0, 1
 MODE_ROBUST = 0x10          # OR-ed: RobustNodeIntersector traversal (node_intersectors.hpp:54-79)
 MODE_QBVH4 = 0x20           # OR-ed: compressed shadow BVH4 (8-bit child bounds; budget-gated, not exact)
+MODE_FMA = 0x40             # OR-ed: the reference CMake build's arithmetic (GCC FMA contraction)
+# Arithmetic of the host scene prep (CERES_ARITH_*): the reference without contraction, or as its
+# own CMake build (g++ -O3 -mavx2 -mfma) compiles it; pair ARITH_FMA scenes with MODE_FMA renders
+ARITH_EXACT, ARITH_FMA = 0, 1
 
 
-def cfg_mode(cfg):
-    """The C-ABI mode of a configs.CONFIGS entry."""
-    return (MODE_PRIMARY if cfg["mode"] == "primary" else MODE_FULL) | (MODE_ROBUST if cfg.get("robust") else 0)
+def cfg_mode(cfg, arith=ARITH_EXACT):
+    """The C-ABI mode of a configs.CONFIGS entry (| MODE_FMA for the reference-flag arithmetic)."""
+    return ((MODE_PRIMARY if cfg["mode"] == "primary" else MODE_FULL) | (MODE_ROBUST if cfg.get("robust") else 0)
+            | (MODE_FMA if arith else 0))
 SCENE_STATS = 1
 
 EXPORTED_SYMBOLS = (
@@ -50,6 +55,8 @@ EXPORTED_SYMBOLS = (
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_multi_f32", "ceres_device_count", "ceres_assemble_rgb8_packed", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
+    "ceres_obj_load_arith", "ceres_proc_mesh_arith", "ceres_rotate_triangles_arith", "ceres_bvh_build_arith",
+    "ceres_camera_basis_arith", "ceres_orbit_cameras_arith",
 )
 
 
@@ -158,6 +165,12 @@ def lib():
     L.ceres_scene_read_timing.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           _u64p]
     L.ceres_scene_wave_log.argtypes = [_vp, _u64p, _sz, ctypes.POINTER(_sz)]
+    L.ceres_obj_load_arith.argtypes = L.ceres_obj_load.argtypes + [ctypes.c_int]
+    L.ceres_proc_mesh_arith.argtypes = L.ceres_proc_mesh.argtypes + [ctypes.c_int]
+    L.ceres_rotate_triangles_arith.argtypes = L.ceres_rotate_triangles.argtypes + [ctypes.c_int]
+    L.ceres_bvh_build_arith.argtypes = L.ceres_bvh_build.argtypes + [ctypes.c_int]
+    L.ceres_camera_basis_arith.argtypes = L.ceres_camera_basis.argtypes + [ctypes.c_int]
+    L.ceres_orbit_cameras_arith.argtypes = L.ceres_orbit_cameras.argtypes + [ctypes.c_int]
     _lib = L
     return L
 
@@ -184,12 +197,13 @@ class Camera:
     """render.hpp:16-22 -- eye, dir, up, fov (degrees); Camera<float> or, with dtype=np.float64,
     Camera<double> (anim.cpp -d)."""
 
-    def __init__(self, eye, dir, up, fov, dtype=np.float32):
+    def __init__(self, eye, dir, up, fov, dtype=np.float32, arith=ARITH_EXACT):
         self.dtype = np.dtype(dtype)
         self.eye = np.asarray(eye, self.dtype)
         self.dir = np.asarray(dir, self.dtype)
         self.up = np.asarray(up, self.dtype)
         self.fov = float(fov)
+        self.arith = int(arith)                      # float cameras: CERES_ARITH_* of the basis
 
     def basis(self, W, H):
         """render.hpp:91-97 on the host (libm stays on the host): {eye, dir, image_u, image_v}."""
@@ -199,8 +213,9 @@ class Camera:
                                                 _p(self.up, ctypes.c_double), self.fov, W, H, _p(out, ctypes.c_double)))
             return np.concatenate([self.eye, out])
         out = np.zeros(9, np.float32)
-        _check(lib().ceres_camera_basis(_p(self.eye, ctypes.c_float), _p(self.dir, ctypes.c_float),
-                                        _p(self.up, ctypes.c_float), self.fov, W, H, _p(out, ctypes.c_float)))
+        _check(lib().ceres_camera_basis_arith(_p(self.eye, ctypes.c_float), _p(self.dir, ctypes.c_float),
+                                              _p(self.up, ctypes.c_float), self.fov, W, H, _p(out, ctypes.c_float),
+                                              self.arith))
         return np.concatenate([self.eye, out]).astype(np.float32)
 
 
@@ -231,9 +246,9 @@ class Bvh:
         self.prim = np.ascontiguousarray(prim, np.uint64)
 
 
-def load_obj(path):
+def load_obj(path, arith=ARITH_EXACT):
     t, n, cnt = _fp(), _fp(), _sz()
-    _check(lib().ceres_obj_load(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt)))
+    _check(lib().ceres_obj_load_arith(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt), int(arith)))
     c = cnt.value
     return Mesh(_take(t, c * 12, np.float32).reshape(c, 12), _take(n, c * 9, np.float32).reshape(c, 9))
 
@@ -279,31 +294,32 @@ def device_free(d_ptr):
     lib().ceres_device_free(d_ptr or None)
 
 
-def proc_mesh(n):
+def proc_mesh(n, arith=ARITH_EXACT):
     t, nn, cnt = _fp(), _fp(), _sz()
-    _check(lib().ceres_proc_mesh(int(n), ctypes.byref(t), ctypes.byref(nn), ctypes.byref(cnt)))
+    _check(lib().ceres_proc_mesh_arith(int(n), ctypes.byref(t), ctypes.byref(nn), ctypes.byref(cnt), int(arith)))
     c = cnt.value
     return Mesh(_take(t, c * 12, np.float32).reshape(c, 12), _take(nn, c * 9, np.float32).reshape(c, 9))
 
 
-def rotate_triangles(mesh, axis, degrees):
+def rotate_triangles(mesh, axis, degrees, arith=ARITH_EXACT):
     ax = {"x": 0, "y": 1, "z": 2}[axis] if isinstance(axis, str) else int(axis)
     if mesh.f64:
         _check(lib().ceres_rotate_triangles_f64(_p(mesh.tri, ctypes.c_double), len(mesh), ax, float(degrees)))
     else:
-        _check(lib().ceres_rotate_triangles(_p(mesh.tri, ctypes.c_float), len(mesh), ax, float(degrees)))
+        _check(lib().ceres_rotate_triangles_arith(_p(mesh.tri, ctypes.c_float), len(mesh), ax, float(degrees),
+                                                  int(arith)))
     return mesh
 
 
-def build_bvh(mesh):
+def build_bvh(mesh, arith=ARITH_EXACT):
     if mesh.f64:
         nodes, prim, m = _u64p(), _u64p(), _sz()
         _check(lib().ceres_bvh_build_f64(_p(mesh.tri, ctypes.c_double), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
                                          ctypes.byref(prim)))
         return Bvh(_take(nodes, m.value * 8, np.uint64).reshape(-1, 8), _take(prim, len(mesh), np.uint64))
     nodes, prim, m = _u32p(), _u64p(), _sz()
-    _check(lib().ceres_bvh_build(_p(mesh.tri, ctypes.c_float), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
-                                 ctypes.byref(prim)))
+    _check(lib().ceres_bvh_build_arith(_p(mesh.tri, ctypes.c_float), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
+                                       ctypes.byref(prim), int(arith)))
     return Bvh(_take(nodes, m.value * 8, np.uint32).reshape(-1, 8), _take(prim, len(mesh), np.uint64))
 
 
@@ -468,10 +484,11 @@ def orbit_cameras(camera, sun, W, H, n_frames, axis=(0, 1, 0), step_deg=None, ro
     d3 = np.zeros((n, 3), np.float32)
     ax = np.asarray(axis, np.float32)
     sn = np.asarray(sun, np.float32)
-    _check(lib().ceres_orbit_cameras(_p(camera.eye, ctypes.c_float), _p(camera.dir, ctypes.c_float),
-                                     _p(camera.up, ctypes.c_float), _p(sn, ctypes.c_float), camera.fov, W, H,
-                                     _p(ax, ctypes.c_float), float(step), n, 1 if rotate_first else 0,
-                                     _p(b, ctypes.c_float), _p(s3, ctypes.c_float), _p(d3, ctypes.c_float)))
+    _check(lib().ceres_orbit_cameras_arith(_p(camera.eye, ctypes.c_float), _p(camera.dir, ctypes.c_float),
+                                           _p(camera.up, ctypes.c_float), _p(sn, ctypes.c_float), camera.fov, W, H,
+                                           _p(ax, ctypes.c_float), float(step), n, 1 if rotate_first else 0,
+                                           _p(b, ctypes.c_float), _p(s3, ctypes.c_float), _p(d3, ctypes.c_float),
+                                           camera.arith))
     return (b, s3, d3) if want_dirs else (b, s3)
 
 
@@ -494,18 +511,18 @@ def bench_views(camera, sun, W, H, F, basis0=None):
     return b12, s3, steps
 
 
-def pose(cfg, frame=0):
+def pose(cfg, frame=0, arith=ARITH_EXACT):
     """(Camera, sun) of a config: configs with "orbit": (axis, step_deg, count) are the anim.cpp
     orbit pose after count + frame rotations; otherwise the config's camera rotated `frame`
     times by configs.BENCH_ORBIT."""
-    cam = Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    cam = Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"], arith=arith)
     axis, step = (cfg["orbit"][0], cfg["orbit"][1]) if cfg.get("orbit") else configs.BENCH_ORBIT
     n = (cfg["orbit"][2] if cfg.get("orbit") else 0) + int(frame)
     if n == 0:
         return cam, np.asarray(cfg["sun"], np.float32)
     b, s3, d3 = orbit_cameras(cam, cfg["sun"], cfg["W"], cfg["H"], n + 1, axis=axis, step_deg=step,
                               rotate_first=False, want_dirs=True)
-    return Camera(b[n, :3], d3[n], cfg["up"], cfg["fov"]), s3[n].copy()
+    return Camera(b[n, :3], d3[n], cfg["up"], cfg["fov"], arith=arith), s3[n].copy()
 
 
 def pose_f64(cfg):
@@ -555,10 +572,11 @@ def row_map(H, row_block, world):
     return out
 
 
-def prepare(cfg, f64=False):
+def prepare(cfg, f64=False, arith=ARITH_EXACT):
     """Scene prep of the reference app for a config (configs.CONFIGS entry): mesh, bvh, camera
     (at the config's orbit pose; pose(cfg) also gives the sun).  f64: the render<double>
-    pipeline (anim.cpp -d) -- double mesh / BVH, camera at the config's pose in double."""
+    pipeline (anim.cpp -d) -- double mesh / BVH, camera at the config's pose in double.
+    arith = ARITH_FMA: every step in the reference CMake build's arithmetic (render with MODE_FMA)."""
     if f64:
         mesh = proc_mesh_f64(cfg["proc"]) if cfg.get("proc") else load_obj_f64(configs.obj_path(cfg))
         if len(mesh) == 0:
@@ -566,13 +584,13 @@ def prepare(cfg, f64=False):
         if cfg.get("rotate"):
             rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1])
         return mesh, build_bvh(mesh), pose_f64(cfg)[0]
-    mesh = proc_mesh(cfg["proc"]) if cfg.get("proc") else load_obj(configs.obj_path(cfg))
+    mesh = proc_mesh(cfg["proc"], arith) if cfg.get("proc") else load_obj(configs.obj_path(cfg), arith)
     if len(mesh) == 0:
         raise CeresError("The given scene is empty or cannot be loaded")
     if cfg.get("rotate"):
-        rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1])
-    bvh = build_bvh(mesh)
-    cam, _ = pose(cfg)
+        rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1], arith)
+    bvh = build_bvh(mesh, arith)
+    cam, _ = pose(cfg, arith=arith)
     return mesh, bvh, cam
 
 

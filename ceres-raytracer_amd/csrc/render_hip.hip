@@ -22,7 +22,9 @@
 // Numerics: compiled with -ffp-contract=off and correctly rounded f32 div/sqrt, explicit
 // fmaf only where the reference calls fast_multiply_add, x^24 in double for std::pow (pow24.hpp,
 // exhaustively equal to glibc for every float) -- every float matches the reference compiled
-// without contraction bit for bit.
+// without contraction bit for bit.  CERES_MODE_FMA instantiates every kernel a second time with
+// an explicit fmaf at exactly the sites where the reference's own CMake build (g++ -O3 -mfma)
+// contracts (kG, oracle/contraction_sites.txt): then every float matches THAT build bit for bit.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -97,6 +99,29 @@ __device__ __forceinline__ float dot(F3 a, F3 b) { float s = a.x * b.x; s += a.y
 __device__ __forceinline__ F3 cross(F3 a, F3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 __device__ __forceinline__ F3 normalize(F3 v) { float inv = 1.0f / sqrtf(dot(v, v)); return v * inv; }
 __device__ __forceinline__ F3 f3(const float* p) { return {p[0], p[1], p[2]}; }
+
+// The reference as its own CMake build compiles it (CMakeLists.txt:11-13, g++ -O3 -mavx2 -mfma;
+// CERES_MODE_FMA, kernels instantiated with kG = true): GCC contracts a*b+c into one FMA at the
+// sites its widening_mul pass picks -- read from the compiler's dump of the reference, listed in
+// oracle/contraction_sites.txt.  dot (vector.hpp:134-141) becomes fma(a2,b2, fma(a0,b0, a1 b1))
+// ("A") everywhere but Triangle::intersect's v = dot(r, e1), fused as fma(a2,b2, fma(a1,b1, a0 b0))
+// ("B"); cross (vector.hpp:159-167) a_j b_k - a_k b_j becomes fma(a_j, b_k, -(a_k b_j)).  With
+// kG = false every helper is the plain contraction-free expression.
+template <bool kG> __device__ __forceinline__ float dotA(F3 a, F3 b) {
+    if constexpr (kG) return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.x, b.x, a.y * b.y));
+    else return dot(a, b);
+}
+template <bool kG> __device__ __forceinline__ float dotB(F3 a, F3 b) {
+    if constexpr (kG) return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
+    else return dot(a, b);
+}
+template <bool kG> __device__ __forceinline__ F3 crossG(F3 a, F3 b) {
+    if constexpr (kG)
+        return {__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+                __builtin_fmaf(a.x, b.y, -(a.y * b.x))};
+    else return cross(a, b);
+}
+template <bool kG> __device__ __forceinline__ F3 normalizeG(F3 v) { float inv = 1.0f / sqrtf(dotA<kG>(v, v)); return v * inv; }
 
 // Wave-uniform fetches.  The fused kernel is bound by the vector-memory return path (PMC of an
 // 8-frame C3 batch: TD busy 79 %, TA 70 % of cycles), which delivers every active lane's 16 B
@@ -174,16 +199,17 @@ struct Stk24 {
 struct Hit { uint32_t slot; float t, u, v; };
 
 // Triangle::intersect (triangle.hpp:95-115, left-handed normal).
+template <bool kG = false>
 __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin, float tmax, float& t_out,
                                          float& u_out, float& v_out) {
     const F3 c = tr.p0 - o;
-    const F3 r = cross(d, c);
-    const float inv_det = rcp_exact(dot(tr.n, d));
-    const float u = dot(r, tr.e2) * inv_det;
-    const float v = dot(r, tr.e1) * inv_det;
+    const F3 r = crossG<kG>(d, c);
+    const float inv_det = rcp_exact(dotA<kG>(tr.n, d));
+    const float u = dotA<kG>(r, tr.e2) * inv_det;
+    const float v = dotB<kG>(r, tr.e1) * inv_det;
     const float w = 1.0f - u - v;
     if (u >= 0 && v >= 0 && w >= 0) {
-        const float t = dot(tr.n, c) * inv_det;
+        const float t = dotA<kG>(tr.n, c) * inv_det;
         if (t >= tmin && t <= tmax) { t_out = t; u_out = u; v_out = v; return true; }
     }
     return false;
@@ -192,12 +218,13 @@ __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin,
 // tri_test on triangle `idx`, the wave-uniform case with its own copy of the test: the test
 // then reads the record from SGPRs instead of first copying the 12 scalar-loaded words into
 // VGPRs to join the vector path (12 v_mov per uniform test; CERES_SPLIT_UNIFORM)
+template <bool kG = false>
 __device__ __forceinline__ bool tri_test_u(const Tri48* tris, uint32_t idx, F3 o, F3 d, float tmin, float tmax,
                                            float& t_out, float& u_out, float& v_out) {
-    if (!CERES_SPLIT_UNIFORM) return tri_test(load_tri_u(tris, idx), o, d, tmin, tmax, t_out, u_out, v_out);
+    if (!CERES_SPLIT_UNIFORM) return tri_test<kG>(load_tri_u(tris, idx), o, d, tmin, tmax, t_out, u_out, v_out);
     uint32_t r;
-    if (uniform_id(idx, r)) return tri_test(load_tri_s(tris + r), o, d, tmin, tmax, t_out, u_out, v_out);
-    return tri_test(load_tri(tris + idx), o, d, tmin, tmax, t_out, u_out, v_out);
+    if (uniform_id(idx, r)) return tri_test<kG>(load_tri_s(tris + r), o, d, tmin, tmax, t_out, u_out, v_out);
+    return tri_test<kG>(load_tri(tris + idx), o, d, tmin, tmax, t_out, u_out, v_out);
 }
 
 // Per-ray constants of the ray-box (slab) test and the test of one box.
@@ -296,7 +323,8 @@ __device__ __forceinline__ bool with_uniform_octant(const Slab<false>& s, Fn&& f
 // whenever y is not NaN (y is tmin / tmax / a previous robust_max -- never NaN) up to the
 // sign of zero, which no comparison below can observe; likewise robust_min and fminf.  The
 // slab values themselves are finite for |coordinates| < 4e31 (|inv| <= 1/FLT_EPSILON).
-template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, int kOct = -1>
+template <bool kAnyHit, bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, int kOct = -1,
+          bool kG = false>
 __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hit& best,
                                       uint32_t& n_pairs, uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f;
@@ -306,7 +334,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         if (kStats) n_tests += P.root_leaf_count;
         for (uint32_t k = P.root_leaf_first; k < P.root_leaf_first + P.root_leaf_count; ++k) {
             float t, u, v;
-            if (tri_test(load_tri(P.tris + k), o, d, tmin, tmax, t, u, v)) {
+            if (tri_test<kG>(load_tri(P.tris + k), o, d, tmin, tmax, t, u, v)) {
                 best = {k, t, u, v}; have = true;
                 if (kAnyHit) return true;
                 tmax = t;
@@ -318,7 +346,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     if constexpr (!kRobust && kOct == -1 && (CERES_OCTANT_SLAB & 1)) {
         bool r = false;
         if (with_uniform_octant(sl, [&](auto k) {
-                r = trace<kAnyHit, kStats, kS, StkT, kRobust, decltype(k)::value>(P, o, d, stk, best, n_pairs, n_tests, overflow);
+                r = trace<kAnyHit, kStats, kS, StkT, kRobust, decltype(k)::value, kG>(P, o, d, stk, best, n_pairs, n_tests, overflow);
             }))
             return r;
     }
@@ -381,7 +409,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         while (k < k_end || k2 < k2_end) {
             const uint32_t idx = k < k_end ? k++ : k2++;
             float t, u, v;
-            if (tri_test_u(P.tris, idx, o, d, tmin, tmax, t, u, v)) {
+            if (tri_test_u<kG>(P.tris, idx, o, d, tmin, tmax, t, u, v)) {
                 best = {idx, t, u, v}; have = true;
                 if (kAnyHit) return true;
                 tmax = t;
@@ -446,19 +474,20 @@ __device__ __forceinline__ N4 load_shadow_node(const KParams& P, uint32_t cur) {
 __device__ __forceinline__ float pick(float4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 __device__ __forceinline__ uint32_t pick(uint4 v, uint32_t c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
 
-template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, bool kQ = false, int kOct = -1>
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, bool kQ = false, int kOct = -1,
+          bool kG = false>
 __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT stk, uint32_t& n_pairs,
                                            uint32_t& n_tests, bool& overflow) {
     const float tmin = 0.0f, tmax = FLT_MAX;
     if (P.root_leaf_count) {
         Hit h;
-        return trace<true, kStats, kS, StkT, kRobust>(P, o, d, stk, h, n_pairs, n_tests, overflow);
+        return trace<true, kStats, kS, StkT, kRobust, -1, kG>(P, o, d, stk, h, n_pairs, n_tests, overflow);
     }
     const Slab<kRobust> sl = make_slab<kRobust>(o, d);
     if constexpr (!kRobust && kOct == -1 && (CERES_OCTANT_SLAB & 2)) {
         bool r = false;
         if (with_uniform_octant(sl, [&](auto k) {
-                r = trace_any4<kStats, kS, StkT, kRobust, kQ, decltype(k)::value>(P, o, d, stk, n_pairs, n_tests, overflow);
+                r = trace_any4<kStats, kS, StkT, kRobust, kQ, decltype(k)::value, kG>(P, o, d, stk, n_pairs, n_tests, overflow);
             }))
             return r;
     }
@@ -512,7 +541,7 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
                 if (kStats) n_tests += k_end - k;
             }
             float t, u, v;
-            if (tri_test_u(P.tris, k, o, d, tmin, tmax, t, u, v)) return true;
+            if (tri_test_u<kG>(P.tris, k, o, d, tmin, tmax, t, u, v)) return true;
             ++k;
         }
         if (inner_mask) {
@@ -559,7 +588,7 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
 // (a select on lane == sp / v_readlane, no memory); it holds at most shadow_stack_entries (the most pushes
 // along any root-leaf path, build_shadow_bvh4) -- the host only takes this path when <= 64.
 // `act`: lanes with a shadow ray; their o / slab in every lane (others: copies of an active one).
-template <int kOct>
+template <int kOct, bool kG>
 __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<false>& sl, F3 o, F3 d, uint64_t act,
                                                 uint32_t lane) {
     constexpr float tmin = 0.0f, tmax = FLT_MAX;
@@ -595,7 +624,7 @@ __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<fal
                 // all 48 B in flight before the first use (one scalar-load wait per triangle, not two)
                 __asm__ volatile("" ::"s"(a.x), "s"(b.x), "s"(g.x));
                 const TriV tr{{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, g.x}, {g.y, g.z, g.w}};
-                const bool h = tri_test(tr, o, d, tmin, tmax, t, u, v);
+                const bool h = tri_test<kG>(tr, o, d, tmin, tmax, t, u, v);
                 occ |= __ballot(h) & lm;
                 lm &= ~occ;
             }
@@ -658,15 +687,41 @@ __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t lr) {
     return ((lr / P.row_block) * P.world + P.rank) * P.row_block + lr % P.row_block;
 }
 
-// Primary ray direction of pixel (i, j) of frame f, render.hpp:109-111.
+// Primary ray direction of pixel (i, j) of frame f, render.hpp:109-111 (GCC: dir + fma(iv, v, iu u)).
+template <bool kG = false>
 __device__ __forceinline__ F3 primary_dir(const KParams& P, uint32_t f, uint32_t i, uint32_t j) {
     const float u = 2 * (float(i) + 0.5f) / float(P.W) - 1.0f;
     const float v = 2 * (float(j) + 0.5f) / float(P.H) - 1.0f;
     const FrameCam& c = P.cam[f];
-    return normalize(f3(c.iu) * u + f3(c.iv) * v + f3(c.dir));
+    if constexpr (kG)
+        return normalizeG<kG>(F3{c.dir[0] + __builtin_fmaf(c.iv[0], v, c.iu[0] * u),
+                                 c.dir[1] + __builtin_fmaf(c.iv[1], v, c.iu[1] * u),
+                                 c.dir[2] + __builtin_fmaf(c.iv[2], v, c.iu[2] * u)});
+    else return normalize(f3(c.iu) * u + f3(c.iv) * v + f3(c.dir));
 }
 
-// smooth_shading, render.hpp:46-84 (pow in double: std::pow(float, int) promotes).
+// Hit point + self-intersection offset, render.hpp:127-133 (p1() = p0 - e1, p2() = p0 + e2).
+// GCC: fma(n, scale, fma(w, p2, fma(v, p1, u p0))) per component.
+template <bool kG>
+__device__ __forceinline__ F3 hit_point(const TriV& tr, F3 normal, float hu, float hv) {
+    const F3 p1 = tr.p0 - tr.e1, p2 = tr.p0 + tr.e2;
+    const float scale = -0.00001;
+    const float w = 1 - hu - hv;
+    if constexpr (kG) {
+        auto c = [&](float p0, float q1, float q2, float n) {
+            return __builtin_fmaf(n, scale, __builtin_fmaf(w, q2, __builtin_fmaf(hv, q1, hu * p0)));
+        };
+        return {c(tr.p0.x, p1.x, p2.x, normal.x), c(tr.p0.y, p1.y, p2.y, normal.y), c(tr.p0.z, p1.z, p2.z, normal.z)};
+    } else {
+        F3 p = tr.p0 * hu + p1 * hv + p2 * w;
+        return p + normal * scale;
+    }
+}
+
+// smooth_shading, render.hpp:46-84 (pow in double: std::pow(float, int) promotes).  GCC fuses
+// lambertian's sum like dot "A", amb + 0.5 lam into fma(lam, 0.5, amb) and each channel's
+// (amb + diffuse) * k + specular into fma(amb + diffuse, k, specular); c[] += w * clamp stays unfused.
+template <bool kG = false>
 __device__ __forceinline__ void shade(F3 sun_line, const float* nrm, F3 view, float u, float v, float c[3]) {
     c[0] = c[1] = c[2] = 0.0f;
     const float amb = 0.2;
@@ -675,13 +730,14 @@ __device__ __forceinline__ void shade(F3 sun_line, const float* nrm, F3 view, fl
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const F3 N{nrm[3 * k], nrm[3 * k + 1], nrm[3 * k + 2]};
-        const float diffuse = 0.5f * fabsf(sun_line.x * N.x + sun_line.y * N.y + sun_line.z * N.z);
-        const float spec = 0.8f * pow24f(dot(N, normalize(sun_line + vneg)));   // == (float)std::pow(double, 24)
-        const float base = amb + diffuse;
+        const float lam = kG ? fabsf(dotA<true>(sun_line, N)) : fabsf(sun_line.x * N.x + sun_line.y * N.y + sun_line.z * N.z);
+        const float spec = 0.8f * pow24f(dotA<kG>(N, normalizeG<kG>(sun_line + vneg)));   // == (float)std::pow(double, 24)
+        const float base = kG ? __builtin_fmaf(lam, 0.5f, amb) : amb + 0.5f * lam;
         auto clamp01 = [](float x) { return (x < 0.f) ? 0.f : (1.f < x) ? 1.f : x; };   // std::clamp
-        c[0] += w[k] * clamp01(base * 0.5f + spec);
-        c[1] += w[k] * clamp01(base * 0.0f + spec);
-        c[2] += w[k] * clamp01(base * 0.8f + spec);
+        auto ch = [&](float k) { return kG ? __builtin_fmaf(base, k, spec) : base * k + spec; };
+        c[0] += w[k] * clamp01(ch(0.5f));
+        c[1] += w[k] * clamp01(ch(0.0f));
+        c[2] += w[k] * clamp01(ch(0.8f));
     }
 }
 
@@ -696,7 +752,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // grid.x: 16-pixel column blocks; grid.y: frames x 16-row blocks of this rank's rows.  The
 // four wavefronts of a workgroup take the 2x2 8x8 tiles of its 16x16 pixels (row-major lanes:
 // C2's rays are coherent already, the Morton lane order measured +2.5 % on solo frames here).
-template <bool kStats, bool kRobust>
+template <bool kStats, bool kRobust, bool kG>
 __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -713,8 +769,8 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     uint32_t n_pairs = 0, n_tests = 0;
     bool overflow = false;
     if (active) {
-        const F3 view = primary_dir(P, f, i, global_row(P, lr));
-        hit = trace<false, kStats, kBlock, uint32_t*, kRobust>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
+        const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
+        hit = trace<false, kStats, kBlock, uint32_t*, kRobust, -1, kG>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
             P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
@@ -725,7 +781,7 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
         if (!hit) {
             store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);                 // render.hpp:116-117
         } else {                                                     // render.hpp:123-125
-            const F3 normal = normalize(load_tri(P.tris + h.slot).n);
+            const F3 normal = normalizeG<kG>(load_tri(P.tris + h.slot).n);
             store_pixel(P, f, lr, i, fabsf(normal.x), fabsf(normal.y), fabsf(normal.z));
         }
     }
@@ -790,7 +846,7 @@ struct StealLdsT {
 // Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
 // intra-wavefront work stealing; on return L.blocked[tid] holds the lane's answer.  Must be
 // reached by all 64 lanes of the wavefront (it loops on wavefront ballots).
-template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, bool kQ = false>
+template <bool kStats, int kS = kBlock, typename StkT = uint32_t*, bool kRobust = false, bool kQ = false, bool kG = false>
 __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, RayWork w, StkT stk, StealLdsT<kS>& L,
                                                uint32_t tid, uint32_t lane, uint32_t& n_pairs, uint32_t& n_tests,
                                                bool& overflow, uint32_t* n_iters = nullptr) {
@@ -804,7 +860,7 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
     if (P.root_leaf_count) {                                           // single-leaf scene
         if (has_job) {
             Hit h;
-            L.blocked[tid] = trace<true, kStats, kS, StkT, kRobust>(P, w.o, w.d, stk, h, n_pairs, n_tests, overflow) ? 1u : 0u;
+            L.blocked[tid] = trace<true, kStats, kS, StkT, kRobust, -1, kG>(P, w.o, w.d, stk, h, n_pairs, n_tests, overflow) ? 1u : 0u;
         }
         active = false;
     }
@@ -853,7 +909,7 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
                     if (kStats) n_tests += k_end - k;
                 }
                 float t, u, v;
-                if (tri_test_u(P.tris, k, w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
+                if (tri_test_u<kG>(P.tris, k, w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
                 ++k;
             }
             if (found) {
@@ -923,11 +979,11 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
     __builtin_amdgcn_wave_barrier();
 }
 
-template <bool kRobust = false>
+template <bool kRobust = false, bool kG = false>
 __device__ __forceinline__ RayWork make_shadow_ray(F3 o, F3 sun) {
     RayWork w;
     w.o = o;
-    w.d = normalize(sun - o);                                          // render.hpp:135
+    w.d = normalizeG<kG>(sun - o);                                     // render.hpp:135
     const Slab<kRobust> sl = make_slab<kRobust>(o, w.d);
     w.ix = sl.ix; w.iy = sl.iy; w.iz = sl.iz; w.sx = sl.sx; w.sy = sl.sy; w.sz = sl.sz;
     return w;
@@ -936,7 +992,7 @@ __device__ __forceinline__ RayWork make_shadow_ray(F3 o, F3 sun) {
 // A tile's shadow rays as one packet_any4 when every lane with a shadow ray shares one ray octant
 // (nearly every tile), the scene is L2-resident (P.packets) and the packet stack fits the 64
 // lanes: returns true and this lane's answer in `blocked`; false (nothing traced) otherwise.
-template <typename StkT, bool kRobust, bool kQ>
+template <typename StkT, bool kRobust, bool kQ, bool kG>
 __device__ __forceinline__ bool shadow_packet(const KParams& P, bool hit, const RayWork& w, uint32_t lane, bool& blocked) {
     if constexpr (!kRobust && !kQ && CERES_SHADOW_PACKET && std::is_same<StkT, uint16_t*>::value) {
         const uint64_t act = __ballot(hit);
@@ -952,14 +1008,14 @@ __device__ __forceinline__ bool shadow_packet(const KParams& P, bool hit, const 
         const Slab<false> sl{bc(w.ix), bc(w.iy), bc(w.iz), bc(w.sx), bc(w.sy), bc(w.sz), o};
         uint64_t occ = 0;
         switch (oct0) {
-            case 0: occ = packet_any4<0>(P, sl, o, d, act, lane); break;
-            case 1: occ = packet_any4<1>(P, sl, o, d, act, lane); break;
-            case 2: occ = packet_any4<2>(P, sl, o, d, act, lane); break;
-            case 3: occ = packet_any4<3>(P, sl, o, d, act, lane); break;
-            case 4: occ = packet_any4<4>(P, sl, o, d, act, lane); break;
-            case 5: occ = packet_any4<5>(P, sl, o, d, act, lane); break;
-            case 6: occ = packet_any4<6>(P, sl, o, d, act, lane); break;
-            default: occ = packet_any4<7>(P, sl, o, d, act, lane); break;
+            case 0: occ = packet_any4<0, kG>(P, sl, o, d, act, lane); break;
+            case 1: occ = packet_any4<1, kG>(P, sl, o, d, act, lane); break;
+            case 2: occ = packet_any4<2, kG>(P, sl, o, d, act, lane); break;
+            case 3: occ = packet_any4<3, kG>(P, sl, o, d, act, lane); break;
+            case 4: occ = packet_any4<4, kG>(P, sl, o, d, act, lane); break;
+            case 5: occ = packet_any4<5, kG>(P, sl, o, d, act, lane); break;
+            case 6: occ = packet_any4<6, kG>(P, sl, o, d, act, lane); break;
+            default: occ = packet_any4<7, kG>(P, sl, o, d, act, lane); break;
         }
         blocked = (occ >> lane) & 1u;
         return true;
@@ -968,6 +1024,7 @@ __device__ __forceinline__ bool shadow_packet(const KParams& P, bool hit, const 
 }
 
 // Shading / store of a lit or occluded pixel (render.hpp:139-150).
+template <bool kG>
 __device__ __forceinline__ void finish_pixel(const KParams& P, uint32_t f, uint32_t lr, uint32_t i, uint32_t pix,
                                              bool blocked, F3 sun_line, uint32_t slot, float hu, float hv,
                                              uint32_t& occluded) {
@@ -976,9 +1033,9 @@ __device__ __forceinline__ void finish_pixel(const KParams& P, uint32_t f, uint3
         ++occluded;
         store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);
     } else {
-        const F3 view = primary_dir(P, f, i, global_row(P, lr));
+        const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
         float c[3];
-        shade(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
+        shade<kG>(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
         store_pixel(P, f, lr, i, c[0], c[1], c[2]);
     }
 }
@@ -990,7 +1047,7 @@ __device__ __forceinline__ void finish_pixel(const KParams& P, uint32_t f, uint3
 // whose pixel missed help the others), then shades.  No shadow-ray queue in HBM, no second
 // launch: the shadow work of early tiles overlaps the primary work of later ones.
 constexpr int kFusedB = 64;      // single-wavefront workgroups (LDS is released per workgroup)
-template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ = false>
+template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ, bool kG>
 __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     constexpr int kB = kFusedB;
     // kernels that trace shadow packets keep only the generic per-lane any-hit loop as fallback
@@ -1058,10 +1115,10 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     uint64_t t_start = 0;
     if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
     if (active) {
-        const F3 view = primary_dir(P, f, i, global_row(P, lr));
+        const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
         // kOct -1: the traversal dispatches on a wave-uniform octant; -2: generic loop only
         constexpr int kOctMode = (!kSteal || (CERES_OCTANT_SLAB & 4)) ? -1 : -2;
-        hit = trace<false, kStats, kB, StkT, kRobust, kOctMode>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
+        hit = trace<false, kStats, kB, StkT, kRobust, kOctMode, kG>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
             P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
@@ -1073,12 +1130,8 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
             store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);                 // render.hpp:116-117
         } else {                                                     // render.hpp:127-135
             const TriV tr = load_tri(P.tris + h.slot);
-            const F3 normal = normalize(tr.n);
-            const F3 p1 = tr.p0 - tr.e1, p2 = tr.p0 + tr.e2;
-            F3 p = tr.p0 * h.u + p1 * h.v + p2 * (1 - h.u - h.v);
-            const float scale = -0.00001;
-            p = p + normal * scale;
-            w = make_shadow_ray<kRobust>(p, f3(P.cam[f].sun));
+            const F3 normal = normalizeG<kG>(tr.n);
+            w = make_shadow_ray<kRobust, kG>(hit_point<kG>(tr, normal, h.u, h.v), f3(P.cam[f].sun));
         }
     }
     const uint32_t n_shadow_t = __popcll(__ballot(hit));
@@ -1093,15 +1146,15 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     // single-frame kernel keeps work stealing: with packets compiled in, its spills cost solo C3
     // +3 % whether or not a tile takes them -- docs/EXPERIMENTS.md)
     bool pk_blocked = false;
-    const bool pk = !kStats && !kSteal && shadow_packet<StkT, kRobust, kQ>(P, hit, w, lane, pk_blocked);
+    const bool pk = !kStats && !kSteal && shadow_packet<StkT, kRobust, kQ, kG>(P, hit, w, lane, pk_blocked);
     if (pk)
         L.blocked[tid] = pk_blocked ? 1u : 0u;
     else if constexpr (kSteal)
-        steal_traverse<kStats, kB, StkT, kRobust, kQ>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
+        steal_traverse<kStats, kB, StkT, kRobust, kQ, kG>(P, hit, w, stk, L, tid, lane, n_pairs, n_tests, overflow, &shadow_iters);
     else
-        L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust, kQ, kPacketsCompiled ? -2 : -1>(
+        L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust, kQ, kPacketsCompiled ? -2 : -1, kG>(
                                     P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
-    if (hit) finish_pixel(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
+    if (hit) finish_pixel<kG>(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
         // primary hits, wave primary pairs, wave shadow pairs
@@ -1470,7 +1523,8 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         return set_error(CERES_EINVAL, "render: %u frames per batch (1..%d)", frames, kMaxFrames);
     const bool robust = (mode & CERES_MODE_ROBUST) != 0;            // RobustNodeIntersector traversal
     const bool qbvh = (mode & CERES_MODE_QBVH4) != 0;              // compressed shadow BVH4 (not exact)
-    mode &= ~(CERES_MODE_ROBUST | CERES_MODE_QBVH4);
+    const bool gfma = (mode & CERES_MODE_FMA) != 0;                 // the reference CMake build's FMA contraction
+    mode &= ~(CERES_MODE_ROBUST | CERES_MODE_QBVH4 | CERES_MODE_FMA);
     if (mode != CERES_MODE_FULL && mode != CERES_MODE_PRIMARY) return set_error(CERES_EINVAL, "render: bad mode %d", mode);
     if (W == 0 || H == 0 || W > 65535u * 16u || H > 0xffffffu) return set_error(CERES_EINVAL, "render: bad size %zux%zu", W, H);
     ceres_tiling t{uint32_t(H), 0, 1};
@@ -1565,40 +1619,48 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             // VGPR budgets: 16-bit-stack scenes (LDS for 7+ waves/SIMD) are compiled for 7 waves,
             // C5-size scenes keep the unconstrained allocation
             constexpr int w32 = CERES_FUSED_MINW32;
-            auto fused = [&](auto rt, auto st) {
-                constexpr bool R = decltype(rt)::value, T = decltype(st)::value;
+            auto fused = [&](auto rt, auto st, auto gt) {
+                constexpr bool R = decltype(rt)::value, T = decltype(st)::value, G = decltype(gt)::value;
                 constexpr int w16 = T ? CERES_FUSED_MINW16_SOLO : CERES_FUSED_MINW16;
                 if constexpr (!R) {
                     if (qbvh) {                                      // compressed shadow BVH4 (non-stats, fast slabs)
-                        if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, false, T, true>), fgrid, fblock, flds, stream, P);
-                        else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, false, T, true>), fgrid, fblock, flds, stream, P);
-                        else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, false, T, true>), fgrid, fblock, flds, stream, P);
+                        if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, false, T, true, G>), fgrid, fblock, flds, stream, P);
+                        else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, false, T, true, G>), fgrid, fblock, flds, stream, P);
+                        else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, false, T, true, G>), fgrid, fblock, flds, stream, P);
                         return;
                     }
                 }
-                if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, uint16_t*, 1, R, T>), fgrid, fblock, flds, stream, P);
-                else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
-                else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);
-                else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, R, T>), fgrid, fblock, flds, stream, P);
-                else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, R, T>), fgrid, fblock, flds, stream, P);
-                else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, R, T>), fgrid, fblock, flds, stream, P);
+                if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, uint16_t*, 1, R, T, false, G>), fgrid, fblock, flds, stream, P);
+                else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, dev::Stk24, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
+                else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, uint32_t*, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
+                else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, R, T, false, G>), fgrid, fblock, flds, stream, P);
+                else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
+            };
+            auto fused_g = [&](auto rt, auto st) {
+                if (gfma) fused(rt, st, std::true_type{});
+                else fused(rt, st, std::false_type{});
             };
             auto fused_s = [&](auto rt) {
-                if (steal) fused(rt, std::true_type{});
-                else fused(rt, std::false_type{});
+                if (steal) fused_g(rt, std::true_type{});
+                else fused_g(rt, std::false_type{});
             };
             if (robust) fused_s(std::true_type{});
             else fused_s(std::false_type{});
         } else {
             const size_t lds = size_t(s->stack_entries + 1) * dev::kBlock * 4;
             const dim3 grid(bx, by * frames), block(dev::kBlock);
-            auto primary = [&](auto rt) {
-                constexpr bool R = decltype(rt)::value;
-                if (stats) hipLaunchKernelGGL((dev::ceres_primary<true, R>), grid, block, lds, stream, P);
-                else hipLaunchKernelGGL((dev::ceres_primary<false, R>), grid, block, lds, stream, P);
+            auto primary = [&](auto rt, auto gt) {
+                constexpr bool R = decltype(rt)::value, G = decltype(gt)::value;
+                if (stats) hipLaunchKernelGGL((dev::ceres_primary<true, R, G>), grid, block, lds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_primary<false, R, G>), grid, block, lds, stream, P);
             };
-            if (robust) primary(std::true_type{});
-            else primary(std::false_type{});
+            auto primary_g = [&](auto rt) {
+                if (gfma) primary(rt, std::true_type{});
+                else primary(rt, std::false_type{});
+            };
+            if (robust) primary_g(std::true_type{});
+            else primary_g(std::false_type{});
         }
         HIP_TRY(hipGetLastError());
         if (e1) HIP_TRY(hipEventRecord(e1, stream));

@@ -5,7 +5,10 @@
 // the camera basis (render.hpp:91-97) and the binned-SAH BVH (binned_sah_builder.hpp:39-234).
 // These stay on the host, as in the north star; they produce the exact bits the gfx950
 // kernels consume, so every float operation follows the reference's order (the library is
-// compiled with -ffp-contract=off; the reference's explicit fmaf stays an fmaf).
+// compiled with -ffp-contract=off; the reference's explicit fmaf stays an fmaf).  Every step
+// comes in two arithmetic flavours (template G, CERES_ARITH_*): G = false is the reference
+// without contraction, G = true the reference as its own CMake build (g++ -O3 -mfma) compiles it,
+// an explicit fma at exactly the sites where GCC contracts (oracle/contraction_sites.txt).
 #include <algorithm>
 #include <array>
 #include <atomic>
@@ -40,6 +43,22 @@ template <class S> inline V3<S> scale(V3<S> a, S s) { return {a.x * s, a.y * s, 
 template <class S> inline S vdot(V3<S> a, V3<S> b) { S s = a.x * b.x; s += a.y * b.y; s += a.z * b.z; return s; }
 template <class S> inline V3<S> vcross(V3<S> a, V3<S> b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 template <class S> inline V3<S> vnormalize(V3<S> v) { S inv = S(1) / std::sqrt(vdot(v, v)); return scale(v, inv); }
+// GCC-contracted forms: dot -> fma(a2,b2, fma(a0,b0, a1 b1)); cross a_j b_k - a_k b_j ->
+// fma(a_j, b_k, -(a_k b_j)) (vector.hpp:134-167 as the reference's build fuses them)
+template <bool G, class S> inline S gdot(V3<S> a, V3<S> b) {
+    if constexpr (G) return std::fma(a.z, b.z, std::fma(a.x, b.x, a.y * b.y));
+    else return vdot(a, b);
+}
+template <bool G, class S> inline V3<S> gcross(V3<S> a, V3<S> b) {
+    if constexpr (G) return {std::fma(a.y, b.z, -(a.z * b.y)), std::fma(a.z, b.x, -(a.x * b.z)), std::fma(a.x, b.y, -(a.y * b.x))};
+    else return vcross(a, b);
+}
+template <bool G, class S> inline V3<S> gnormalize(V3<S> v) { S inv = S(1) / std::sqrt(gdot<G>(v, v)); return scale(v, inv); }
+// a * b + c * d (sub: a * b - c * d) with GCC's fusion of the first product
+template <bool G, class S> inline S gmad2(S a, S b, S c, S d, bool sub) {
+    if constexpr (G) return std::fma(a, b, sub ? -(c * d) : c * d);
+    else return sub ? a * b - c * d : a * b + c * d;
+}
 using Vec = V3<float>;
 
 template <class S> struct TriT { S p0[3], e1[3], e2[3], n[3]; };     // bvh::Triangle<S>
@@ -49,8 +68,8 @@ template <> struct NodeT<float> { float bounds[6]; uint32_t primitive_count, fir
 template <> struct NodeT<double> { double bounds[6]; uint64_t primitive_count, first_child_or_primitive; };
 static_assert(sizeof(NodeT<float>) == 32 && sizeof(NodeT<double>) == 64, "Node");
 
-template <class S> inline TriT<S> tri_from_points(V3<S> p0, V3<S> p1, V3<S> p2) {   // Triangle ctor, triangle.hpp:30-34
-    V3<S> e1 = p0 - p1, e2 = p2 - p0, n = vcross(e1, e2);
+template <bool G, class S> inline TriT<S> tri_from_points(V3<S> p0, V3<S> p1, V3<S> p2) {   // Triangle ctor, triangle.hpp:30-34
+    V3<S> e1 = p0 - p1, e2 = p2 - p0, n = gcross<G>(e1, e2);
     return TriT<S>{{p0.x, p0.y, p0.z}, {e1.x, e1.y, e1.z}, {e2.x, e2.y, e2.z}, {n.x, n.y, n.z}};
 }
 template <class S> inline V3<S> P0(const TriT<S>& t) { return {t.p0[0], t.p0[1], t.p0[2]}; }
@@ -62,7 +81,7 @@ template <class S> inline V3<S> N(const TriT<S>& t) { return {t.n[0], t.n[1], t.
 // Accumulates fan-triangulated faces and area-weighted (un-normalised, left-handed) face
 // normals per vertex in face order, exactly like obj_norms.hpp:84-115.  Vertex coordinates
 // are floats from strtof (obj_norms.hpp:78-80), widened for S = double.
-template <class S>
+template <class S, bool G>
 struct MeshBuilder {
     std::vector<V3<S>> verts, vn;
     std::vector<TriT<S>> tris;
@@ -70,13 +89,13 @@ struct MeshBuilder {
 
     void add_vertex(V3<S> v) { verts.push_back(v); vn.push_back({S(0), S(0), S(0)}); }
     void add_triangle(size_t a, size_t b, size_t c) {
-        tris.push_back(tri_from_points(verts[a], verts[b], verts[c]));
+        tris.push_back(tri_from_points<G>(verts[a], verts[b], verts[c]));
         V3<S> n = N(tris.back());
         vn[a] = vn[a] + n; vn[b] = vn[b] + n; vn[c] = vn[c] + n;
         corner.push_back(uint32_t(a)); corner.push_back(uint32_t(b)); corner.push_back(uint32_t(c));
     }
     int finish(S** tri, S** norm, size_t* n_tri) {
-        for (auto& n : vn) n = vnormalize(n);                // obj_norms.hpp:109-111
+        for (auto& n : vn) n = gnormalize<G>(n);             // obj_norms.hpp:109-111
         const size_t nt = tris.size();
         *n_tri = nt;
         *tri = static_cast<S*>(std::malloc(std::max<size_t>(1, nt * sizeof(TriT<S>))));
@@ -116,8 +135,8 @@ inline bool face_index(char** cursor, long* out) {
     return true;
 }
 
-template <class S>
-int parse_obj(const char* data, size_t len, MeshBuilder<S>& mb) {
+template <class S, bool G>
+int parse_obj(const char* data, size_t len, MeshBuilder<S, G>& mb) {
     constexpr size_t kMaxLine = 1024;                       // istream::getline(line, 1024)
     char line[kMaxLine];
     size_t pos = 0;
@@ -155,7 +174,7 @@ int parse_obj(const char* data, size_t len, MeshBuilder<S>& mb) {
     return CERES_OK;
 }
 
-template <class S>
+template <class S, bool G = false>
 int obj_load(const char* path, S** tri, S** norm, size_t* n_tri) {
     if (!path || !tri || !norm || !n_tri) return set_error(CERES_EINVAL, "ceres_obj_load: null argument");
     *tri = *norm = nullptr; *n_tri = 0;
@@ -166,16 +185,16 @@ int obj_load(const char* path, S** tri, S** norm, size_t* n_tri) {
         while ((got = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + got);
         std::fclose(f);
     }   // unreadable file: empty mesh, like obj_norms.hpp:123-126
-    MeshBuilder<S> mb;
+    MeshBuilder<S, G> mb;
     int rc = parse_obj(buf.data(), buf.size(), mb);
     if (rc) return rc;
     return mb.finish(tri, norm, n_tri);
 }
 
-template <class S>
+template <class S, bool G = false>
 int proc_mesh(int n, S** tri, S** norm, size_t* n_tri) {
     if (n < 2 || !tri || !norm || !n_tri) return set_error(CERES_EINVAL, "ceres_proc_mesh: need n >= 2");
-    MeshBuilder<S> mb;
+    MeshBuilder<S, G> mb;
     const size_t nv = size_t(n) * size_t(n);
     mb.verts.reserve(nv); mb.vn.reserve(nv);
     mb.tris.reserve(2 * size_t(n - 1) * size_t(n - 1));
@@ -195,22 +214,22 @@ int proc_mesh(int n, S** tri, S** norm, size_t* n_tri) {
     return mb.finish(tri, norm, n_tri);
 }
 
-template <class S>
+template <class S, bool G = false>
 int rotate_triangles(S* tri, size_t n_tri, int axis, S degrees) {         // render.hpp:24-44
     if ((!tri && n_tri) || axis < 0 || axis > 2) return set_error(CERES_EINVAL, "ceres_rotate_triangles: bad argument");
     const S pi = S(3.14159265359);
     const S c = std::cos(degrees * pi / S(180));
     const S s = std::sin(degrees * pi / S(180));
-    auto rot = [&](V3<S> p) -> V3<S> {
-        if (axis == 0) return {p.x, p.y * c - p.z * s, p.y * s + p.z * c};
-        if (axis == 1) return {p.x * c + p.z * s, p.y, -p.x * s + p.z * c};
-        return {p.x * c - p.y * s, p.x * s + p.y * c, p.z};
+    auto rot = [&](V3<S> p) -> V3<S> {                      // (GCC fuses each coordinate's first product)
+        if (axis == 0) return {p.x, gmad2<G>(p.y, c, p.z, s, true), gmad2<G>(p.y, s, p.z, c, false)};
+        if (axis == 1) return {gmad2<G>(p.x, c, p.z, s, false), p.y, gmad2<G>(-p.x, s, p.z, c, false)};
+        return {gmad2<G>(p.x, c, p.y, s, true), gmad2<G>(p.x, s, p.y, c, false), p.z};
     };
     TriT<S>* t = reinterpret_cast<TriT<S>*>(tri);
     #pragma omp parallel for schedule(static)
     for (size_t i = 0; i < n_tri; ++i) {
         const V3<S> p0 = P0(t[i]), p1 = P0(t[i]) - E1(t[i]), p2 = P0(t[i]) + E2(t[i]);   // p1(), p2()
-        t[i] = tri_from_points(rot(p0), rot(p1), rot(p2));
+        t[i] = tri_from_points<G>(rot(p0), rot(p1), rot(p2));
     }
     return CERES_OK;
 }
@@ -236,8 +255,20 @@ template <class S> inline void grow(BoxT<S>& a, const BoxT<S>& b) {
     a.hi = {greater(a.hi.x, b.hi.x), greater(a.hi.y, b.hi.y), greater(a.hi.z, b.hi.z)};
 }
 template <class S> inline S box_half_area(const BoxT<S>& b) { V3<S> d = b.hi - b.lo; return (d.x + d.y) * d.z + d.x * d.y; }
+// GCC fuses half_area's FIRST product in find_split's sweeps (binned_sah_builder.hpp:98,109) and
+// its SECOND in the node's max_split_cost (:179); the sweep's cost is fma(count, ha, right_cost)
+template <bool G, class S> inline S half_area_sweep(const BoxT<S>& b) {
+    V3<S> d = b.hi - b.lo;
+    if constexpr (G) return std::fma(d.x + d.y, d.z, d.x * d.y);
+    else return (d.x + d.y) * d.z + d.x * d.y;
+}
+template <bool G, class S> inline S half_area_node(const BoxT<S>& b) {
+    V3<S> d = b.hi - b.lo;
+    if constexpr (G) return std::fma(d.x, d.y, (d.x + d.y) * d.z);
+    else return (d.x + d.y) * d.z + d.x * d.y;
+}
 
-template <class S>
+template <class S, bool G>
 struct SahBuild {
     using Node = NodeT<S>;
     using Box = BoxT<S>;
@@ -283,12 +314,12 @@ struct SahBuild {
         for (int axis = 0; axis < 3; ++axis) {
             Bin* row = bins[axis];
             Box acc = empty_box<S>(); size_t cnt = 0;
-            for (size_t i = kBins - 1; i > 0; --i) { grow(acc, row[i].box); cnt += row[i].count; row[i].right = box_half_area(acc) * S(cnt); }
+            for (size_t i = kBins - 1; i > 0; --i) { grow(acc, row[i].box); cnt += row[i].count; row[i].right = half_area_sweep<G>(acc) * S(cnt); }
             acc = empty_box<S>(); cnt = 0;
             best_cost[axis] = std::numeric_limits<S>::max(); best_split[axis] = kBins;
             for (size_t i = 0; i + 1 < kBins; ++i) {
                 grow(acc, row[i].box); cnt += row[i].count;
-                S cost = box_half_area(acc) * S(cnt) + row[i + 1].right;
+                S cost = G ? std::fma(S(cnt), half_area_sweep<G>(acc), row[i + 1].right) : box_half_area(acc) * S(cnt) + row[i + 1].right;
                 if (cost < best_cost[axis]) { best_cost[axis] = cost; best_split[axis] = i + 1; }
             }
         }
@@ -296,7 +327,7 @@ struct SahBuild {
         if (best_cost[0] > best_cost[1]) axis = 1;
         if (best_cost[axis] > best_cost[2]) axis = 2;
         size_t split_at = best_split[axis];
-        const S leaf_cost = box_half_area(bb) * (S(n) - S(1));   // traversal_cost = 1
+        const S leaf_cost = half_area_node<G>(bb) * (S(n) - S(1));   // traversal_cost = 1
         if (best_split[axis] == kBins || best_cost[axis] >= leaf_cost) {
             if (n <= kMaxLeaf) return make_leaf();
             // largest_axis (bounding_box.hpp:53-59), then the 0.4 quantile of the bin counts
@@ -343,7 +374,7 @@ struct SahBuild {
     }
 };
 
-template <class S>
+template <class S, bool G = false>
 int bvh_build(const S* tri, size_t n_tri, NodeT<S>** nodes_out, size_t* n_nodes, uint64_t** prim64) {
     if (!tri || !nodes_out || !n_nodes || !prim64) return set_error(CERES_EINVAL, "ceres_bvh_build: null argument");
     if (n_tri == 0) return set_error(CERES_EINVAL, "The given scene is empty or cannot be loaded");
@@ -365,9 +396,9 @@ int bvh_build(const S* tri, size_t n_tri, NodeT<S>** nodes_out, size_t* n_nodes,
     std::vector<NodeT<S>> nodes(2 * n_tri + 1);
     std::vector<size_t> prim(n_tri);
     for (size_t i = 0; i < n_tri; ++i) prim[i] = i;
-    SahBuild<S> sb;
+    SahBuild<S, G> sb;
     sb.nodes = nodes.data(); sb.prim = prim.data(); sb.boxes = boxes.data(); sb.centers = centers.data();
-    SahBuild<S>::store_box(nodes[0], global);
+    SahBuild<S, G>::store_box(nodes[0], global);
     #pragma omp parallel
     #pragma omp single
     sb.run({0, 0, n_tri, 0});
@@ -382,12 +413,12 @@ int bvh_build(const S* tri, size_t n_tri, NodeT<S>** nodes_out, size_t* n_nodes,
 }
 
 // render.hpp:91-97 (the basis; eye is passed through by the callers)
-template <class S>
+template <class S, bool G = false>
 int camera_basis(const S dir[3], const S up[3], S fov_deg, size_t width, size_t height, S out9[9]) {
     if (!dir || !up || !out9 || !width || !height) return set_error(CERES_EINVAL, "ceres_camera_basis: bad argument");
-    const V3<S> d = vnormalize(V3<S>{dir[0], dir[1], dir[2]});
-    V3<S> u = vnormalize(vcross(d, V3<S>{up[0], up[1], up[2]}));
-    V3<S> v = vnormalize(vcross(u, d));
+    const V3<S> d = gnormalize<G>(V3<S>{dir[0], dir[1], dir[2]});
+    V3<S> u = gnormalize<G>(gcross<G>(d, V3<S>{up[0], up[1], up[2]}));
+    V3<S> v = gnormalize<G>(gcross<G>(u, d));
     const S w = std::tan(fov_deg * S(3.14159265 * (1.0 / 180.0) * 0.5));
     const S ratio = S(height) / S(width);
     u = scale(u, w);
@@ -400,19 +431,30 @@ int camera_basis(const S dir[3], const S up[3], S fov_deg, size_t width, size_t 
 // The orbit of anim.cpp:76-88: t = Transform<S>().rotate(axis, step / 180 * pi)
 // (transform.hpp:67-104, Markley-Crassidis matrix composed onto the identity) applied to the
 // camera eye, camera dir and sun once per frame; `up` is not rotated.
-template <class S>
+template <class S, bool G = false>
 int orbit_cameras(const S eye[3], const S dir[3], const S up[3], const S sun[3], S fov_deg, size_t width, size_t height,
                   const S axis[3], S step_deg, uint32_t n_frames, int rotate_first, S* basis12, S* sun3, S* dir3) {
     if (!eye || !dir || !up || !sun || !axis || !basis12 || !sun3 || !width || !height)
         return set_error(CERES_EINVAL, "ceres_orbit_cameras: bad argument");
     const S pi = S(3.14159265359);
     const S angle = step_deg / 180.0f * pi;                  // anim.cpp:77, a float literal 180
-    const V3<S> n = vnormalize(V3<S>{axis[0], axis[1], axis[2]});
+    const V3<S> n = gnormalize<G>(V3<S>{axis[0], axis[1], axis[2]});
     const S s = std::sin(angle), c = std::cos(angle);
+    // transform.hpp:80-96; GCC fuses every entry's outer (1-c) n_r * n_k product
+    auto ent = [&](S nr, S nk, S add, bool sub) -> S {       // (1-c) nr nk +/- add
+        const S cr = (1 - c) * nr;
+        if constexpr (G) return std::fma(cr, nk, sub ? -add : add);
+        else return sub ? cr * nk - add : cr * nk + add;
+    };
+    auto diag = [&](S nr) -> S {                             // c + (1-c) nr nr
+        const S cr = (1 - c) * nr;
+        if constexpr (G) return std::fma(cr, nr, c);
+        else return c + cr * nr;
+    };
     const S m[3][3] = {
-        {c + (1 - c) * n.x * n.x, (1 - c) * n.x * n.y + s * n.z, (1 - c) * n.x * n.z - s * n.y},
-        {(1 - c) * n.y * n.x - s * n.z, c + (1 - c) * n.y * n.y, (1 - c) * n.y * n.z + s * n.x},
-        {(1 - c) * n.z * n.x + s * n.y, (1 - c) * n.z * n.y - s * n.x, c + (1 - c) * n.z * n.z}};
+        {diag(n.x), ent(n.x, n.y, s * n.z, false), ent(n.x, n.z, s * n.y, true)},
+        {ent(n.y, n.x, s * n.z, true), diag(n.y), ent(n.y, n.z, s * n.x, false)},
+        {ent(n.z, n.x, s * n.y, false), ent(n.z, n.y, s * n.x, true), diag(n.z)}};
     S a[3][3];                                              // identity * m, summed like transform.hpp:96-102
     const S id[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
     for (int r = 0; r < 3; ++r)
@@ -421,17 +463,17 @@ int orbit_cameras(const S eye[3], const S dir[3], const S up[3], const S sun[3],
             for (int i = 0; i < 3; ++i) acc += id[r][i] * m[i][col];
             a[r][col] = acc;
         }
-    auto apply = [&](V3<S> p) -> V3<S> {                    // operator(), transform.hpp:106-112 (v = 0)
-        return {a[0][0] * p.x + a[0][1] * p.y + a[0][2] * p.z + S(0),
-                a[1][0] * p.x + a[1][1] * p.y + a[1][2] * p.z + S(0),
-                a[2][0] * p.x + a[2][1] * p.y + a[2][2] * p.z + S(0)};
+    auto apply = [&](V3<S> p) -> V3<S> {                    // operator(), transform.hpp:111-118 (v = 0)
+        return {gdot<G>(V3<S>{a[0][0], a[0][1], a[0][2]}, p) + S(0),
+                gdot<G>(V3<S>{a[1][0], a[1][1], a[1][2]}, p) + S(0),
+                gdot<G>(V3<S>{a[2][0], a[2][1], a[2][2]}, p) + S(0)};
     };
     V3<S> e{eye[0], eye[1], eye[2]}, d{dir[0], dir[1], dir[2]}, l{sun[0], sun[1], sun[2]};
     for (uint32_t f = 0; f < n_frames; ++f) {
         if (rotate_first || f > 0) { e = apply(e); d = apply(d); l = apply(l); }
         const S dv[3] = {d.x, d.y, d.z};
         basis12[12 * f] = e.x; basis12[12 * f + 1] = e.y; basis12[12 * f + 2] = e.z;
-        if (int rc = camera_basis(dv, up, fov_deg, width, height, basis12 + 12 * f + 3)) return rc;
+        if (int rc = camera_basis<S, G>(dv, up, fov_deg, width, height, basis12 + 12 * f + 3)) return rc;
         sun3[3 * f] = l.x; sun3[3 * f + 1] = l.y; sun3[3 * f + 2] = l.z;
         if (dir3) { dir3[3 * f] = d.x; dir3[3 * f + 1] = d.y; dir3[3 * f + 2] = d.z; }
     }
@@ -582,6 +624,7 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
     std::vector<Item> st;
     out.emplace_back();
     st.push_back({0, 0, 0});
+    size_t collapsed_records = 1;     // records made from sibling pairs (piece nodes excluded): a tree has at most one per pair
     while (!st.empty()) {
         const Item it = st.back(); st.pop_back();
         const SiblingPair& P = pairs[it.pair];
@@ -613,8 +656,9 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
                 if (int rc = leaf_word(ents[c].box, ents[c].count, ents[c].first, acc, w)) return rc;
                 rec.child[c] = w;
             } else {
-                if (out.size() > pairs.size() || ents[c].first >= pairs.size())   // a tree has fewer records than pairs
+                if (collapsed_records >= pairs.size() || ents[c].first >= pairs.size())   // a tree has no more records than pairs
                     return set_error(CERES_EINVAL, "build_shadow_bvh4: sibling pairs do not form a tree");
+                ++collapsed_records;
                 if (out.size() > kNode4MaxFirst) return set_error(CERES_EUNSUPPORTED, "shadow BVH4: more than 2^27 records");
                 const uint32_t idx = uint32_t(out.size());
                 rec.child[c] = node4_child(0, idx);
@@ -679,6 +723,48 @@ int ceres_orbit_cameras_f64(const double eye[3], const double dir[3], const doub
                             uint32_t n_frames, int rotate_first, double* basis12, double* sun3, double* dir3) {
     return orbit_cameras<double>(eye, dir, up, sun, fov_deg, width, height, axis, step_deg, n_frames, rotate_first,
                                  basis12, sun3, dir3);
+}
+
+// ---- the same steps in a chosen arithmetic (CERES_ARITH_EXACT / CERES_ARITH_FMA) ----
+static int bad_arith(int arith) {
+    return arith == CERES_ARITH_EXACT || arith == CERES_ARITH_FMA ? 0 : set_error(CERES_EINVAL, "unknown arithmetic %d", arith);
+}
+int ceres_obj_load_arith(const char* path, float** tri48, float** norm36, size_t* n_tri, int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? obj_load<float, true>(path, tri48, norm36, n_tri) : obj_load<float, false>(path, tri48, norm36, n_tri);
+}
+int ceres_proc_mesh_arith(int n, float** tri48, float** norm36, size_t* n_tri, int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? proc_mesh<float, true>(n, tri48, norm36, n_tri) : proc_mesh<float, false>(n, tri48, norm36, n_tri);
+}
+int ceres_rotate_triangles_arith(float* tri48, size_t n_tri, int axis, float degrees, int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? rotate_triangles<float, true>(tri48, n_tri, axis, degrees) : rotate_triangles<float, false>(tri48, n_tri, axis, degrees);
+}
+int ceres_bvh_build_arith(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64, int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    if (!nodes32) return set_error(CERES_EINVAL, "ceres_bvh_build: null argument");
+    NodeT<float>* nodes = nullptr;
+    const int rc = arith ? bvh_build<float, true>(tri48, n_tri, &nodes, n_nodes, prim64)
+                         : bvh_build<float, false>(tri48, n_tri, &nodes, n_nodes, prim64);
+    *nodes32 = reinterpret_cast<uint32_t*>(nodes);
+    return rc;
+}
+int ceres_camera_basis_arith(const float eye[3], const float dir[3], const float up[3], float fov_deg,
+                             size_t width, size_t height, float out9[9], int arith) {
+    (void)eye;
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? camera_basis<float, true>(dir, up, fov_deg, width, height, out9)
+                 : camera_basis<float, false>(dir, up, fov_deg, width, height, out9);
+}
+int ceres_orbit_cameras_arith(const float eye[3], const float dir[3], const float up[3], const float sun[3], float fov_deg,
+                              size_t width, size_t height, const float axis[3], float step_deg, uint32_t n_frames,
+                              int rotate_first, float* basis12, float* sun3, float* dir3, int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? orbit_cameras<float, true>(eye, dir, up, sun, fov_deg, width, height, axis, step_deg, n_frames,
+                                              rotate_first, basis12, sun3, dir3)
+                 : orbit_cameras<float, false>(eye, dir, up, sun, fov_deg, width, height, axis, step_deg, n_frames,
+                                               rotate_first, basis12, sun3, dir3);
 }
 
 }  // extern "C"

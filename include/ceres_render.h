@@ -47,7 +47,7 @@ typedef enum {
     CERES_MODE_ROBUST = 0x10, /* OR-ed flag: traverse with the library's RobustNodeIntersector
                                 (node_intersectors.hpp:54-79) instead of render()'s FastNodeIntersector;
                                 float scenes only */
-    CERES_MODE_QBVH4 = 0x20  /* OR-ed flag (full mode, float, not with ROBUST): shadow rays traverse
+    CERES_MODE_QBVH4 = 0x20, /* OR-ed flag (full mode, float, not with ROBUST): shadow rays traverse
                                 a COMPRESSED BVH4 -- 64-B nodes, child boxes quantised to 8 bits per
                                 bound, rounded outwards -- instead of the exact 128-B one.  Not
                                 bit-exact: a box can only grow, so every leaf the reference reaches
@@ -55,7 +55,25 @@ typedef enum {
                                 the reference's slab tests never reach (a lit pixel turns dark).
                                 Held to the SURVEY section 7 budget (+-1 LSB, <= 1e-5 of pixels),
                                 never the default (node_intersectors.hpp:35-47,83-103). */
+    CERES_MODE_FMA = 0x40    /* OR-ed flag: the arithmetic of the reference as its own CMake build
+                                compiles it (CMakeLists.txt:11-13, g++ -O3 -mavx2 -mfma, where GCC
+                                contracts a*b+c into FMA): an explicit fmaf at exactly the sites GCC
+                                fuses (primary direction render.hpp:111, Moller-Trumbore
+                                triangle.hpp:98-109, hit point :129-133, normalize/cross/dot
+                                vector.hpp:134-167, shading render.hpp:48-81; the list with the
+                                compiler evidence is oracle/contraction_sites.txt).  Bit-identical to
+                                _ref/ref_render (the reference-flag build) given a scene prepared with
+                                CERES_ARITH_FMA; without it, bit-identical to the -ffp-contract=off
+                                build.  Combines with ROBUST, QBVH4 and PRIMARY. */
 } ceres_mode;
+
+/* Arithmetic of the host scene preparation (the *_arith calls below): CERES_ARITH_EXACT is the
+ * reference compiled without contraction, CERES_ARITH_FMA the reference's own CMake build (the
+ * triangle normals cross(e1, e2), the rotation, the vertex-normal normalisation, the SAH costs,
+ * the camera basis and the orbit Transform all contract there, so that build's scene differs
+ * bit-wise from the exact one: pair it with CERES_MODE_FMA renders). */
+#define CERES_ARITH_EXACT 0
+#define CERES_ARITH_FMA   1
 
 typedef struct ceres_scene ceres_scene;
 
@@ -127,6 +145,20 @@ int ceres_orbit_cameras(const float eye[3], const float dir[3], const float up[3
                         float fov_deg, size_t width, size_t height, const float axis[3], float step_deg,
                         uint32_t n_frames, int rotate_first, float* basis12, float* sun3, float* dir3);
 void ceres_free(void* p);
+/* The six steps above in a chosen arithmetic, arith = CERES_ARITH_EXACT (= the calls above) or
+ * CERES_ARITH_FMA (the reference's own CMake build: obj_norms.hpp's normals, the Triangle
+ * constructor's cross product, rotate_triangles, the SAH costs of binned_sah_builder.hpp:98-109,179,
+ * the camera basis and Transform contract as GCC contracts them; oracle/contraction_sites.txt). */
+int ceres_obj_load_arith(const char* path, float** tri48, float** norm36, size_t* n_tri, int arith);
+int ceres_proc_mesh_arith(int n, float** tri48, float** norm36, size_t* n_tri, int arith);
+int ceres_rotate_triangles_arith(float* tri48, size_t n_tri, int axis, float degrees, int arith);
+int ceres_bvh_build_arith(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64,
+                          int arith);
+int ceres_camera_basis_arith(const float eye[3], const float dir[3], const float up[3], float fov_deg,
+                             size_t width, size_t height, float out9[9], int arith);
+int ceres_orbit_cameras_arith(const float eye[3], const float dir[3], const float up[3], const float sun[3],
+                              float fov_deg, size_t width, size_t height, const float axis[3], float step_deg,
+                              uint32_t n_frames, int rotate_first, float* basis12, float* sun3, float* dir3, int arith);
 
 /* ---- double precision (render<double>, anim.cpp's -d mode, anim.cpp:146-155) ----
  * The same host steps with Scalar = double: bvh::Triangle<double> (96 B), tri_norms as

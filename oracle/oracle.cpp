@@ -5,10 +5,15 @@
 //
 // A from-scratch restatement (not a copy) of iracigt/ceres-raytracer's render() path,
 // written so that every floating-point operation happens in the same order as in the
-// reference.  Compiled with -ffp-contract=off, it is bit-identical to the reference
-// headers compiled with -ffp-contract=off (oracle/_ref/ref_render_exact); against the
-// reference's own CMake flags (-mfma with GCC's default contraction) it differs only in a
-// few edge pixels (see tests/golden/*.json "ppm_bytes_differing_ref_vs_exact").
+// reference.  Compiled with -ffp-contract=off, and every function comes in two arithmetic
+// flavours selected by a `contract` argument:
+//   contract = 0  bit-identical to the reference headers compiled with -ffp-contract=off
+//                 (oracle/_ref/ref_render_exact);
+//   contract = 1  bit-identical to the reference as its own CMake build compiles it
+//                 (CMakeLists.txt:11-13, -O3 -mavx2 -mfma: GCC 11 fuses a*b+c into FMA at the
+//                 sites its widening_mul pass picks, oracle/_ref/ref_render).  Each such site is
+//                 an explicit fmaf here, read from `g++ -fdump-tree-widening_mul-lineno` of the
+//                 reference build (oracle/contraction_sites.txt lists them with file:line).
 //
 // Parity is PINNED: tests/test_oracle_golden.py checks this library against the golden
 // fixtures generated from the reference itself (tests/golden/make_golden.py): PPM
@@ -45,10 +50,22 @@ inline V3 cross(V3 a, V3 b) {                                                 //
 }
 inline V3 normalize(V3 v) { float inv = 1.0f / std::sqrt(dot(v, v)); return mul(v, inv); }   // vector.hpp:143-154
 
+// GCC-contracted forms (G = true) of the same expressions.  dot (vector.hpp:134-141) is
+// ((a0 b0 + a1 b1) + a2 b2); GCC fuses it as fma(a2, b2, fma(a0, b0, a1 b1)) ("A") everywhere
+// but in Triangle::intersect's v = dot(r, e1), where it fuses fma(a2, b2, fma(a1, b1, a0 b0))
+// ("B").  cross (vector.hpp:159-167) a_j b_k - a_k b_j becomes fma(a_j, b_k, -(a_k b_j)).
+template <bool G> inline float dotA(V3 a, V3 b) { return G ? std::fmaf(a.z, b.z, std::fmaf(a.x, b.x, a.y * b.y)) : dot(a, b); }
+template <bool G> inline float dotB(V3 a, V3 b) { return G ? std::fmaf(a.z, b.z, std::fmaf(a.y, b.y, a.x * b.x)) : dot(a, b); }
+template <bool G> inline V3 crossG(V3 a, V3 b) {
+    if (!G) return cross(a, b);
+    return {std::fmaf(a.y, b.z, -(a.z * b.y)), std::fmaf(a.z, b.x, -(a.x * b.z)), std::fmaf(a.x, b.y, -(a.y * b.x))};
+}
+template <bool G> inline V3 normalizeG(V3 v) { float inv = 1.0f / std::sqrt(dotA<G>(v, v)); return mul(v, inv); }
+
 // Triangle (triangle.hpp:17-37): p0, e1 = p0 - p1, e2 = p2 - p0, n = cross(e1, e2); 48 bytes.
 struct Tri { V3 p0, e1, e2, n; };
 static_assert(sizeof(Tri) == 48, "Triangle layout");
-inline Tri make_tri(V3 p0, V3 p1, V3 p2) { Tri t; t.p0 = p0; t.e1 = sub(p0, p1); t.e2 = sub(p2, p0); t.n = cross(t.e1, t.e2); return t; }
+template <bool G> inline Tri make_tri(V3 p0, V3 p1, V3 p2) { Tri t; t.p0 = p0; t.e1 = sub(p0, p1); t.e2 = sub(p2, p0); t.n = crossG<G>(t.e1, t.e2); return t; }
 inline V3 tri_p1(const Tri& t) { return sub(t.p0, t.e1); }                   // triangle.hpp:36
 inline V3 tri_p2(const Tri& t) { return add(t.p0, t.e2); }                   // triangle.hpp:37
 
@@ -66,6 +83,10 @@ inline void box_extend(Box& a, const Box& b) {                               // 
 }
 inline void box_extend(Box& a, V3 v) { box_extend(a, Box{v, v}); }
 inline float half_area(const Box& b) { V3 d = sub(b.hi, b.lo); return (d.x + d.y) * d.z + d.x * d.y; }   // bounding_box.hpp:43-46
+// GCC fuses half_area's first product inside find_split's sweeps (binned_sah_builder.hpp:98,109)
+// and its second product in the node's max_split_cost (:179)
+template <bool G> inline float half_area_sweep(const Box& b) { V3 d = sub(b.hi, b.lo); return G ? std::fmaf(d.x + d.y, d.z, d.x * d.y) : half_area(b); }
+template <bool G> inline float half_area_node(const Box& b) { V3 d = sub(b.hi, b.lo); return G ? std::fmaf(d.x, d.y, (d.x + d.y) * d.z) : half_area(b); }
 inline int largest_axis(const Box& b) {                                      // bounding_box.hpp:53-59
     V3 d = sub(b.hi, b.lo); int a = 0;
     if (d.x < d.y) a = 1;
@@ -97,7 +118,7 @@ bool read_index(char** pp, int* out) {                                       // 
 
 struct Mesh { std::vector<Tri> tris; std::vector<std::array<V3, 3>> norms; };
 
-int load_stream(std::istream& is, Mesh& m) {                                 // obj_norms.hpp:57-118
+template <bool G> int load_stream(std::istream& is, Mesh& m) {                                 // obj_norms.hpp:57-118
     static constexpr size_t max_line = 1024;
     char line[max_line];
     std::vector<V3> verts, vnorm;
@@ -119,7 +140,7 @@ int load_stream(std::istream& is, Mesh& m) {                                 // 
                 if (j >= verts.size()) { g_err = "OBJ face index out of range"; return -2; }   // obj_norms.hpp:90 assert
                 V3 v = verts[j];
                 if (i >= 2) {                                                // fan triangulation, obj_norms.hpp:92-98
-                    m.tris.push_back(make_tri(pts[0], pts[1], v));
+                    m.tris.push_back(make_tri<G>(pts[0], pts[1], v));
                     V3 n = m.tris.back().n;
                     vnorm[id[0]] = add(vnorm[id[0]], n);
                     vnorm[id[1]] = add(vnorm[id[1]], n);
@@ -130,7 +151,7 @@ int load_stream(std::istream& is, Mesh& m) {                                 // 
             }
         }
     }
-    for (auto& n : vnorm) n = normalize(n);                                  // obj_norms.hpp:109-111
+    for (auto& n : vnorm) n = normalizeG<G>(n);                              // obj_norms.hpp:109-111
     m.norms.reserve(tidx.size());
     for (auto& t : tidx) m.norms.push_back({vnorm[t[0]], vnorm[t[1]], vnorm[t[2]]});   // obj_norms.hpp:113-115
     return 0;
@@ -151,7 +172,7 @@ constexpr size_t kBins = 16;
 struct Bin { Box box; size_t count; float right_cost; };
 struct Item { size_t node, begin, end, depth; size_t size() const { return end - begin; } };
 
-struct Builder {
+template <bool G> struct Builder {
     std::vector<Node> nodes;
     std::vector<size_t> prim;
     const Box* boxes; const V3* centers;
@@ -166,12 +187,13 @@ struct Builder {
     std::pair<float, size_t> find_split(int axis) {                          // binned_sah_builder.hpp:89-114
         Bin* b = bins[axis];
         Box cur = box_empty(); size_t cnt = 0;
-        for (size_t i = kBins - 1; i > 0; --i) { box_extend(cur, b[i].box); cnt += b[i].count; b[i].right_cost = half_area(cur) * cnt; }
+        for (size_t i = kBins - 1; i > 0; --i) { box_extend(cur, b[i].box); cnt += b[i].count; b[i].right_cost = half_area_sweep<G>(cur) * cnt; }
         cur = box_empty(); cnt = 0;
         std::pair<float, size_t> best(FLT_MAX, kBins);
         for (size_t i = 0; i < kBins - 1; ++i) {
             box_extend(cur, b[i].box); cnt += b[i].count;
-            float cost = half_area(cur) * cnt + b[i + 1].right_cost;
+            float cost = G ? std::fmaf(float(cnt), half_area_sweep<G>(cur), b[i + 1].right_cost)
+                           : half_area(cur) * cnt + b[i + 1].right_cost;
             if (cost < best.first) best = {cost, i + 1};
         }
         return best;
@@ -201,7 +223,7 @@ struct Builder {
         if (best[0].first > best[1].first) ax = 1;
         if (best[ax].first > best[2].first) ax = 2;
         size_t split = best[ax].second;
-        float max_cost = half_area(bb) * (it.size() - traversal_cost);
+        float max_cost = half_area_node<G>(bb) * (it.size() - traversal_cost);
         if (best[ax].second == kBins || best[ax].first >= max_cost) {
             if (it.size() > max_leaf) {                                      // median-ish fallback, :180-196
                 ax = largest_axis(bb);
@@ -234,22 +256,22 @@ struct Ctx {
 };
 
 // Triangle::intersect, triangle.hpp:95-115 (left-handed normal)
-inline bool tri_hit(const Tri& tr, V3 o, V3 d, float tmin, float tmax, float* t, float* u, float* v) {
+template <bool G> inline bool tri_hit(const Tri& tr, V3 o, V3 d, float tmin, float tmax, float* t, float* u, float* v) {
     V3 c = sub(tr.p0, o);
-    V3 r = cross(d, c);
-    float inv_det = 1.0f / dot(tr.n, d);
-    float uu = dot(r, tr.e2) * inv_det;
-    float vv = dot(r, tr.e1) * inv_det;
+    V3 r = crossG<G>(d, c);
+    float inv_det = 1.0f / dotA<G>(tr.n, d);
+    float uu = dotA<G>(r, tr.e2) * inv_det;
+    float vv = dotB<G>(r, tr.e1) * inv_det;
     float ww = 1.0f - uu - vv;
     if (uu >= 0 && vv >= 0 && ww >= 0) {
-        float tt = dot(tr.n, c) * inv_det;
+        float tt = dotA<G>(tr.n, c) * inv_det;
         if (tt >= tmin && tt <= tmax) { *t = tt; *u = uu; *v = vv; return true; }
     }
     return false;
 }
 
 // Closest-hit traversal with statistics; returns true on hit.  Stack overflow sets *ovf.
-bool traverse(const Ctx& cx, V3 o, V3 d, Hit* best, uint64_t* pairs, uint64_t* tests, bool* ovf, bool robust = false) {
+template <bool G> bool traverse(const Ctx& cx, V3 o, V3 d, Hit* best, uint64_t* pairs, uint64_t* tests, bool* ovf, bool robust = false) {
     float tmin = 0.0f, tmax = FLT_MAX;                                       // ray.hpp:17-21
     bool have = false;
     auto leaf = [&](const Node& n) {                                         // intersect_leaf :43-63
@@ -258,7 +280,7 @@ bool traverse(const Ctx& cx, V3 o, V3 d, Hit* best, uint64_t* pairs, uint64_t* t
         for (size_t i = b; i < e; ++i) {
             size_t idx = size_t(cx.prim[i]);                                 // primitive_at, primitive_intersectors.hpp:17-20
             float t, u, v;
-            if (tri_hit(cx.tris[idx], o, d, tmin, tmax, &t, &u, &v)) { *best = {uint32_t(idx), t, u, v}; have = true; tmax = t; }
+            if (tri_hit<G>(cx.tris[idx], o, d, tmin, tmax, &t, &u, &v)) { *best = {uint32_t(idx), t, u, v}; have = true; tmax = t; }
         }
     };
     if (cx.nodes[0].count != 0) { leaf(cx.nodes[0]); return have; }          // root-is-leaf, :72-73
@@ -320,20 +342,27 @@ bool traverse(const Ctx& cx, V3 o, V3 d, Hit* best, uint64_t* pairs, uint64_t* t
 }
 
 // ---------------------------------------------------------------- shading (render.hpp:46-84)
-inline float lambertian(V3 s, V3 n) { return std::fabs(s.x * n.x + s.y * n.y + s.z * n.z); }
-inline float blinn_phong_spec(V3 s, V3 n, V3 view) { return (float)std::pow((double)dot(n, normalize(add(s, view))), 24.0); }
+// lambertian's sum (render.hpp:48) contracts like dot "A"; in smooth_shading GCC fuses
+// amb + 0.5 lam into fma(lam, 0.5, amb) and each channel's (amb + diffuse) * k + specular into
+// fma(amb + diffuse, k, specular) (render.hpp:67-81); the c[] accumulation stays unfused.
+template <bool G> inline float lambertian(V3 s, V3 n) { return G ? std::fabs(dotA<true>(s, n)) : std::fabs(s.x * n.x + s.y * n.y + s.z * n.z); }
+template <bool G> inline float blinn_phong_spec(V3 s, V3 n, V3 view) { return (float)std::pow((double)dotA<G>(n, normalizeG<G>(add(s, view))), 24.0); }
 inline float clampf(float v, float lo, float hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }   // std::clamp
-inline void smooth_shading(V3 sun_line, const std::array<V3, 3>& N, V3 view, float u, float v, float c[3]) {
+template <bool G> inline void smooth_shading(V3 sun_line, const std::array<V3, 3>& N, V3 view, float u, float v, float c[3]) {
     c[0] = c[1] = c[2] = 0.f;
     const float amb = 0.2;
     const V3 vneg = mul(view, -1.0f);
     const float w[3] = {u, v, 1 - u - v};
     for (int k = 0; k < 3; ++k) {
-        float diffuse = 0.5f * lambertian(sun_line, N[k]);
-        float specular = 0.8f * blinn_phong_spec(sun_line, N[k], vneg);
-        c[0] += w[k] * clampf((amb + diffuse) * 0.5f + specular, 0.f, 1.f);
-        c[1] += w[k] * clampf((amb + diffuse) * 0.0f + specular, 0.f, 1.f);
-        c[2] += w[k] * clampf((amb + diffuse) * 0.8f + specular, 0.f, 1.f);
+        const float lam = lambertian<G>(sun_line, N[k]);
+        float specular = 0.8f * blinn_phong_spec<G>(sun_line, N[k], vneg);
+        const float base = G ? std::fmaf(lam, 0.5f, amb) : amb + 0.5f * lam;
+        const float kr = G ? std::fmaf(base, 0.5f, specular) : base * 0.5f + specular;
+        const float kg = G ? std::fmaf(base, 0.0f, specular) : base * 0.0f + specular;
+        const float kb = G ? std::fmaf(base, 0.8f, specular) : base * 0.8f + specular;
+        c[0] += w[k] * clampf(kr, 0.f, 1.f);
+        c[1] += w[k] * clampf(kg, 0.f, 1.f);
+        c[2] += w[k] * clampf(kb, 0.f, 1.f);
     }
 }
 
@@ -382,25 +411,25 @@ int oracle_bvh_canonical(const uint32_t* nodes32, size_t n_nodes, const uint64_t
     return 0;
 }
 
-int oracle_load_obj(const char* path, float** tri48, float** norm36, size_t* n_tri) {   // obj_norms.hpp:120-127
+int oracle_load_obj(const char* path, float** tri48, float** norm36, size_t* n_tri, int contract) {   // obj_norms.hpp:120-127
     std::ifstream is(path);
     Mesh m;
-    if (is) { int rc = load_stream(is, m); if (rc) return rc; }
+    if (is) { int rc = contract ? load_stream<true>(is, m) : load_stream<false>(is, m); if (rc) return rc; }
     return export_mesh(m, tri48, norm36, n_tri);
 }
 
-int oracle_load_obj_text(const char* text, size_t len, float** tri48, float** norm36, size_t* n_tri) {
+int oracle_load_obj_text(const char* text, size_t len, float** tri48, float** norm36, size_t* n_tri, int contract) {
     std::istringstream is(std::string(text, len));
     Mesh m;
-    int rc = load_stream(is, m);
+    int rc = contract ? load_stream<true>(is, m) : load_stream<false>(is, m);
     if (rc) return rc;
     return export_mesh(m, tri48, norm36, n_tri);
 }
 
-// Procedural heightfield (SURVEY.md §8(d) C5): n x n vertices on [0,1]^2, two triangles per
-// quad ("f a b c" / "f a c d"), vertex = float(x), float(y), float(z(x,y)) computed in double.
-// Equivalent to feeding the OBJ text of oracle/ref_harness.cpp:proc_obj through the loader.
-int oracle_proc_mesh(int n, float** tri48, float** norm36, size_t* n_tri) {
+}  // extern "C"
+
+namespace {
+template <bool G> int proc_mesh(int n, float** tri48, float** norm36, size_t* n_tri) {
     if (n < 2) { g_err = "proc mesh needs n >= 2"; return -1; }
     std::vector<V3> verts(size_t(n) * n), vnorm(size_t(n) * n, V3{0.f, 0.f, 0.f});
     for (int j = 0; j < n; ++j)
@@ -418,41 +447,42 @@ int oracle_proc_mesh(int n, float** tri48, float** norm36, size_t* n_tri) {
             size_t a = size_t(j) * n + i, b = a + 1, c = a + n + 1, d = a + n;
             const size_t f[2][3] = {{a, b, c}, {a, c, d}};
             for (auto& q : f) {
-                m.tris.push_back(make_tri(verts[q[0]], verts[q[1]], verts[q[2]]));
+                m.tris.push_back(make_tri<G>(verts[q[0]], verts[q[1]], verts[q[2]]));
                 V3 nn = m.tris.back().n;
                 for (int k = 0; k < 3; ++k) vnorm[q[k]] = add(vnorm[q[k]], nn);
                 tidx.push_back({q[0], q[1], q[2]});
             }
         }
-    for (auto& v : vnorm) v = normalize(v);
+    for (auto& v : vnorm) v = normalizeG<G>(v);
     m.norms.reserve(nt);
     for (auto& t : tidx) m.norms.push_back({vnorm[t[0]], vnorm[t[1]], vnorm[t[2]]});
     return export_mesh(m, tri48, norm36, n_tri);
 }
 
-// rotate_triangles<Axis> (render.hpp:24-44): cos/sin of degrees*pi/180 in float, then rebuild
-// each Triangle from p0, p1() = p0 - e1, p2() = p0 + e2.
-void oracle_rotate(float* tri48, size_t n, int axis, float degrees) {
+// rotate_triangles<Axis> (render.hpp:24-44).  GCC fuses each rotated coordinate's first product:
+// p1 c - p2 s -> fma(p1, c, -(p2 s)), p1 s + p2 c -> fma(p1, s, p2 c), -p0 s + p2 c -> fma(-p0, s, p2 c).
+template <bool G> void rotate(float* tri48, size_t n, int axis, float degrees) {
     const float pi = float(3.14159265359);
     float c = std::cos(degrees * pi / float(180));
     float s = std::sin(degrees * pi / float(180));
+    auto f2 = [](float a, float b, float x, float y, bool minus) {      // a*b -/+ x*y
+        if (G) return std::fmaf(a, b, minus ? -(x * y) : x * y);
+        return minus ? a * b - x * y : a * b + x * y;
+    };
     auto rot = [&](V3 p) -> V3 {
-        if (axis == 0) return {p.x, p.y * c - p.z * s, p.y * s + p.z * c};
-        if (axis == 1) return {p.x * c + p.z * s, p.y, -p.x * s + p.z * c};
-        return {p.x * c - p.y * s, p.x * s + p.y * c, p.z};
+        if (axis == 0) return {p.x, f2(p.y, c, p.z, s, true), f2(p.y, s, p.z, c, false)};
+        if (axis == 1) return {f2(p.x, c, p.z, s, false), p.y, f2(-p.x, s, p.z, c, false)};
+        return {f2(p.x, c, p.y, s, true), f2(p.x, s, p.y, c, false), p.z};
     };
     Tri* t = reinterpret_cast<Tri*>(tri48);
     #pragma omp parallel for
     for (size_t i = 0; i < n; ++i) {
         V3 p0 = rot(t[i].p0), p1 = rot(tri_p1(t[i])), p2 = rot(tri_p2(t[i]));
-        t[i] = make_tri(p0, p1, p2);
+        t[i] = make_tri<G>(p0, p1, p2);
     }
 }
 
-// compute_bounding_boxes_and_centers + compute_bounding_boxes_union (utilities.hpp:142-171)
-// + BinnedSahBuilder<Bvh,16>::build (binned_sah_builder.hpp:39-66), single-threaded:
-// the topology (and leaf primitive order) is the reference's; node numbering may differ.
-int oracle_build_bvh(const float* tri48, size_t n, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64) {
+template <bool G> int build_bvh(const float* tri48, size_t n, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64) {
     if (n == 0) { g_err = "empty scene"; return -1; }
     const Tri* t = reinterpret_cast<const Tri*>(tri48);
     std::vector<Box> boxes(n); std::vector<V3> centers(n);
@@ -463,12 +493,12 @@ int oracle_build_bvh(const float* tri48, size_t n, uint32_t** nodes32, size_t* n
     }
     Box global = box_empty();
     for (size_t i = 0; i < n; ++i) box_extend(global, boxes[i]);
-    Builder B;
+    Builder<G> B;
     B.nodes.assign(2 * n + 1, Node{});
     B.prim.resize(n);
     for (size_t i = 0; i < n; ++i) B.prim[i] = i;
     B.boxes = boxes.data(); B.centers = centers.data();
-    Builder::set_box(B.nodes[0], global);
+    Builder<G>::set_box(B.nodes[0], global);
     std::vector<Item> stack{{0, 0, n, 0}};                                   // top_down_builder.hpp:47-72
     while (!stack.empty()) {
         Item it = stack.back(); stack.pop_back();
@@ -487,22 +517,29 @@ int oracle_build_bvh(const float* tri48, size_t n, uint32_t** nodes32, size_t* n
     return 0;
 }
 
-// anim.cpp:76-88 orbit step: Transform<float>().rotate(axis, step/180*pi) (transform.hpp:67-104)
-// then operator() (transform.hpp:106-112) on eye, dir and sun, `count` times, in place.
-void oracle_orbit(const float axis[3], float step_deg, int count, float eye[3], float dir[3], float sun[3]) {
+// Transform::rotate (transform.hpp:67-104) then operator() (:111-118).  GCC fuses every matrix
+// entry's (1-c) n_r * n_k product (c + (1-c) n_r n_r -> fma((1-c) n_r, n_r, c); off-diagonal
+// fma((1-c) n_r, n_k, +/-(s n_j))) and applies the rows as dot "A" (then + v = 0).
+template <bool G> void orbit(const float axis[3], float step_deg, int count, float eye[3], float dir[3], float sun[3]) {
     const float pi = float(3.14159265359);
     const float angle = step_deg / 180.0f * pi;
-    const V3 n = normalize(V3{axis[0], axis[1], axis[2]});
+    const V3 n = normalizeG<G>(V3{axis[0], axis[1], axis[2]});
     const float nv[3] = {n.x, n.y, n.z};
     const float s = std::sin(angle), c = std::cos(angle);
     float m[3][3];
-    for (int r = 0; r < 3; ++r)
-        for (int k = 0; k < 3; ++k) m[r][k] = (1 - c) * nv[r] * nv[k];
+    const float sn[3] = {s * nv[0], s * nv[1], s * nv[2]};
     // Markley-Crassidis: diagonal c + (1-c) n_r n_r; off-diagonal (1-c) n_r n_k -/+ s n_j
-    m[0][0] = c + m[0][0]; m[1][1] = c + m[1][1]; m[2][2] = c + m[2][2];
-    m[0][1] = m[0][1] + s * nv[2]; m[0][2] = m[0][2] - s * nv[1];
-    m[1][0] = m[1][0] - s * nv[2]; m[1][2] = m[1][2] + s * nv[0];
-    m[2][0] = m[2][0] + s * nv[1]; m[2][1] = m[2][1] - s * nv[0];
+    const float sign[3][3] = {{0, 1, -1}, {-1, 0, 1}, {1, -1, 0}};
+    const int other[3][3] = {{0, 2, 1}, {2, 0, 0}, {1, 0, 0}};
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) {
+            const float cr = (1 - c) * nv[r];
+            if (r == k) m[r][k] = G ? std::fmaf(cr, nv[k], c) : c + cr * nv[k];
+            else {
+                const float t = sign[r][k] > 0 ? sn[other[r][k]] : -sn[other[r][k]];
+                m[r][k] = G ? std::fmaf(cr, nv[k], t) : (sign[r][k] > 0 ? cr * nv[k] + sn[other[r][k]] : cr * nv[k] - sn[other[r][k]]);
+            }
+        }
     float a[3][3];
     for (int r = 0; r < 3; ++r)                    // ret.a = identity * mat, accumulated from 0
         for (int k = 0; k < 3; ++k) {
@@ -512,19 +549,17 @@ void oracle_orbit(const float axis[3], float step_deg, int count, float eye[3], 
         }
     auto apply = [&](float* p) {
         float q[3];
-        for (int r = 0; r < 3; ++r) q[r] = a[r][0] * p[0] + a[r][1] * p[1] + a[r][2] * p[2] + 0.0f;
+        for (int r = 0; r < 3; ++r) q[r] = dotA<G>(V3{a[r][0], a[r][1], a[r][2]}, V3{p[0], p[1], p[2]}) + 0.0f;
         p[0] = q[0]; p[1] = q[1]; p[2] = q[2];
     };
     for (int k = 0; k < count; ++k) { apply(eye); apply(dir); apply(sun); }
 }
 
 // Camera basis, render.hpp:91-97.  out = {dir, image_u*w, image_v*w*ratio}.
-void oracle_camera_basis(const float eye[3], const float dir[3], const float up[3], float fov,
-                         size_t W, size_t H, float out[9]) {
-    (void)eye;
-    V3 d = normalize(V3{dir[0], dir[1], dir[2]});
-    V3 u = normalize(cross(d, V3{up[0], up[1], up[2]}));
-    V3 v = normalize(cross(u, d));
+template <bool G> void camera_basis(const float dir[3], const float up[3], float fov, size_t W, size_t H, float out[9]) {
+    V3 d = normalizeG<G>(V3{dir[0], dir[1], dir[2]});
+    V3 u = normalizeG<G>(crossG<G>(d, V3{up[0], up[1], up[2]}));
+    V3 v = normalizeG<G>(crossG<G>(u, d));
     float w = std::tan(fov * float(3.14159265 * (1.0 / 180.0) * 0.5));
     float ratio = float(H) / float(W);
     u = mul(u, w);
@@ -532,18 +567,59 @@ void oracle_camera_basis(const float eye[3], const float dir[3], const float up[
     float o[9] = {d.x, d.y, d.z, u.x, u.y, u.z, v.x, v.y, v.z};
     std::memcpy(out, o, sizeof o);
 }
+}  // namespace
+
+extern "C" {
+
+// Procedural heightfield (SURVEY.md §8(d) C5): n x n vertices on [0,1]^2, two triangles per
+// quad ("f a b c" / "f a c d"), vertex = float(x), float(y), float(z(x,y)) computed in double
+// without contraction (the mesh is an input, the same in both arithmetic flavours).
+// Equivalent to feeding the OBJ text of oracle/ref_harness.cpp:proc_obj through the loader.
+int oracle_proc_mesh(int n, float** tri48, float** norm36, size_t* n_tri, int contract) {
+    return contract ? proc_mesh<true>(n, tri48, norm36, n_tri) : proc_mesh<false>(n, tri48, norm36, n_tri);
+}
+
+// rotate_triangles<Axis> (render.hpp:24-44): cos/sin of degrees*pi/180 in float, then rebuild
+// each Triangle from p0, p1() = p0 - e1, p2() = p0 + e2.
+void oracle_rotate(float* tri48, size_t n, int axis, float degrees, int contract) {
+    if (contract) rotate<true>(tri48, n, axis, degrees); else rotate<false>(tri48, n, axis, degrees);
+}
+
+// compute_bounding_boxes_and_centers + compute_bounding_boxes_union (utilities.hpp:142-171)
+// + BinnedSahBuilder<Bvh,16>::build (binned_sah_builder.hpp:39-66), single-threaded:
+// the topology (and leaf primitive order) is the reference's; node numbering may differ.
+int oracle_build_bvh(const float* tri48, size_t n, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64, int contract) {
+    return contract ? build_bvh<true>(tri48, n, nodes32, n_nodes, prim64) : build_bvh<false>(tri48, n, nodes32, n_nodes, prim64);
+}
+
+// anim.cpp:76-88 orbit step: Transform<float>().rotate(axis, step/180*pi) (transform.hpp:67-104)
+// then operator() (transform.hpp:106-112) on eye, dir and sun, `count` times, in place.
+void oracle_orbit(const float axis[3], float step_deg, int count, float eye[3], float dir[3], float sun[3], int contract) {
+    if (contract) orbit<true>(axis, step_deg, count, eye, dir, sun); else orbit<false>(axis, step_deg, count, eye, dir, sun);
+}
+
+void oracle_camera_basis(const float eye[3], const float dir[3], const float up[3], float fov,
+                         size_t W, size_t H, float out[9], int contract) {
+    (void)eye;
+    if (contract) camera_basis<true>(dir, up, fov, W, H, out); else camera_basis<false>(dir, up, fov, W, H, out);
+}
 
 // render() (render.hpp:86-156) over the full framebuffer.
 //   mode 0: primary + shadow + smooth shading; mode 1: primary only, pixel = |normalize(n)|;
 //   | 0x10: RobustNodeIntersector traversal instead of FastNodeIntersector
+//   | 0x20: the reference-flag arithmetic (GCC contraction, see the header)
 //   pixels: 3*W*H floats (row j=0 at the bottom, render.hpp:107) or null
 //   ppm:    3*W*H bytes of the P6 body (rows top-down, static.cpp:137-145) or null
 //   rec_*:  optional per-pixel records (prim -1 on miss; shadow -1 none / 0 lit / 1 occluded)
 //   counts: {rays, hits, primary_pairs, primary_tests, shadow_pairs, shadow_tests}
-int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const uint32_t* nodes32, size_t n_nodes,
-                  const uint64_t* prim64, const float eye[3], const float basis[9], const float sun[3], int mode,
-                  size_t W, size_t H, float* pixels, uint8_t* ppm, int32_t* rec_prim, float* rec_tuv,
-                  int8_t* rec_shadow, uint64_t counts[6], int threads, uint32_t* rec_pairs) {
+}  // extern "C"
+
+namespace {
+template <bool G>
+int render_impl(const float* tri48, const float* norm36, size_t n_tri, const uint32_t* nodes32, size_t n_nodes,
+                const uint64_t* prim64, const float eye[3], const float basis[9], const float sun[3], int mode,
+                size_t W, size_t H, float* pixels, uint8_t* ppm, int32_t* rec_prim, float* rec_tuv,
+                int8_t* rec_shadow, uint64_t counts[6], int threads, uint32_t* rec_pairs) {
     if (n_tri == 0 || n_nodes == 0) { g_err = "empty scene"; return -1; }
     const bool robust = (mode & 0x10) != 0;
     mode &= 0xf;
@@ -564,10 +640,13 @@ int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const u
             size_t index = 3 * (W * j + i);
             float u = 2 * (i + float(0.5)) / float(W) - float(1);          // render.hpp:109-111
             float v = 2 * (j + float(0.5)) / float(H) - float(1);
-            V3 view = normalize(add(add(mul(IU, u), mul(IV, v)), D));
+            // iu*u + iv*v + dir; GCC fuses the iv*v product: dir + fma(iv, v, iu*u)
+            V3 view = G ? normalizeG<G>(V3{D.x + std::fmaf(IV.x, v, IU.x * u), D.y + std::fmaf(IV.y, v, IU.y * u),
+                                            D.z + std::fmaf(IV.z, v, IU.z * u)})
+                        : normalize(add(add(mul(IU, u), mul(IV, v)), D));
             Hit h{}; bool ovf = false;
             const uint64_t pp0 = pp, sp0 = sp_;
-            bool hit = traverse(cx, E, view, &h, &pp, &pt, &ovf, robust);
+            bool hit = traverse<G>(cx, E, view, &h, &pp, &pt, &ovf, robust);
             rays++;
             float c[3] = {0.f, 0.f, 0.f};
             int32_t rp = -1; int8_t rs = -1;
@@ -575,19 +654,28 @@ int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const u
                 hits++;
                 rp = int32_t(h.prim);
                 const Tri& tr = cx.tris[h.prim];
-                V3 normal = normalize(tr.n);
+                V3 normal = normalizeG<G>(tr.n);
                 if (mode == 1) {                                             // render.hpp:123-125
                     c[0] = std::fabs(normal.x); c[1] = std::fabs(normal.y); c[2] = std::fabs(normal.z);
                 } else {
                     float hu = h.u, hv = h.v;                                // render.hpp:127-135
-                    V3 p = add(add(mul(tr.p0, hu), mul(tri_p1(tr), hv)), mul(tri_p2(tr), 1 - hu - hv));
                     float scale = -0.00001;
-                    p = add(p, mul(normal, scale));
-                    V3 sun_line = normalize(sub(S, p));
+                    V3 p;
+                    if (G) {                                                 // fma(n, scale, fma(w, p2, fma(v, p1, u p0)))
+                        const float w = 1 - hu - hv;
+                        const V3 p1 = tri_p1(tr), p2 = tri_p2(tr);
+                        p = {std::fmaf(normal.x, scale, std::fmaf(w, p2.x, std::fmaf(hv, p1.x, hu * tr.p0.x))),
+                             std::fmaf(normal.y, scale, std::fmaf(w, p2.y, std::fmaf(hv, p1.y, hu * tr.p0.y))),
+                             std::fmaf(normal.z, scale, std::fmaf(w, p2.z, std::fmaf(hv, p1.z, hu * tr.p0.z)))};
+                    } else {
+                        p = add(add(mul(tr.p0, hu), mul(tri_p1(tr), hv)), mul(tri_p2(tr), 1 - hu - hv));
+                        p = add(p, mul(normal, scale));
+                    }
+                    V3 sun_line = normalizeG<G>(sub(S, p));
                     Hit h2{};
-                    bool sh = traverse(cx, p, sun_line, &h2, &sp_, &st, &ovf, robust);   // render.hpp:136-138
+                    bool sh = traverse<G>(cx, p, sun_line, &h2, &sp_, &st, &ovf, robust);   // render.hpp:136-138
                     rays++;
-                    if (!sh) { smooth_shading(sun_line, norms[h.prim], view, hu, hv, c); rs = 0; }
+                    if (!sh) { smooth_shading<G>(sun_line, norms[h.prim], view, hu, hv, c); rs = 0; }
                     else { hits++; rs = 1; }
                 }
             }
@@ -608,5 +696,13 @@ int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const u
     if (ovf_any) { g_err = "traversal stack overflow (64 entries)"; return -4; }
     return 0;
 }
+}  // namespace
 
-}  // extern "C"
+extern "C" int oracle_render(const float* tri48, const float* norm36, size_t n_tri, const uint32_t* nodes32, size_t n_nodes,
+                             const uint64_t* prim64, const float eye[3], const float basis[9], const float sun[3], int mode,
+                             size_t W, size_t H, float* pixels, uint8_t* ppm, int32_t* rec_prim, float* rec_tuv,
+                             int8_t* rec_shadow, uint64_t counts[6], int threads, uint32_t* rec_pairs) {
+    auto f = (mode & 0x20) ? render_impl<true> : render_impl<false>;
+    return f(tri48, norm36, n_tri, nodes32, n_nodes, prim64, eye, basis, sun, mode & ~0x20, W, H, pixels, ppm,
+             rec_prim, rec_tuv, rec_shadow, counts, threads, rec_pairs);
+}

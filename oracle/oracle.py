@@ -34,15 +34,17 @@ def lib():
             build()
         L = ctypes.CDLL(LIB_PATH)
         L.oracle_last_error.restype = ctypes.c_char_p
-        L.oracle_load_obj.argtypes = [ctypes.c_char_p, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz)]
-        L.oracle_load_obj_text.argtypes = [ctypes.c_char_p, _sz, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz)]
-        L.oracle_proc_mesh.argtypes = [ctypes.c_int, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz)]
-        L.oracle_rotate.argtypes = [_fp, _sz, ctypes.c_int, ctypes.c_float]
+        L.oracle_load_obj.argtypes = [ctypes.c_char_p, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz),
+                                      ctypes.c_int]
+        L.oracle_load_obj_text.argtypes = [ctypes.c_char_p, _sz, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz),
+                                           ctypes.c_int]
+        L.oracle_proc_mesh.argtypes = [ctypes.c_int, ctypes.POINTER(_fp), ctypes.POINTER(_fp), ctypes.POINTER(_sz), ctypes.c_int]
+        L.oracle_rotate.argtypes = [_fp, _sz, ctypes.c_int, ctypes.c_float, ctypes.c_int]
         L.oracle_rotate.restype = None
-        L.oracle_build_bvh.argtypes = [_fp, _sz, ctypes.POINTER(_u32p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p)]
-        L.oracle_camera_basis.argtypes = [_fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp]
+        L.oracle_build_bvh.argtypes = [_fp, _sz, ctypes.POINTER(_u32p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p), ctypes.c_int]
+        L.oracle_camera_basis.argtypes = [_fp, _fp, _fp, ctypes.c_float, _sz, _sz, _fp, ctypes.c_int]
         L.oracle_camera_basis.restype = None
-        L.oracle_orbit.argtypes = [_fp, ctypes.c_float, ctypes.c_int, _fp, _fp, _fp]
+        L.oracle_orbit.argtypes = [_fp, ctypes.c_float, ctypes.c_int, _fp, _fp, _fp, ctypes.c_int]
         L.oracle_orbit.restype = None
         L.oracle_render.argtypes = [_fp, _fp, _sz, _u32p, _sz, _u64p, _fp, _fp, _fp, ctypes.c_int, _sz, _sz,
                                     _fp, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int32), _fp,
@@ -88,80 +90,82 @@ def _take(p, count, dtype):
     return a
 
 
-def load_mesh(path=None, proc=0):
-    """obj_norms.hpp:120 load_from_file (or the C5 procedural mesh): (tri48 [n,12] f32, norm36 [n,9] f32)."""
+def load_mesh(path=None, proc=0, contract=False):
+    """obj_norms.hpp:120 load_from_file (or the C5 procedural mesh): (tri48 [n,12] f32, norm36 [n,9] f32).
+    contract=True: the arithmetic of the reference's own CMake build (GCC FMA contraction)."""
     L = lib()
     t, nrm, n = _fp(), _fp(), _sz()
     if proc:
-        _check(L.oracle_proc_mesh(int(proc), ctypes.byref(t), ctypes.byref(nrm), ctypes.byref(n)))
+        _check(L.oracle_proc_mesh(int(proc), ctypes.byref(t), ctypes.byref(nrm), ctypes.byref(n), int(contract)))
     else:
-        _check(L.oracle_load_obj(path.encode(), ctypes.byref(t), ctypes.byref(nrm), ctypes.byref(n)))
+        _check(L.oracle_load_obj(path.encode(), ctypes.byref(t), ctypes.byref(nrm), ctypes.byref(n), int(contract)))
     n = n.value
     tri = _take(t, n * 12, np.float32).reshape(n, 12)
     nor = _take(nrm, n * 9, np.float32).reshape(n, 9)
     return tri, nor
 
 
-def rotate(tri, axis, degrees):
+def rotate(tri, axis, degrees, contract=False):
     ax = {"x": 0, "y": 1, "z": 2}[axis] if isinstance(axis, str) else int(axis)
-    lib().oracle_rotate(_ptr(tri, ctypes.c_float), tri.shape[0], ax, float(degrees))
+    lib().oracle_rotate(_ptr(tri, ctypes.c_float), tri.shape[0], ax, float(degrees), int(contract))
     return tri
 
 
-def build_bvh(tri):
+def build_bvh(tri, contract=False):
     """Binned SAH (binned_sah_builder.hpp:39-234): nodes [m,8] u32 (bvh.hpp Node), prim u64."""
     L = lib()
     nodes, prim, m = _u32p(), _u64p(), _sz()
     _check(L.oracle_build_bvh(_ptr(tri, ctypes.c_float), tri.shape[0], ctypes.byref(nodes), ctypes.byref(m),
-                              ctypes.byref(prim)))
+                              ctypes.byref(prim), int(contract)))
     m = m.value
     return _take(nodes, m * 8, np.uint32).reshape(m, 8), _take(prim, tri.shape[0], np.uint64)
 
 
-def camera_basis(eye, dir, up, fov, W, H):
+def camera_basis(eye, dir, up, fov, W, H, contract=False):
     out = np.zeros(9, np.float32)
     f3 = lambda v: np.asarray(v, np.float32)  # noqa: E731
     e, d, u = f3(eye), f3(dir), f3(up)
     lib().oracle_camera_basis(_ptr(e, ctypes.c_float), _ptr(d, ctypes.c_float), _ptr(u, ctypes.c_float),
-                              float(fov), W, H, _ptr(out, ctypes.c_float))
+                              float(fov), W, H, _ptr(out, ctypes.c_float), int(contract))
     return out
 
 
-def orbit(axis, step_deg, count, eye, dir, sun):
+def orbit(axis, step_deg, count, eye, dir, sun, contract=False):
     """anim.cpp:76-88: eye, dir, sun after `count` Transform rotations (oracle restatement)."""
     f3 = lambda v: np.array(v, np.float32)  # noqa: E731
     a, e, d, s = f3(axis), f3(eye), f3(dir), f3(sun)
     lib().oracle_orbit(_ptr(a, ctypes.c_float), float(np.float32(step_deg)), int(count), _ptr(e, ctypes.c_float),
-                       _ptr(d, ctypes.c_float), _ptr(s, ctypes.c_float))
+                       _ptr(d, ctypes.c_float), _ptr(s, ctypes.c_float), int(contract))
     return e, d, s
 
 
-def pose(cfg, frame=0):
+def pose(cfg, frame=0, contract=False):
     """(eye, dir, sun) of a config; configs with "orbit": (axis, step_deg, count) are rotated
     count + frame times like anim.cpp's camera/sun."""
     eye, dir, sun = cfg["eye"], cfg["dir"], cfg["sun"]
     n = (cfg["orbit"][2] if cfg.get("orbit") else 0) + frame
     if n:
         axis, step = (cfg["orbit"][0], cfg["orbit"][1]) if cfg.get("orbit") else (cfg["orbit_axis"], cfg["orbit_step"])
-        return orbit(axis, step, n, eye, dir, sun)
+        return orbit(axis, step, n, eye, dir, sun, contract)
     f3 = lambda v: np.array(v, np.float32)  # noqa: E731
     return f3(eye), f3(dir), f3(sun)
 
 
-def prepare(cfg):
-    """Scene prep of the reference app (obj load, rotate, BVH build, camera basis) for a config dict."""
+def prepare(cfg, contract=False):
+    """Scene prep of the reference app (obj load, rotate, BVH build, camera basis) for a config dict;
+    contract=True: with the reference-flag (GCC FMA contraction) arithmetic."""
     import sys
     pkg = os.path.join(os.path.dirname(HERE), "ceres-raytracer_amd")
     if pkg not in sys.path:
         sys.path.insert(0, pkg)
     import configs as _c
-    tri, nor = load_mesh(_c.obj_path(cfg), cfg.get("proc", 0))
+    tri, nor = load_mesh(_c.obj_path(cfg), cfg.get("proc", 0), contract)
     if cfg.get("rotate"):
-        rotate(tri, cfg["rotate"][0], cfg["rotate"][1])
-    nodes, prim = build_bvh(tri)
-    eye, dir, sun = pose(cfg)
-    basis = camera_basis(eye, dir, cfg["up"], cfg["fov"], cfg["W"], cfg["H"])
-    return dict(tri=tri, norm=nor, nodes=nodes, prim=prim, basis=basis, eye=eye, sun=sun)
+        rotate(tri, cfg["rotate"][0], cfg["rotate"][1], contract)
+    nodes, prim = build_bvh(tri, contract)
+    eye, dir, sun = pose(cfg, 0, contract)
+    basis = camera_basis(eye, dir, cfg["up"], cfg["fov"], cfg["W"], cfg["H"], contract)
+    return dict(tri=tri, norm=nor, nodes=nodes, prim=prim, basis=basis, eye=eye, sun=sun, contract=bool(contract))
 
 
 def render(scene, cfg, basis=None, want_pixels=True, want_ppm=True, want_records=False, threads=0, want_pairs=False,
@@ -183,7 +187,8 @@ def render(scene, cfg, basis=None, want_pixels=True, want_ppm=True, want_records
     _check(L.oracle_render(_ptr(tri, ctypes.c_float), _ptr(nor, ctypes.c_float), tri.shape[0],
                            _ptr(nodes, ctypes.c_uint32), nodes.shape[0], _ptr(prim, ctypes.c_uint64),
                            _ptr(eye, ctypes.c_float), _ptr(basis, ctypes.c_float), _ptr(sun, ctypes.c_float),
-                           (1 if cfg["mode"] == "primary" else 0) | (0x10 if cfg.get("robust") else 0), W, H,
+                           (1 if cfg["mode"] == "primary" else 0) | (0x10 if cfg.get("robust") else 0)
+                           | (0x20 if scene.get("contract") else 0), W, H,
                            _ptr(px, ctypes.c_float),
                            _ptr(ppm, ctypes.c_uint8), _ptr(rp, ctypes.c_int32), _ptr(tuv, ctypes.c_float),
                            _ptr(rs, ctypes.c_int8), _ptr(counts, ctypes.c_uint64), int(threads),

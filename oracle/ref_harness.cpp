@@ -117,6 +117,10 @@ static bool parse(int argc, char** argv, Args& a) {
 // Procedural heightfield (SURVEY.md §8(d) C5 definition), emitted as OBJ text into a
 // stream so it goes through the reference loader (obj_norms.hpp:57-118) unchanged.
 // Vertex coordinates are printed with %.9g so they round-trip exactly through strtof.
+// The mesh is an INPUT, defined by SURVEY.md's formula, not by the reference's flags: z is
+// computed without FMA contraction in both builds (the reference-flag build would otherwise
+// fuse 400x + 300y and the final sum, giving _ref/ref_render a different mesh).
+__attribute__((optimize("fp-contract=off")))
 static std::string proc_obj(int n) {
     std::string s;
     s.reserve(size_t(n) * n * 40 + size_t(n) * n * 2 * 30);

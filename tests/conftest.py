@@ -51,6 +51,19 @@ def load_golden(name):
     return meta, rec, ppm
 
 
+def load_ref_records(name):
+    """<name>.ref.records.npz: the per-pixel records of the reference-flag build (make_golden.py)."""
+    return dict(np.load(os.path.join(GOLDEN, name + ".ref.records.npz")))
+
+
+def ref_scene_hashes(meta, contract):
+    """(tri48, norm36, canonical BVH) sha256 of the fixture's exact or reference-flag build."""
+    if contract:
+        r = meta["ref_scene"]
+        return r["tri48_sha256"], r["norm36_sha256"], r["bvh_canonical_sha256"]
+    return meta["tri48_sha256"], meta["norm36_sha256"], meta["bvh_canonical_sha256"]
+
+
 def load_orbit(name):
     """tests/golden/orbit/<name>.json (make_golden.py --orbit): the reference's PPM sha256 and
     rays / hits of every bench orbit view, keyed by the float32 step's hex bits."""

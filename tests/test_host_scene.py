@@ -2,7 +2,8 @@
 
 The OBJ loader, rotate_triangles, camera basis and binned-SAH builder of the product must
 produce exactly the bits the reference produces (they feed the GPU kernels): checked here on
-CPU without touching a GPU.
+CPU without touching a GPU -- in both arithmetics: ARITH_EXACT against the contraction-free
+reference build, ARITH_FMA against the reference's own CMake build (the "ref*" fixture keys).
 """
 import hashlib
 import os
@@ -10,49 +11,53 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_names, hexbits, load_golden
+from conftest import GOLDEN, golden_names, hexbits, load_golden, ref_scene_hashes
 
 import configs
 
 NAMES = [n for n in golden_names() if n != "proc_c5"]
 
 
+@pytest.mark.parametrize("arith", [0, 1], ids=["exact", "fma"])
 @pytest.mark.parametrize("name", NAMES)
-def test_product_scene_prep_matches_reference(pkg, name):
+def test_product_scene_prep_matches_reference(pkg, name, arith):
     meta, _, _ = load_golden(name)
     cfg = configs.CONFIGS[name]
-    mesh, bvh, cam = pkg.prepare(cfg)
+    mesh, bvh, cam = pkg.prepare(cfg, arith=arith)
+    tri, nor, canon = ref_scene_hashes(meta, arith)
     assert len(mesh) == meta["n_tri"]
-    assert hashlib.sha256(mesh.tri.tobytes()).hexdigest() == meta["tri48_sha256"]
-    assert hashlib.sha256(mesh.norm.tobytes()).hexdigest() == meta["norm36_sha256"]
+    assert hashlib.sha256(mesh.tri.tobytes()).hexdigest() == tri
+    assert hashlib.sha256(mesh.norm.tobytes()).hexdigest() == nor
     import make_golden
-    assert make_golden.canonical_bvh_sha(bvh.nodes.tobytes(), bvh.prim.tobytes()) == meta["bvh_canonical_sha256"]
-    assert bvh.nodes.shape[0] == meta["n_nodes"]
+    assert make_golden.canonical_bvh_sha(bvh.nodes.tobytes(), bvh.prim.tobytes()) == canon
+    assert bvh.nodes.shape[0] == meta["ref_n_nodes" if arith else "n_nodes"]
     b = cam.basis(cfg["W"], cfg["H"])
-    eye = meta["pose"]["eye"] if "pose" in meta else hexbits(np.asarray(cfg["eye"], np.float32))
-    assert hexbits(b[:3]) == eye
-    assert hexbits(b[3:]) == meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]
-    if "pose" in meta:
-        assert hexbits(pkg.pose(cfg)[1]) == meta["pose"]["sun"]
+    pose, basis = (meta["ref_pose"], meta["ref_basis"]) if arith else (meta["pose"], meta["basis"])
+    assert hexbits(b[:3]) == pose["eye"]
+    assert hexbits(b[3:]) == basis["dir"] + basis["u"] + basis["v"]
+    assert hexbits(pkg.pose(cfg, arith=arith)[1]) == pose["sun"]
 
 
+@pytest.mark.parametrize("arith", [0, 1], ids=["exact", "fma"])
 @pytest.mark.parametrize("name", ["dragon_orbit3_333x217", "bunny_orbit7_160x120"])
-def test_orbit_frames_match_reference_transform(pkg, oracle_mod, name):
+def test_orbit_frames_match_reference_transform(pkg, oracle_mod, name, arith):
     """anim.cpp orbit (transform.hpp): the product's multi-frame orbit equals the reference pose
     pinned by the fixture at frame `count`, and the oracle's restatement at every frame."""
     meta, _, _ = load_golden(name)
     cfg = configs.CONFIGS[name]
     (axis, step, count) = cfg["orbit"]
-    cam0 = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
+    cam0 = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"], arith=arith)
     n = count + 4
     b, s3 = pkg.orbit_cameras(cam0, cfg["sun"], cfg["W"], cfg["H"], n, axis=axis, step_deg=step, rotate_first=False)
-    assert hexbits(b[count, :3]) == meta["pose"]["eye"]
-    assert hexbits(b[count, 3:]) == meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]
-    assert hexbits(s3[count]) == meta["pose"]["sun"]
+    pose, basis = (meta["ref_pose"], meta["ref_basis"]) if arith else (meta["pose"], meta["basis"])
+    assert hexbits(b[count, :3]) == pose["eye"]
+    assert hexbits(b[count, 3:]) == basis["dir"] + basis["u"] + basis["v"]
+    assert hexbits(s3[count]) == pose["sun"]
     for k in range(n):
-        e, d, s = oracle_mod.orbit(axis, step, k, cfg["eye"], cfg["dir"], cfg["sun"])
+        e, d, s = oracle_mod.orbit(axis, step, k, cfg["eye"], cfg["dir"], cfg["sun"], contract=arith)
         assert hexbits(b[k, :3]) == hexbits(e) and hexbits(s3[k]) == hexbits(s)
-        assert hexbits(b[k, 3:]) == hexbits(oracle_mod.camera_basis(e, d, cfg["up"], cfg["fov"], cfg["W"], cfg["H"]))
+        assert hexbits(b[k, 3:]) == hexbits(oracle_mod.camera_basis(e, d, cfg["up"], cfg["fov"], cfg["W"], cfg["H"],
+                                                                    contract=arith))
     # rotate_first (anim.cpp's own order) is the same sequence shifted by one frame
     b1, s1 = pkg.orbit_cameras(cam0, cfg["sun"], cfg["W"], cfg["H"], n - 1, axis=axis, step_deg=step)
     np.testing.assert_array_equal(b1.view(np.uint32), b[1:].view(np.uint32))
@@ -72,15 +77,17 @@ def test_product_matches_oracle_on_c5_mesh(pkg, oracle_mod):
         make_golden.canonical_bvh_sha(nodes.tobytes(), prim.tobytes())
 
 
-def test_product_c5_scene_matches_reference(pkg, oracle_mod):
+@pytest.mark.parametrize("arith", [0, 1], ids=["exact", "fma"])
+def test_product_c5_scene_matches_reference(pkg, oracle_mod, arith):
     """Full C5 (9,999,392 triangles): rotated triangles, normals and the binned-SAH BVH of the
     product's host path equal the reference's dump (tests/golden/proc_c5.json scene hashes)."""
     meta, _, _ = load_golden("proc_c5")
-    mesh, bvh, _ = pkg.prepare(configs.CONFIGS["proc_c5"])
-    assert len(mesh) == meta["n_tri"] and bvh.nodes.shape[0] == meta["n_nodes"]
-    assert hashlib.sha256(mesh.tri.tobytes()).hexdigest() == meta["tri48_sha256"]
-    assert hashlib.sha256(mesh.norm.tobytes()).hexdigest() == meta["norm36_sha256"]
-    assert oracle_mod.canonical_bvh_sha(bvh.nodes, bvh.prim) == meta["bvh_canonical_sha256"]
+    mesh, bvh, _ = pkg.prepare(configs.CONFIGS["proc_c5"], arith=arith)
+    tri, nor, canon = ref_scene_hashes(meta, arith)
+    assert len(mesh) == meta["n_tri"] and bvh.nodes.shape[0] == meta["ref_n_nodes" if arith else "n_nodes"]
+    assert hashlib.sha256(mesh.tri.tobytes()).hexdigest() == tri
+    assert hashlib.sha256(mesh.norm.tobytes()).hexdigest() == nor
+    assert oracle_mod.canonical_bvh_sha(bvh.nodes, bvh.prim) == canon
 
 
 def test_oracle_canonical_hash_equals_python_definition(pkg, oracle_mod):
