@@ -25,16 +25,28 @@ Scene upload, OBJ load and BVH build are outside the timed region, as in the ref
 (static.cpp:129-133).  value = (primary + shadow rays of all F frames) x steps / wall time
 (max over ranks).  One process per GPU (torch.distributed, backend nccl = RCCL).
 
+Arithmetic (--arith): "fma" (default) = the reference as its own CMake build compiles it
+(CMakeLists.txt:11-13, g++ -O3 -mavx2 -mfma: GCC contracts a*b+c into FMA; the scene, camera,
+orbit and kernels use CERES_ARITH_FMA / CERES_MODE_FMA) -- the same build the CPU baseline times
+(oracle/_ref/ref_render) -- so every frame is checked against THAT build's PPM; "exact" = the
+contraction-free reference (-ffp-contract=off), checked against its PPMs.
+
 Also reported (rank 0):
-  roofline      dominant kernel's algorithmic bytes per launch (pinned reference statistics,
-                SURVEY.md §8(d): 64 B per node-pair visit + 56 B per triangle test) / its mean
-                device duration from HIP events around back-to-back launches on their stream, for
-                one full frame on one GPU.  `bound` is chosen from the measured counters
-                (profiles/pmc_summary.json, rocprofv3 --pmc of the same solo launch): "hbm" when the
-                DRAM bytes are at least half the algorithmic bytes, else "l2" (the bytes are
-                served on-die; priced against the ~34.5 TB/s aggregate L2); `limiter` names what
-                the counters say stalls the kernel; `hbm_frac_algorithmic` keeps SURVEY §8(d)'s
-                algorithmic-bytes-vs-8-TB/s figure as a secondary field.
+  roofline      the dominant kernel AS THE STEP RUNS IT: one ceres_render_batch_device launch of 16
+                of the step's orbit views (whole frames), launched back to back on ONE stream
+                between two HIP events (mean launch duration = per-kernel evidence, comparable
+                with a single-stream rocprofv3 trace).  achieved = the launch's ALGORITHMIC bytes
+                (pinned reference statistics per view, tests/golden/orbit/<cfg>.json, SURVEY.md
+                §8(d): 64 B per node-pair visit + 56 B per triangle test) / that duration.  `bound`
+                is chosen from the measured counters (profiles/pmc_summary.json, rocprofv3 --pmc of
+                the same launch): "hbm" when the DRAM bytes are at least half the algorithmic
+                bytes, else "l2" (served on-die; priced against the ~34.5 TB/s aggregate L2);
+                `limiter` names what the counters say stalls the kernel; `hbm_frac_algorithmic`
+                keeps SURVEY §8(d)'s algorithmic-bytes-vs-8-TB/s figure.
+  roofline_step the timed regime itself: algorithmic bytes of every frame of a step (all ranks)
+                / ms_per_step, per GPU, priced against the L2 and against HBM (steps overlap on
+                --streams streams, so this is a throughput, not a launch duration).
+  roofline_solo one whole frame of frame 0's view per launch (the latency regime), as `roofline`.
   c3_only       the same timed loop with all F frames = the C3 view itself (the orbit mix is
                 lighter: fewer shadow rays per frame), value + shadow-ray fractions of both.
   cpu_baseline  the REFERENCE hot path (oracle/_ref/ref_render, reference CMake flags) timed
@@ -79,19 +91,35 @@ def load_golden(name):
     return None
 
 
-def pinned_basis(meta, cfg, cam):
-    """C3 camera basis from the fixture's hex bits (never trust a host libm for parity)."""
+def pinned_basis(meta, cfg, cam, build="exact"):
+    """C3 camera basis from the fixture's hex bits (never trust a host libm for parity); build =
+    "ref" (the reference CMake build's basis, FMA arithmetic) or "exact"."""
     if meta is None:
         return cam.basis(cfg["W"], cfg["H"])
-    bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
+    b = meta["ref_basis"] if build == "ref" else meta["basis"]
+    bits = [int(h, 16) for h in b["dir"] + b["u"] + b["v"]]
     return np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
 
 
-def step_views(pkg, cfg, meta, cam, F, V=None):
+def view_entry(e, build):
+    """A view of an orbit fixture in one build: the contraction-free entry or its "ref" part."""
+    if e is None:
+        return None
+    return e.get("ref") if build == "ref" else e
+
+
+def algorithmic_bytes(stats):
+    """64 B per node-pair visit + 56 B per triangle test (48-B Triangle + 8-B
+    primitive index), from the reference's own Statistics (single_ray_traverser.hpp:132-135)."""
+    return 64 * (stats["primary_pairs"] + stats.get("shadow_pairs", 0)) + \
+        56 * (stats["primary_tests"] + stats.get("shadow_tests", 0))
+
+
+def step_views(pkg, cfg, meta, cam, F, V=None, build="exact"):
     """Cameras (basis12 [F,12], sun3 [F,3]) of one bench step of F frames (pkg.bench_views: frame f
     rotated once by f x 360 / F degrees about z, frame 0 = C3 with the fixture's basis bits).
     `V` is accepted for older tools and ignored."""
-    b12, s3, _ = pkg.bench_views(cam, cfg["sun"], cfg["W"], cfg["H"], F, basis0=pinned_basis(meta, cfg, cam))
+    b12, s3, _ = pkg.bench_views(cam, cfg["sun"], cfg["W"], cfg["H"], F, basis0=pinned_basis(meta, cfg, cam, build))
     return b12, s3
 
 
@@ -109,12 +137,13 @@ def step_key(step):
     return "%08x" % int(np.asarray(step, np.float32).view(np.uint32))
 
 
-def cpu_baseline(cfg_name, cfg, rays_per_frame, budget_s=3.0):
+def cpu_baseline(cfg_name, cfg, rays_per_frame, budget_s=3.0, build="ref"):
     """Reference CPU path on this host, bounded sample of the same workload (rank 0, N = 1)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import configs
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
-    ref = os.path.join(REPO, "oracle", "_ref", "ref_render")
+    # the reference binary of the same arithmetic as the GPU run (the CMake-flag build by default)
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_render" if build == "ref" else "ref_render_exact")
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     if os.access(ref, os.X_OK):
         try:
@@ -128,12 +157,13 @@ def cpu_baseline(cfg_name, cfg, rays_per_frame, budget_s=3.0):
             return {"value": round(out["rays"] / (ms * 1e3), 3), "unit": "Mrays/s", "cores": threads,
                     "kind": "reference",
                     "sample": f"{cfg_name}: {reps} full frames of reference render() (render.hpp:87, "
-                              f"-O3 -mavx2 -mfma -fopenmp), median {ms:.2f} ms/frame, {out['rays']} rays/frame",
+                              f"-O3 -mavx2 -mfma -fopenmp{'' if build == 'ref' else ' -ffp-contract=off'}), "
+                              f"median {ms:.2f} ms/frame, {out['rays']} rays/frame",
                     "cpu_model": _cpu_model()}
         except Exception as e:  # noqa: BLE001 -- fall through to the port
             sys.stderr.write(f"reference CPU baseline failed ({e}); timing the oracle port\n")
     import oracle
-    sc = oracle.prepare(cfg)
+    sc = oracle.prepare(cfg, contract=build == "ref")
     oracle.render(sc, cfg, want_pixels=True, want_ppm=False, threads=threads)
     times = []
     t_end = time.time() + budget_s
@@ -225,6 +255,20 @@ def roofline_block(name, nbytes, ms, pmc, scene_bytes):
     return out
 
 
+def roofline_step_block(nbytes, ms_step, world):
+    """The timed regime priced at the roofline: the algorithmic bytes of every frame of a step (all
+    ranks) / ms_per_step, per GPU, against the aggregate L2 (~34.5 TB/s) and against HBM (8 TB/s).
+    Steps overlap on several streams, so this is a sustained throughput, not a launch duration."""
+    if not nbytes or ms_step <= 0:
+        return None
+    job = nbytes / (ms_step * 1e-3) / 1e9
+    per_gpu = job / world
+    return {"algorithmic_bytes_per_step": int(nbytes), "ms_per_step": round(ms_step, 5), "unit": "GB/s",
+            "achieved_job": round(job, 1), "achieved_per_gpu": round(per_gpu, 1),
+            "frac_l2": round(per_gpu / L2_PEAK_GBS, 4), "frac_hbm": round(per_gpu / HBM_PEAK_GBS, 4),
+            "source": "per-view reference Statistics, tests/golden/orbit/<config>.json (64 B/node pair + 56 B/test)"}
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -249,6 +293,8 @@ def main():
     ap.add_argument("--streams", type=int, default=8,
                     help="HIP streams the steps rotate over (step k on stream k %% S, its own buffers): step k+1 "
                          "fills the tail of step k")
+    ap.add_argument("--arith", choices=("fma", "exact"), default="fma",
+                    help="fma: the reference's CMake build (GCC FMA contraction); exact: -ffp-contract=off")
     args = ap.parse_args()
 
     import torch
@@ -281,17 +327,20 @@ def main():
 
     W, H = cfg["W"], cfg["H"]
     F = args.frames or args.frames_per_gpu * world
-    mesh, bvh, cam = pkg.prepare(cfg)
+    build = "ref" if args.arith == "fma" else "exact"          # the fixtures' key for this arithmetic
+    arith = pkg.ARITH_FMA if build == "ref" else pkg.ARITH_EXACT
+    mesh, bvh, cam = pkg.prepare(cfg, arith=arith)
     scene = pkg.Scene(mesh, bvh, device=local_rank)
     # F views of the orbit, frame f rotated once by f x 360 / F degrees (frame 0 = C3, fixture bits)
-    b12, s3, steps_deg = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=pinned_basis(meta, cfg, cam))
+    b12, s3, steps_deg = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=pinned_basis(meta, cfg, cam, build))
     exchange = world > 1 and args.collect == "exchange" and F % world == 0
     if exchange:
         # batch order for the all-to-all: rank q owns batch frames q*k .. q*k+k-1, which are orbit
         # frames q, q + N, q + 2N, ... (batch frame 0 = orbit frame 0 = C3)
         order = D.exchange_order(F, world)
         b12, s3, steps_deg = b12[order], s3[order], steps_deg[order]
-    mode = pkg.cfg_mode(cfg)
+    mode = pkg.cfg_mode(cfg, arith)
+    full_mode = (mode & 0xf) == pkg.MODE_FULL
     row_block = args.row_block if world > 1 else H
     tiling = pkg.Tiling(row_block, rank, world)
     S = max(1, args.streams)
@@ -380,7 +429,7 @@ def main():
         head = b"P6 %d %d 255\n" % (W, H)
         n = [0, 0, 0]                                            # [checked, matched, unpinned]
         for f, body in mine:
-            e = None if orbit_fx is None else orbit_fx.get(step_key(views["steps"][f]))
+            e = None if orbit_fx is None else view_entry(orbit_fx.get(step_key(views["steps"][f])), build)
             if e is None:
                 n[2] += 1
                 continue
@@ -390,7 +439,7 @@ def main():
         if world > 1:
             dist.all_reduce(stat)
         stat = stat.cpu().numpy()
-        keys = [None if orbit_fx is None else orbit_fx.get(step_key(x)) for x in views["steps"]]
+        keys = [None if orbit_fx is None else view_entry(orbit_fx.get(step_key(x)), build) for x in views["steps"]]
         ref_rays = sum(e["rays"] for e in keys) if all(keys) else None
         ref_hits = sum(e["hits"] for e in keys) if all(keys) else None
         checks = {"frames": F, "frames_checked": int(stat[0]), "frames_unpinned": int(stat[2]),
@@ -442,6 +491,16 @@ def main():
             dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         return float(elapsed.item())
 
+    def step_bytes(steps):
+        """Algorithmic bytes of one step's frames (whole job), from every view's pinned reference
+        statistics, or None when a view is unpinned."""
+        if orbit_fx is None:
+            return None
+        es = [view_entry(orbit_fx.get(step_key(x)), build) for x in steps]
+        if not all(e is not None and "stats" in e for e in es):
+            return None
+        return int(sum(algorithmic_bytes(e["stats"]) for e in es))
+
     # validation step of the orbit views (not timed): exact counts + every frame vs the reference
     rays_step, hits_step, orbit_checks = validate()
     parity = None
@@ -455,13 +514,16 @@ def main():
         torch.cuda.synchronize(dev)
         c0 = c0.cpu().numpy()
         body = b"P6 %d %d 255\n" % (W, H) + rgb0.view(H, 3 * W).cpu().numpy().tobytes()
-        parity.update(frame0_ppm_sha256_matches_reference=hashlib.sha256(body).hexdigest() == meta["ppm_sha256"]["exact"],
-                      rays_match=int(c0[0]) == meta["exact"]["rays"], hits_match=int(c0[1]) == meta["exact"]["hits"])
+        parity.update(reference_build="reference CMake flags (-O3 -mavx2 -mfma, GCC FMA contraction)" if build == "ref"
+                      else "reference with -ffp-contract=off",
+                      frame0_ppm_sha256_matches_reference=hashlib.sha256(body).hexdigest() == meta["ppm_sha256"][build],
+                      rays_match=int(c0[0]) == meta[build]["rays"], hits_match=int(c0[1]) == meta[build]["hits"])
     if parity is not None:
         parity.update(orbit_checks)
 
     T = timed(prime=True)
     value = rays_step * args.steps / T / 1e6
+    bytes_step = step_bytes(views["steps"])
     primary_step = F * W * H
     view0 = None
     if not args.no_view0_only:
@@ -471,14 +533,49 @@ def main():
                      steps=np.repeat(steps_deg[:1], F))
         rays0, hits0, checks0 = validate()
         T0 = timed(prime=False)
+        b0 = step_bytes(views["steps"])
         view0 = {"value": round(rays0 * args.steps / T0 / 1e6, 3), "unit": "Mrays/s",
+                 "roofline_step": roofline_step_block(b0, T0 / args.steps * 1e3, world),
                  "ms_per_step": round(T0 / args.steps * 1e3, 5), "rays_per_step": rays0, "hits_per_step": hits0,
-                 "shadow_ray_frac": round((rays0 - primary_step) / rays0, 4) if mode == pkg.MODE_FULL else 0.0,
+                 "shadow_ray_frac": round((rays0 - primary_step) / rays0, 4) if full_mode else 0.0,
                  "parity": checks0}
 
-    roofline = None
+    roofline = roofline_solo = None
     cpu = None
     if rank == 0 and not args.no_roofline and meta is not None:
+        # the step's kernel: one 16-frame launch of the step's first 16 orbit views (whole frames),
+        # n_b launches back to back on ONE stream between two HIP events -- no other stream's work
+        # overlaps, so the mean is a per-launch duration (and agrees with a single-stream trace)
+        nb_f = min(16, F)
+        vb12, vs3, vsteps = b12[np.argsort(steps_deg)][:nb_f], s3[np.argsort(steps_deg)][:nb_f], \
+            np.sort(steps_deg)[:nb_f]
+        bat_rgb = torch.empty(nb_f * 3 * W * H, dtype=torch.uint8, device=dev)
+        bat_px = None if args.no_float else torch.empty(nb_f * 3 * W * H, dtype=torch.float32, device=dev)
+        whole = pkg.Tiling(H, 0, 1)
+
+        def batch_launch():
+            scene.render_batch_device(vb12, vs3, W, H, mode=mode, tiling=whole,
+                                      d_pixels=0 if bat_px is None else bat_px.data_ptr(), d_rgb8=bat_rgb.data_ptr(),
+                                      stream=sh)
+        for _ in range(3):
+            batch_launch()
+        n_b = max(10, min(args.steps, 100))
+        evb0, evb1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        evb0.record(stream)
+        for _ in range(n_b):
+            batch_launch()
+        evb1.record(stream)
+        torch.cuda.synchronize(dev)
+        batch_ms = evb0.elapsed_time(evb1) / n_b
+        bb = step_bytes(vsteps)
+        kname = "ceres_fused" if full_mode else "ceres_primary"
+        if bb is not None:
+            roofline = roofline_block(kname, bb, batch_ms,
+                                      pmc_entry(args.config, f"{kname}_batch{nb_f}_{args.arith}"),
+                                      scene.info()["device_bytes"])
+            roofline.update(launch=f"ceres_render_batch_device, {nb_f} orbit views (steps {vsteps[0]:g}..{vsteps[-1]:g} "
+                                   f"deg), whole {W}x{H} frames, {n_b} launches back to back on one stream",
+                            frames_per_launch=nb_f)
         # dominant kernel, timed live with HIP events on the launch stream (one full frame, this GPU)
         solo = pkg.Tiling(H, 0, 1)
         solo_rgb = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
@@ -497,14 +594,18 @@ def main():
         ev1.record(stream)
         torch.cuda.synchronize(dev)
         mean_ms = ev0.elapsed_time(ev1) / n_t
-        ex = meta["exact"]
+        ex = meta[build]
         b_p = 64 * ex["primary_pairs"] + 56 * ex["primary_tests"]
         b_s = 64 * ex["shadow_pairs"] + 56 * ex["shadow_tests"]
         # one kernel per frame: ceres_fused (primary + shadow + shading) or ceres_primary (primary only)
-        name, nbytes = ("ceres_fused", b_p + b_s) if mode == pkg.MODE_FULL else ("ceres_primary", b_p)
-        roofline = roofline_block(name, nbytes, mean_ms, pmc_entry(args.config, name), scene.info()["device_bytes"])
+        name, nbytes = ("ceres_fused", b_p + b_s) if full_mode else ("ceres_primary", b_p)
+        pmc = pmc_entry(args.config, f"{name}_solo_{args.arith}") or \
+            (pmc_entry(args.config, name) if args.arith == "exact" else None)
+        roofline_solo = roofline_block(name, nbytes, mean_ms, pmc, scene.info()["device_bytes"])
+        if roofline is None:
+            roofline = roofline_solo
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.config, cfg, rays_step if F == 1 else meta["exact"]["rays"])
+        cpu = cpu_baseline(args.config, cfg, rays_step if F == 1 else meta[build]["rays"], build=build)
 
     if rank == 0:
         line = {
@@ -512,17 +613,17 @@ def main():
             if args.config == "dragon_1080" else f"Mrays/sec ({args.config})",
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(T / args.steps * 1e3, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "arith": args.arith,
             "data": ("real mesh from the reference repo (data/%s)" % cfg["obj"] if cfg["obj"] else
                      "procedural %dx%d-vertex heightfield generated in-process (SURVEY.md §8(d) C5 definition)"
                      % (cfg["proc"], cfg["proc"]))
                     + "; frame 0 = the config camera, frames 1.. = the anim.cpp-style orbit about z",
             "config": {"workload": f"{args.config}: {cfg['obj'] or 'proc'} {W}x{H} "
-                                   f"{'primary+shadow' if mode == pkg.MODE_FULL else 'primary only'}, "
+                                   f"{'primary+shadow' if full_mode else 'primary only'}, "
                                    f"{F} orbit frame(s) per step",
                        "W": W, "H": H, "frames_per_step": F, "rays_per_step": rays_step, "hits_per_step": hits_step,
                        "shadow_ray_frac": round((rays_step - primary_step) / rays_step, 4)
-                       if mode == pkg.MODE_FULL else 0.0,
+                       if full_mode else 0.0,
                        "row_block": row_block, "parallelism": f"row-interleaved frames x{world}"
                        + ((" + one RCCL all-to-all per step: frame f gathered to rank f (pipelined)" if exchange
                            else " + one RCCL gather per step to rank 0 (pipelined)") if world > 1 else ""),
@@ -535,7 +636,8 @@ def main():
                 "recv_bytes_per_rank_step": (world - 1) * (F // world if exchange else F) * H * 3 * W // world,
                 "xgmi_link_ms_est": round((F // world if exchange else F) * H * 3 * W / world / 76.8e6, 4),
                 "ms_per_step": round(T / args.steps * 1e3, 5)},
-            "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
+            "roofline": roofline, "roofline_step": roofline_step_block(bytes_step, T / args.steps * 1e3, world),
+            "roofline_solo": roofline_solo, "cpu_baseline": cpu, "parity": parity,
         }
         if view0 is not None:
             line["c3_only_value" if args.config == "dragon_1080" else "view0_only_value"] = view0["value"]

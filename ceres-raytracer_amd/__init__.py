@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = (
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
     "ceres_obj_load_arith", "ceres_proc_mesh_arith", "ceres_rotate_triangles_arith", "ceres_bvh_build_arith",
-    "ceres_camera_basis_arith", "ceres_orbit_cameras_arith",
+    "ceres_camera_basis_arith", "ceres_orbit_cameras_arith", "ceres_content_hash",
 )
 
 
@@ -165,6 +165,8 @@ def lib():
     L.ceres_scene_read_timing.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           _u64p]
     L.ceres_scene_wave_log.argtypes = [_vp, _u64p, _sz, ctypes.POINTER(_sz)]
+    L.ceres_content_hash.argtypes = [_vp, _sz]
+    L.ceres_content_hash.restype = ctypes.c_uint64
     L.ceres_obj_load_arith.argtypes = L.ceres_obj_load.argtypes + [ctypes.c_int]
     L.ceres_proc_mesh_arith.argtypes = L.ceres_proc_mesh.argtypes + [ctypes.c_int]
     L.ceres_rotate_triangles_arith.argtypes = L.ceres_rotate_triangles.argtypes + [ctypes.c_int]

@@ -9,7 +9,13 @@
 //                [--rotate x|y|z deg] [--size W H] [-o|--out file.ppm] [--primary-only]
 //                [--proc N] [--device D] [--bench reps] [--json]
 //                [--orbit ax ay az step_deg count] [--frames N] [--gpu-bvh] [--double|-d]
-//                [--gpus N] [--row-block R] [--robust] [--qbvh]
+//                [--gpus N] [--row-block R] [--robust] [--qbvh] [--exact | --fma]
+//
+// Arithmetic (float pipeline): --fma (the default) computes every step as the reference's own
+// CMake build does (CMakeLists.txt:11-13, g++ -O3 -mavx2 -mfma: GCC contracts a*b+c into FMA at
+// the sites listed in oracle/contraction_sites.txt) -- the scene (normals, rotation, SAH costs),
+// the camera basis, the orbit and the kernels (CERES_ARITH_FMA + CERES_MODE_FMA), so the PPM is
+// the one that build writes.  --exact is the contraction-free reference (-ffp-contract=off).
 //
 // --robust traverses with the library's RobustNodeIntersector (node_intersectors.hpp:54-79,
 // T. Ize's padded-inverse slab test) instead of render()'s FastNodeIntersector.
@@ -59,6 +65,7 @@ struct Opts {
     size_t W = 1920, H = 1080;
     int mode = CERES_MODE_FULL, proc = 0, device = 0, bench = 0, gpus = 1, row_block = 8;
     bool json = false, gpu_bvh = false, f64 = false;
+    int arith = CERES_ARITH_FMA;                   // --fma (default) / --exact
     int orbit_count = 0, frames = 1;
 };
 
@@ -67,7 +74,7 @@ int usage() {
                  "usage: render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]\n"
                  "              [--rotate x|y|z deg] [--size W H] [-o out.ppm] [--primary-only] [--proc N]\n"
                  "              [--device D] [--bench reps] [--json] [--orbit ax ay az step_deg count] [--frames N]\n"
-                 "              [--gpu-bvh] [--double] [--gpus N] [--row-block R] [--robust] [--qbvh]\n");
+                 "              [--gpu-bvh] [--double] [--gpus N] [--row-block R] [--robust] [--qbvh] [--exact|--fma]\n");
     return 2;
 }
 
@@ -107,6 +114,8 @@ bool parse(int argc, char** argv, Opts& o) {
         else if (a == "--primary-only") o.mode = (o.mode & CERES_MODE_ROBUST) | CERES_MODE_PRIMARY;
         else if (a == "--robust") o.mode |= CERES_MODE_ROBUST;             // RobustNodeIntersector traversal
         else if (a == "--qbvh") o.mode |= CERES_MODE_QBVH4;                // compressed shadow BVH4 (not exact)
+        else if (a == "--exact") o.arith = CERES_ARITH_EXACT;              // the -ffp-contract=off reference
+        else if (a == "--fma") o.arith = CERES_ARITH_FMA;                  // the reference's CMake build
         else if (a == "--proc") { if (!have(1)) return false; o.proc = std::atoi(argv[++i]); }
         else if (a == "--device") { if (!have(1)) return false; o.device = std::atoi(argv[++i]); }
         else if (a == "--gpus") { if (!have(1)) return false; o.gpus = std::atoi(argv[++i]); if (o.gpus < 1) return false; }
@@ -132,17 +141,22 @@ bool parse(int argc, char** argv, Opts& o) {
 template <class S> struct Api;
 template <> struct Api<float> {
     using Node = uint32_t;
-    static int load(const char* p, float** t, float** n, size_t* c) { return ceres_obj_load(p, t, n, c); }
-    static int proc(int k, float** t, float** n, size_t* c) { return ceres_proc_mesh(k, t, n, c); }
-    static int rotate(float* t, size_t c, int ax, float deg) { return ceres_rotate_triangles(t, c, ax, deg); }
-    static int bvh(const float* t, size_t c, Node** nodes, size_t* m, uint64_t** prim, bool gpu, int dev) {
-        return gpu ? ceres_bvh_build_gpu(t, c, nodes, m, prim, dev) : ceres_bvh_build(t, c, nodes, m, prim);
+    static int load(const char* p, float** t, float** n, size_t* c, int ar) { return ceres_obj_load_arith(p, t, n, c, ar); }
+    static int proc(int k, float** t, float** n, size_t* c, int ar) { return ceres_proc_mesh_arith(k, t, n, c, ar); }
+    static int rotate(float* t, size_t c, int ax, float deg, int ar) { return ceres_rotate_triangles_arith(t, c, ax, deg, ar); }
+    static int bvh(const float* t, size_t c, Node** nodes, size_t* m, uint64_t** prim, bool gpu, int dev, int ar) {
+        if (gpu && ar != CERES_ARITH_EXACT) {
+            std::fprintf(stderr, "error: --gpu-bvh builds the contraction-free BVH only: add --exact\n");
+            return CERES_EUNSUPPORTED;
+        }
+        return gpu ? ceres_bvh_build_gpu(t, c, nodes, m, prim, dev) : ceres_bvh_build_arith(t, c, nodes, m, prim, ar);
     }
     static ceres_scene* scene(const float* t, size_t c, const float* n, const Node* nodes, size_t m, const uint64_t* prim, int dev) {
         return ceres_scene_create(t, c, n, nodes, m, prim, dev, 0);
     }
-    static int orbit(const Num<float>& v, size_t W, size_t H, uint32_t k, float* b, float* s) {
-        return ceres_orbit_cameras(v.eye, v.dir, v.up, v.sun, v.fov, W, H, v.orbit_axis, v.orbit_step, k, 0, b, s, nullptr);
+    static int orbit(const Num<float>& v, size_t W, size_t H, uint32_t k, float* b, float* s, int ar) {
+        return ceres_orbit_cameras_arith(v.eye, v.dir, v.up, v.sun, v.fov, W, H, v.orbit_axis, v.orbit_step, k, 0, b, s,
+                                         nullptr, ar);
     }
     static int render(ceres_scene* sc, const float* b, const float* s, int mode, uint8_t* rgb, size_t W, size_t H, ceres_stats* st) {
         return ceres_render_f32(sc, b, s, mode, nullptr, rgb, W, H, st);
@@ -154,17 +168,18 @@ template <> struct Api<float> {
 };
 template <> struct Api<double> {
     using Node = uint64_t;
-    static int load(const char* p, double** t, double** n, size_t* c) { return ceres_obj_load_f64(p, t, n, c); }
-    static int proc(int k, double** t, double** n, size_t* c) { return ceres_proc_mesh_f64(k, t, n, c); }
-    static int rotate(double* t, size_t c, int ax, double deg) { return ceres_rotate_triangles_f64(t, c, ax, deg); }
-    static int bvh(const double* t, size_t c, Node** nodes, size_t* m, uint64_t** prim, bool gpu, int) {
+    // render<double>: the contraction-free double build (its FMA sites are not modelled)
+    static int load(const char* p, double** t, double** n, size_t* c, int) { return ceres_obj_load_f64(p, t, n, c); }
+    static int proc(int k, double** t, double** n, size_t* c, int) { return ceres_proc_mesh_f64(k, t, n, c); }
+    static int rotate(double* t, size_t c, int ax, double deg, int) { return ceres_rotate_triangles_f64(t, c, ax, deg); }
+    static int bvh(const double* t, size_t c, Node** nodes, size_t* m, uint64_t** prim, bool gpu, int, int) {
         if (gpu) { std::fprintf(stderr, "error: --gpu-bvh builds single-precision BVHs only\n"); return CERES_EUNSUPPORTED; }
         return ceres_bvh_build_f64(t, c, nodes, m, prim);
     }
     static ceres_scene* scene(const double* t, size_t c, const double* n, const Node* nodes, size_t m, const uint64_t* prim, int dev) {
         return ceres_scene_create_f64(t, c, n, nodes, m, prim, dev, 0);
     }
-    static int orbit(const Num<double>& v, size_t W, size_t H, uint32_t k, double* b, double* s) {
+    static int orbit(const Num<double>& v, size_t W, size_t H, uint32_t k, double* b, double* s, int) {
         return ceres_orbit_cameras_f64(v.eye, v.dir, v.up, v.sun, v.fov, W, H, v.orbit_axis, v.orbit_step, k, 0, b, s, nullptr);
     }
     static int render(ceres_scene* sc, const double* b, const double* s, int mode, uint8_t* rgb, size_t W, size_t H, ceres_stats* st) {
@@ -183,15 +198,15 @@ template <class S>
 int run(const Opts& o, const Num<S>& v) {
     using A = Api<S>;
     S* tri = nullptr; S* norm = nullptr; size_t n_tri = 0;
-    const int rc_load = o.proc ? A::proc(o.proc, &tri, &norm, &n_tri) : A::load(o.obj.c_str(), &tri, &norm, &n_tri);
+    const int rc_load = o.proc ? A::proc(o.proc, &tri, &norm, &n_tri, o.arith) : A::load(o.obj.c_str(), &tri, &norm, &n_tri, o.arith);
     if (rc_load != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
     if (n_tri == 0) { std::fprintf(stderr, "The given scene is empty or cannot be loaded\n"); return 1; }   // static.cpp:77-80
-    if (o.rot_axis >= 0) A::rotate(tri, n_tri, o.rot_axis, v.rot_deg);
+    if (o.rot_axis >= 0) A::rotate(tri, n_tri, o.rot_axis, v.rot_deg, o.arith);
 
     std::printf("Building BVH ( using BinnedSahBuilder%s )...\n", o.gpu_bvh ? " on the GPU" : "");
     const double t0 = now_s();
     typename A::Node* nodes = nullptr; uint64_t* prim = nullptr; size_t n_nodes = 0;
-    const int rc_bvh = A::bvh(tri, n_tri, &nodes, &n_nodes, &prim, o.gpu_bvh, o.device);
+    const int rc_bvh = A::bvh(tri, n_tri, &nodes, &n_nodes, &prim, o.gpu_bvh, o.device, o.arith);
     if (rc_bvh != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
     std::printf("%g\n", now_s() - t0);
     std::printf("BVH of %zu node(s) and %zu reference(s)\n", n_nodes, n_tri);
@@ -223,7 +238,7 @@ int run(const Opts& o, const Num<S>& v) {
     // frame poses: count + k orbit rotations for frame k (count = 0, frames = 1: the plain camera)
     const uint32_t n_pose = uint32_t(o.orbit_count + o.frames);
     std::vector<S> bases(12 * size_t(n_pose)), suns(3 * size_t(n_pose));
-    if (A::orbit(v, o.W, o.H, n_pose, bases.data(), suns.data()) != CERES_OK) {
+    if (A::orbit(v, o.W, o.H, n_pose, bases.data(), suns.data(), o.arith) != CERES_OK) {
         std::fprintf(stderr, "error: %s\n", ceres_last_error()); destroy(); return 1;
     }
     std::vector<uint8_t> rgb(3 * o.W * o.H);
@@ -288,5 +303,7 @@ int run(const Opts& o, const Num<S>& v) {
 int main(int argc, char** argv) {
     Opts o;
     if (!parse(argc, argv, o)) return usage();
+    if (o.f64) o.arith = CERES_ARITH_EXACT;                      // render<double>: contraction-free only
+    if (o.arith == CERES_ARITH_FMA) o.mode |= CERES_MODE_FMA;
     return o.f64 ? run<double>(o, o.d) : run<float>(o, o.f);
 }

@@ -725,6 +725,43 @@ int ceres_orbit_cameras_f64(const double eye[3], const double dir[3], const doub
                                  basis12, sun3, dir3);
 }
 
+// Content hash for the drop-in render.hpp's per-call scene check (render.hpp:86-156 reads the
+// caller's arrays on every call): 64-bit multiply-mix over 8-byte words in 256-KiB chunks hashed
+// in parallel (OpenMP), chunk hashes folded in order -- deterministic for a given byte string.
+uint64_t ceres_content_hash(const void* p, size_t bytes) {
+    if (!p || !bytes) return 0x9e3779b97f4a7c15ull ^ bytes;
+    constexpr size_t kChunk = 256 << 10;
+    const size_t n_chunks = (bytes + kChunk - 1) / kChunk;
+    auto mix = [](uint64_t h, uint64_t w) {
+        h ^= w * 0x9e3779b97f4a7c15ull;
+        h = (h << 31) | (h >> 33);
+        return h * 0xbf58476d1ce4e5b9ull;
+    };
+    auto chunk_hash = [&](size_t c) {
+        const unsigned char* b = static_cast<const unsigned char*>(p) + c * kChunk;
+        const size_t n = std::min(kChunk, bytes - c * kChunk);
+        uint64_t h[4] = {0x243f6a8885a308d3ull, 0x13198a2e03707344ull, 0xa4093822299f31d0ull, 0x082efa98ec4e6c89ull};
+        size_t i = 0;
+        for (; i + 32 <= n; i += 32) {
+            uint64_t w[4];
+            std::memcpy(w, b + i, 32);
+            for (int k = 0; k < 4; ++k) h[k] = mix(h[k], w[k]);
+        }
+        for (; i < n; i += 8) {                                  // < 32 bytes left: zero-padded words
+            uint64_t w = 0;
+            std::memcpy(&w, b + i, std::min<size_t>(8, n - i));
+            h[0] = mix(h[0], w);
+        }
+        return mix(mix(mix(mix(h[0], h[1]), h[2]), h[3]), n);
+    };
+    std::vector<uint64_t> hs(n_chunks);
+    #pragma omp parallel for schedule(static) if (n_chunks > 4)
+    for (size_t c = 0; c < n_chunks; ++c) hs[c] = chunk_hash(c);
+    uint64_t h = 0x6a09e667f3bcc908ull ^ bytes;
+    for (uint64_t x : hs) h = mix(h, x);
+    return h;
+}
+
 // ---- the same steps in a chosen arithmetic (CERES_ARITH_EXACT / CERES_ARITH_FMA) ----
 static int bad_arith(int arith) {
     return arith == CERES_ARITH_EXACT || arith == CERES_ARITH_FMA ? 0 : set_error(CERES_EINVAL, "unknown arithmetic %d", arith);

@@ -19,8 +19,21 @@
 // error path); tri_norms == nullptr throws instead of dereferencing null (render.hpp:142).
 // Scalar = double (anim.cpp -d) runs the double-precision GPU path (ceres_render_f64) over the
 // caller's bvh::Bvh<double> / bvh::Triangle<double> (64-B nodes, 96-B triangles).
-// The uploaded scene is cached per (bvh, triangles, tri_norms, node_count, fingerprint), so
-// multi-frame callers like anim.cpp:82-125 upload once.  Link with -lceres_hip.
+//
+// Per-call contract (render.hpp:86-156 reads bvh, triangles and tri_norms on EVERY call): the
+// uploaded scene is reused only while the full content of those arrays -- BVH nodes,
+// primitive_indices, triangles and tri_norms -- is unchanged (a multithreaded 64-bit content
+// hash per call, ceres_content_hash: ~0.1 ms for the dragon's 3 MB), so multi-frame callers like
+// anim.cpp:82-125 upload once and a caller that edits any of them in place gets the edited scene.
+// Define CERES_DROPIN_TRUST_UNCHANGED to skip the hash (the caller promises never to edit the
+// arrays behind the same pointers).
+//
+// Arithmetic: the reference's CMake build (g++ -O3 -mavx2 -mfma) contracts a*b+c into FMA, so a
+// caller compiling its scene code (obj_norms / lib/bvh / rotate_triangles) that way holds the
+// contracted scene; this header then renders, rotates and builds the camera basis in the same
+// arithmetic (CERES_ARITH_FMA / CERES_MODE_FMA).  Default: FMA when GCC optimises with FMA
+// enabled (__GNUC__ && !__clang__ && __FMA__ && __OPTIMIZE__), else contraction-free; override
+// with -DCERES_DROPIN_ARITH=CERES_ARITH_EXACT or CERES_ARITH_FMA.  Link with -lceres_hip.
 #ifndef CERES_RENDER_HPP_DROPIN
 #define CERES_RENDER_HPP_DROPIN
 
@@ -38,6 +51,14 @@
 #include <vector>
 
 #include "ceres_render.h"
+
+#ifndef CERES_DROPIN_ARITH
+#if defined(__GNUC__) && !defined(__clang__) && defined(__FMA__) && defined(__OPTIMIZE__)
+#define CERES_DROPIN_ARITH CERES_ARITH_FMA
+#else
+#define CERES_DROPIN_ARITH CERES_ARITH_EXACT
+#endif
+#endif
 
 namespace ceres {
 
@@ -75,32 +96,18 @@ using HostBvh64 = BasicHostBvh<double>;
 
 namespace detail {
 
+// The scene uploaded by the last call, keyed by the caller's pointers and the content hashes
+// of everything render() reads (render.hpp:86-156).
 struct SceneCache {
-    const void *bvh = nullptr, *tris = nullptr, *norms = nullptr, *nodes = nullptr;
+    const void *bvh = nullptr, *tris = nullptr, *norms = nullptr, *nodes = nullptr, *prim = nullptr;
     size_t node_count = 0, n_tri = 0;
     bool f64 = false;
-    uint64_t fingerprint = 0;
+    uint64_t h_nodes = 0, h_prim = 0, h_tris = 0, h_norms = 0;
     ceres_scene* scene = nullptr;
     std::mutex mu;
     ~SceneCache() { if (scene) ceres_scene_destroy(scene); }
 };
 inline SceneCache& cache() { static SceneCache c; return c; }
-
-inline uint64_t fnv(uint64_t h, const void* p, size_t n) {
-    const unsigned char* b = static_cast<const unsigned char*>(p);
-    for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ull; }
-    return h;
-}
-// Sampled fingerprint (every 4096th record + both ends) so an edited mesh re-uploads.
-inline uint64_t fingerprint(const void* nodes, size_t n_nodes, size_t node_bytes, const void* tris, size_t n_tri,
-                            size_t tri_bytes) {
-    uint64_t h = 1469598103934665603ull;
-    for (size_t i = 0; i < n_nodes; i += 4096) h = fnv(h, static_cast<const char*>(nodes) + node_bytes * i, node_bytes);
-    if (n_nodes) h = fnv(h, static_cast<const char*>(nodes) + node_bytes * (n_nodes - 1), node_bytes);
-    for (size_t i = 0; i < n_tri; i += 4096) h = fnv(h, static_cast<const char*>(tris) + tri_bytes * i, tri_bytes);
-    if (n_tri) h = fnv(h, static_cast<const char*>(tris) + tri_bytes * (n_tri - 1), tri_bytes);
-    return h;
-}
 
 [[noreturn]] inline void fail(const char* what) {
     throw std::runtime_error(std::string(what) + ": " + ceres_last_error());
@@ -118,14 +125,16 @@ struct Camera {                                                      // render.h
 };
 
 // render.hpp:24-44 -- rotation about one axis, in place, rebuilding each triangle from p0,
-// p1() = p0 - e1, p2() = p0 + e2 (bit-identical to the reference; runs on the host).
+// p1() = p0 - e1, p2() = p0 + e2 (bit-identical to the reference in CERES_DROPIN_ARITH's
+// arithmetic; float scenes -- the double build's contraction is not modelled; runs on the host).
 template <size_t Axis, typename Scalar, typename Tri>
 static void rotate_triangles(Scalar degrees, Tri* triangles, size_t triangle_count) {
     static_assert((std::is_same<Scalar, float>::value && sizeof(Tri) == 48) ||
                   (std::is_same<Scalar, double>::value && sizeof(Tri) == 96), "ceres: bvh::Triangle<float|double> only");
     const int rc = std::is_same<Scalar, double>::value
         ? ceres_rotate_triangles_f64(reinterpret_cast<double*>(triangles), triangle_count, int(Axis), double(degrees))
-        : ceres_rotate_triangles(reinterpret_cast<float*>(triangles), triangle_count, int(Axis), float(degrees));
+        : ceres_rotate_triangles_arith(reinterpret_cast<float*>(triangles), triangle_count, int(Axis), float(degrees),
+                                       CERES_DROPIN_ARITH);
     if (rc != CERES_OK) ceres::detail::fail("rotate_triangles");
 }
 
@@ -140,37 +149,50 @@ std::pair<int, int> render(const Camera<Scalar>& camera, const Vec& sun_position
     const auto* nodes = bvh.nodes.get();
     const size_t n_nodes = bvh.node_count;
     static_assert(sizeof(*nodes) == 8 * sizeof(Scalar), "bvh node must be bvh::Bvh<Scalar>::Node layout");
-    // triangle count = end of the furthest leaf (the reference never passes it explicitly): a scan
-    // of every node, done again only when the cached scene's BVH identity or fingerprint changes
-    // (a 10M-triangle BVH has 20M nodes: the scan alone would cost tens of ms per call)
-    auto scan_n_tri = [&] {
-        size_t n = 0;
-        for (size_t k = 0; k < n_nodes; ++k)
-            if (nodes[k].primitive_count)
-                n = std::max<size_t>(n, size_t(nodes[k].first_child_or_primitive) + size_t(nodes[k].primitive_count));
-        return n;
-    };
+    const uint64_t* prim = reinterpret_cast<const uint64_t*>(bvh.primitive_indices.get());
     auto& c = ceres::detail::cache();
     std::lock_guard<std::mutex> lock(c.mu);
-    const bool same_bvh = c.scene && c.bvh == &bvh && c.nodes == nodes && c.node_count == n_nodes && c.f64 == kF64;
-    size_t n_tri = same_bvh ? c.n_tri : scan_n_tri();
-    uint64_t fp = ceres::detail::fingerprint(nodes, n_nodes, sizeof(*nodes), triangles, n_tri, sizeof(TriT));
-    if (same_bvh && fp != c.fingerprint) {                            // edited in place: full rescan
-        n_tri = scan_n_tri();
-        fp = ceres::detail::fingerprint(nodes, n_nodes, sizeof(*nodes), triangles, n_tri, sizeof(TriT));
+    const bool same_ptrs = c.scene && c.bvh == &bvh && c.nodes == nodes && c.prim == prim && c.tris == triangles &&
+                           c.norms == tri_norms && c.node_count == n_nodes && c.f64 == kF64;
+#ifdef CERES_DROPIN_TRUST_UNCHANGED
+    const bool reuse = same_ptrs;
+#else
+    // every call: the BVH nodes first (the triangle count follows from them), then the rest
+    const uint64_t h_nodes = ceres_content_hash(nodes, n_nodes * sizeof(*nodes));
+    size_t n_tri = c.n_tri;
+    if (!same_ptrs || h_nodes != c.h_nodes) {
+        // triangle count = end of the furthest leaf (the reference never passes it explicitly)
+        n_tri = 0;
+        for (size_t k = 0; k < n_nodes; ++k)
+            if (nodes[k].primitive_count)
+                n_tri = std::max<size_t>(n_tri, size_t(nodes[k].first_child_or_primitive) + size_t(nodes[k].primitive_count));
     }
-    if (!c.scene || c.bvh != &bvh || c.tris != triangles || c.norms != tri_norms || c.node_count != n_nodes ||
-        c.n_tri != n_tri || c.fingerprint != fp || c.f64 != kF64) {
+    const uint64_t h_prim = ceres_content_hash(prim, n_tri * sizeof(uint64_t));
+    const uint64_t h_tris = ceres_content_hash(triangles, n_tri * sizeof(TriT));
+    const uint64_t h_norms = ceres_content_hash(tri_norms, n_tri * 9 * sizeof(Scalar));
+    const bool reuse = same_ptrs && h_nodes == c.h_nodes && n_tri == c.n_tri && h_prim == c.h_prim &&
+                       h_tris == c.h_tris && h_norms == c.h_norms;
+#endif
+    if (!reuse) {
+#ifdef CERES_DROPIN_TRUST_UNCHANGED
+        size_t n_tri = 0;
+        for (size_t k = 0; k < n_nodes; ++k)
+            if (nodes[k].primitive_count)
+                n_tri = std::max<size_t>(n_tri, size_t(nodes[k].first_child_or_primitive) + size_t(nodes[k].primitive_count));
+#endif
         if (c.scene) ceres_scene_destroy(c.scene);
-        const uint64_t* prim = reinterpret_cast<const uint64_t*>(bvh.primitive_indices.get());
+        c.scene = nullptr;
         c.scene = kF64 ? ceres_scene_create_f64(reinterpret_cast<const double*>(triangles), n_tri,
                                                 reinterpret_cast<const double*>(tri_norms), nodes, n_nodes, prim, 0, 0)
                        : ceres_scene_create(reinterpret_cast<const float*>(triangles), n_tri,
                                             reinterpret_cast<const float*>(tri_norms), nodes, n_nodes, prim, 0, 0);
         if (!c.scene) ceres::detail::fail("ceres_scene_create");
-        c.bvh = &bvh; c.nodes = nodes; c.tris = triangles; c.norms = tri_norms; c.node_count = n_nodes; c.n_tri = n_tri;
-        c.fingerprint = fp;
+        c.bvh = &bvh; c.nodes = nodes; c.prim = prim; c.tris = triangles; c.norms = tri_norms; c.node_count = n_nodes;
+        c.n_tri = n_tri;
         c.f64 = kF64;
+#ifndef CERES_DROPIN_TRUST_UNCHANGED
+        c.h_nodes = h_nodes; c.h_prim = h_prim; c.h_tris = h_tris; c.h_norms = h_norms;
+#endif
     }
     Scalar eye[3] = {Scalar(camera.eye[0]), Scalar(camera.eye[1]), Scalar(camera.eye[2])};
     Scalar dir[3] = {Scalar(camera.dir[0]), Scalar(camera.dir[1]), Scalar(camera.dir[2])};
@@ -184,8 +206,10 @@ std::pair<int, int> render(const Camera<Scalar>& camera, const Vec& sun_position
         if (ceres_camera_basis_f64(eye, dir, up, camera.fov, width, height, basis + 3) != CERES_OK) ceres::detail::fail("camera basis");
         rc = ceres_render_f64(c.scene, basis, sun, CERES_MODE_FULL, pixels, nullptr, width, height, &st);
     } else {
-        if (ceres_camera_basis(eye, dir, up, camera.fov, width, height, basis + 3) != CERES_OK) ceres::detail::fail("camera basis");
-        rc = ceres_render_f32(c.scene, basis, sun, CERES_MODE_FULL, pixels, nullptr, width, height, &st);
+        if (ceres_camera_basis_arith(eye, dir, up, camera.fov, width, height, basis + 3, CERES_DROPIN_ARITH) != CERES_OK)
+            ceres::detail::fail("camera basis");
+        const int mode = CERES_MODE_FULL | (CERES_DROPIN_ARITH == CERES_ARITH_FMA ? CERES_MODE_FMA : 0);
+        rc = ceres_render_f32(c.scene, basis, sun, mode, pixels, nullptr, width, height, &st);
     }
     if (rc != CERES_OK) ceres::detail::fail("ceres render");
     return std::pair<int, int>(int(st.rays), int(st.hits));

@@ -291,6 +291,11 @@ int ceres_scene_read_timing(ceres_scene* scene, double* kernel_ms, double* shado
  * the wavefront's primary node pairs, its shadow node pairs}.  Synchronises the device. */
 int ceres_scene_wave_log(ceres_scene* scene, uint64_t* out, size_t max_waves, size_t* n_waves);
 
+/* 64-bit content hash of a byte range (multithreaded; deterministic for a given byte string) --
+ * what the drop-in include/ceres/render.hpp uses to honour render.hpp:86-156's per-call reading
+ * of the caller's triangles / tri_norms / BVH while uploading a scene only when they change. */
+uint64_t ceres_content_hash(const void* p, size_t bytes);
+
 /* Launch-geometry introspection for the roofline accounting in bench.py (kernel names as
  * they appear in rocprofv3 traces). */
 const char* ceres_kernel_names(void);

@@ -149,3 +149,54 @@ def test_scene_accepts_leaf_too_large_for_packed_word(pkg):
     assert not h
     err = L.ceres_last_error()
     assert b"BVH4" not in err and b"device" in err, err
+
+
+def test_scene_accepts_big_leaf_beside_uncollapsed_inner_pairs(pkg):
+    """the shadow BVH4's tree check must not count piece nodes.  Root = {a leaf of 1000
+    coincident-centroid triangles (-> ~20 piece nodes), an inner node whose two children are inner
+    nodes again}: 4 sibling pairs, 3 collapsed records + the pieces.  Without a GPU, scene creation
+    gets past the relayout and the BVH4 (no "do not form a tree") and fails only at the device step."""
+    import numpy as np
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    n = 1004
+    tri = np.zeros((n, 12), np.float32)
+    tri[:, 3] = 1.0
+    tri[:, 8] = 1.0
+    nor = np.zeros((n, 9), np.float32)
+    nodes = np.zeros(9, dtype=[("b", np.float32, 6), ("count", np.uint32), ("first", np.uint32)])
+    nodes["b"][:] = [-1, 1, -1, 1, -1, 1]
+    nodes[0]["first"] = 1                                         # root -> 1, 2
+    nodes[1]["count"], nodes[1]["first"] = 1000, 0                # the big leaf
+    nodes[2]["first"] = 3                                         # inner -> 3, 4 (both inner)
+    nodes[3]["first"] = 5
+    nodes[4]["first"] = 7
+    for k, first in zip((5, 6, 7, 8), (1000, 1001, 1002, 1003)):
+        nodes[k]["count"], nodes[k]["first"] = 1, first
+    prim = np.arange(n, dtype=np.uint64)
+    L = pkg.lib()
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))     # noqa: E731
+    h = L.ceres_scene_create(fp(tri), n, fp(nor), nodes.ctypes.data_as(ctypes.c_void_p), nodes.shape[0],
+                             prim.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 0, 0)
+    assert not h
+    err = L.ceres_last_error()
+    assert b"tree" not in err and b"BVH4" not in err and b"device" in err, err
+
+
+def test_content_hash(pkg):
+    """ceres_content_hash (the drop-in's per-call scene check): deterministic, and any single changed
+    byte -- in a full 32-B block, in the <32-B tail, in any 256-KiB chunk -- changes it."""
+    import numpy as np
+    L = pkg.lib()
+    rng = np.random.default_rng(7)
+    for size in (1, 7, 31, 33, 1000, (256 << 10) + 5, 3 << 20):
+        a = rng.integers(0, 256, size, dtype=np.uint8)
+        h0 = L.ceres_content_hash(a.ctypes.data_as(ctypes.c_void_p), size)
+        assert h0 == L.ceres_content_hash(a.ctypes.data_as(ctypes.c_void_p), size)
+        for pos in {0, size // 2, size - 1, max(0, size - 9)}:
+            b = a.copy()
+            b[pos] ^= 1
+            assert L.ceres_content_hash(b.ctypes.data_as(ctypes.c_void_p), size) != h0, (size, pos)
+        if size > 1:
+            assert L.ceres_content_hash(a.ctypes.data_as(ctypes.c_void_p), size - 1) != h0

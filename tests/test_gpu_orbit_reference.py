@@ -4,7 +4,8 @@ transform.hpp:67-112) rendered the way bench.py renders it -- one ceres_render_b
 launch per 64 frames per rank, each rank its interleaved 8-row blocks, frames in the
 FrameExchange batch order at N > 1 -- reassembled, and compared by PPM sha256 with the
 reference's own render() of the same view (tests/golden/orbit/<cfg>.json, made by
-oracle/_ref/ref_render_exact --orbit-views).  The step's rays / hits equal the sum of the
+oracle/_ref/ref_render{_exact,} --orbit-views): in both arithmetics, the reference CMake build's
+(FMA contraction, bench.py's default) and the contraction-free one.  The step's rays / hits equal the sum of the
 reference's per-view counts (render.hpp:155).  N = 1 is the bench step on one GPU; N = 2, 4, 8
 are the weak-scaling steps (16N views, 22.5/N degrees apart), every rank's share rendered here
 in turn on the one GPU."""
@@ -22,27 +23,32 @@ pytestmark = pytest.mark.gpu
 MAXF = 64          # frames per batch launch (kMaxFrames)
 
 
-def _basis0(meta, cfg):
-    bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
+def _basis0(meta, cfg, build):
+    b = meta["ref_basis"] if build == "ref" else meta["basis"]
+    bits = [int(h, 16) for h in b["dir"] + b["u"] + b["v"]]
     return np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
 
 
 _scenes = {}
 
 
-def _scene(pkg, name):
-    if name not in _scenes:
+def _scene(pkg, name, arith):
+    if (name, arith) not in _scenes:
         _scenes.clear()                     # one big scene resident at a time
         cfg = configs.CONFIGS[name]
-        mesh, bvh, cam = pkg.prepare(cfg)
-        _scenes[name] = (pkg.Scene(mesh, bvh, device=0), cam)
-    return _scenes[name]
+        mesh, bvh, cam = pkg.prepare(cfg, arith=arith)
+        _scenes[(name, arith)] = (pkg.Scene(mesh, bvh, device=0), cam)
+    return _scenes[(name, arith)]
 
 
-@pytest.mark.parametrize("name,world", [("bunny_640", 1), ("dragon_1080", 1), ("dragon_1080", 2), ("dragon_1080", 4),
-                                        ("dragon_1080", 8), ("bunny_1080", 1), ("bunny_1080_primary", 1),
-                                        ("dragon_4096", 1), ("dragon_4096", 8), ("proc_c5", 1), ("proc_c5", 8)])
-def test_bench_step_frames_match_reference(pkg, name, world):
+CASES = [("bunny_640", 1), ("dragon_1080", 1), ("dragon_1080", 2), ("dragon_1080", 4), ("dragon_1080", 8),
+         ("bunny_1080", 1), ("bunny_1080_primary", 1), ("dragon_4096", 1), ("dragon_4096", 8), ("proc_c5", 1),
+         ("proc_c5", 8)]
+
+
+@pytest.mark.parametrize("build", ["ref", "exact"])
+@pytest.mark.parametrize("name,world", CASES)
+def test_bench_step_frames_match_reference(pkg, name, world, build):
     import torch
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a HIP device (no CPU fallback exists)")
@@ -51,14 +57,15 @@ def test_bench_step_frames_match_reference(pkg, name, world):
     W, H = cfg["W"], cfg["H"]
     meta, _, _ = load_golden(name)
     fx = load_orbit(name)["by_step_bits"]
-    scene, cam = _scene(pkg, name)
+    arith = pkg.ARITH_FMA if build == "ref" else pkg.ARITH_EXACT
+    scene, cam = _scene(pkg, name, arith)
     F = 16 * world
-    b12, s3, steps = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=_basis0(meta, cfg))
+    b12, s3, steps = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=_basis0(meta, cfg, build))
     if world > 1:
         order = D.exchange_order(F, world)
         b12, s3, steps = b12[order], s3[order], steps[order]
     row_block = 8 if world > 1 else H
-    mode = pkg.cfg_mode(cfg)
+    mode = pkg.cfg_mode(cfg, arith)
     st = torch.cuda.current_stream().cuda_stream
     _, maxrows = D.ppm_row_permutation(H, row_block, world)
     idx = torch.as_tensor(D.ppm_row_permutation(H, row_block, world)[0], device="cuda")
@@ -86,10 +93,11 @@ def test_bench_step_frames_match_reference(pkg, name, world):
     bad = []
     ref_rays = ref_hits = 0
     for f in range(F):
-        e = fx["%08x" % int(np.asarray(steps[f], np.float32).view(np.uint32))]
+        e0 = fx["%08x" % int(np.asarray(steps[f], np.float32).view(np.uint32))]
+        e = e0["ref"] if build == "ref" else e0
         ref_rays += e["rays"]; ref_hits += e["hits"]
         full = torch.cat([b[f] for b in per_rank])[idx].cpu().numpy()
         if hashlib.sha256(head + full.tobytes()).hexdigest() != e["sha256"]:
-            bad.append((f, e["k"]))
+            bad.append((f, e0["k"]))
     assert not bad, f"frames differing from the reference (batch frame, orbit view k): {bad}"
     assert (rays, hits) == (ref_rays, ref_hits)

@@ -15,7 +15,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, REPO, golden_names, hexbits, load_golden, ppm_budget_ok
+from conftest import GOLDEN, REPO, golden_names, hexbits, load_golden, load_ref_records, ppm_budget_ok
 
 import configs
 
@@ -355,17 +355,22 @@ def test_batch_rejects_bad_frame_counts(gpu):
         scene.render_batch_device(np.zeros((2, 12), np.float32), np.zeros((3, 3), np.float32), 8, 8)
 
 
-def test_cli_orbit_frames(gpu, tmp_path):
+# ./render's arithmetic: default (--fma) = the reference's CMake build, --exact = -ffp-contract=off
+CLI_ARITH = {"ref": [], "exact": ["--exact"]}
+
+
+@pytest.mark.parametrize("build", ["ref", "exact"])
+def test_cli_orbit_frames(gpu, tmp_path, build):
     """./render --orbit ... --frames 2 writes the anim.cpp orbit frames; frame 0 = fixture pose."""
     pkg = gpu
     name = "dragon_orbit3_333x217"
     meta, _, ppm = load_golden(name)
     out = tmp_path / "orbit.ppm"
-    args = configs.cli_args(configs.CONFIGS[name])
+    args = configs.cli_args(configs.CONFIGS[name]) + CLI_ARITH[build]
     r = subprocess.run([pkg.CLI_PATH] + args + ["--frames", "2", "-o", str(out)], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0, r.stderr
-    assert (tmp_path / "orbit_000.ppm").read_bytes() == ppm["exact"]
+    assert (tmp_path / "orbit_000.ppm").read_bytes() == ppm[build]
     assert (tmp_path / "orbit_001.ppm").exists()
     assert "Total Rays:" in r.stdout
 
@@ -430,58 +435,105 @@ def test_c5_single_launch_xcd_local_order(gpu):
     scene.close()
 
 
-@pytest.mark.parametrize("gpu_bvh", [False, True])
-def test_cli_writes_reference_ppm(gpu, tmp_path, gpu_bvh):
+@pytest.mark.parametrize("gpu_bvh,build", [(False, "ref"), (False, "exact"), (True, "exact")])
+def test_cli_writes_reference_ppm(gpu, tmp_path, gpu_bvh, build):
+    """static.cpp's sequence: the default writes the reference CMake build's PPM byte for byte,
+    --exact the contraction-free build's (bunny 640x480 is where they differ most: 20 bytes)."""
     pkg = gpu
     name = "bunny_640"
     meta, _, ppm = load_golden(name)
     out = tmp_path / "bunny.ppm"
-    args = configs.cli_args(configs.CONFIGS[name]) + (["--gpu-bvh"] if gpu_bvh else [])
+    args = configs.cli_args(configs.CONFIGS[name]) + (["--gpu-bvh"] if gpu_bvh else []) + CLI_ARITH[build]
     r = subprocess.run([pkg.CLI_PATH] + args + ["-o", str(out)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    assert "Rays: %d\tHits: %d" % (meta["exact"]["rays"], meta["exact"]["hits"]) in r.stdout
-    assert out.read_bytes() == ppm["exact"]
+    assert "Rays: %d\tHits: %d" % (meta[build]["rays"], meta[build]["hits"]) in r.stdout
+    assert out.read_bytes() == ppm[build]
 
 
-def test_dropin_render_hpp_runs(gpu, tmp_path):
-    """A static.cpp-style program on include/ceres/render.hpp renders the reference frame."""
-    pkg = gpu
-    name = "dragon_333x217"
-    meta, _, _ = load_golden(name)
-    src = tmp_path / "app.cpp"
-    src.write_text(r'''
+DROPIN_APP = r"""
 #include <cstdio>
 #include <vector>
 #include "ceres/render.hpp"
+// static.cpp's sequence (load :76, rotate :83-88, BVH :100-107, render :130) on the drop-in header,
+// then the caller EDITS its arrays in place between two render() calls (render.hpp:86-156 reads
+// them on every call): argv[3] = a triangle whose three vertex normals are flipped, argv[4] = a
+// triangle whose p0 moves by 1e-3 along y.  Both float framebuffers go to argv[2].{0,1}.
 int main(int argc, char** argv) {
     float* tri; float* nrm; size_t n;
-    if (ceres_obj_load(argv[1], &tri, &nrm, &n)) return 3;
+    if (ceres_obj_load_arith(argv[1], &tri, &nrm, &n, CERES_DROPIN_ARITH)) return 3;
     rotate_triangles<0>(90.0f, reinterpret_cast<ceres::HostTriangle*>(tri), n);
     uint32_t* nodes; uint64_t* prim; size_t m;
-    if (ceres_bvh_build(tri, n, &nodes, &m, &prim)) return 4;
+    if (ceres_bvh_build_arith(tri, n, &nodes, &m, &prim, CERES_DROPIN_ARITH)) return 4;
     ceres::HostBvh bvh;
     bvh.nodes.reset(new ceres::HostBvh::Node[m]); std::memcpy(bvh.nodes.get(), nodes, 32 * m);
     bvh.primitive_indices.reset(new size_t[n]); std::memcpy(bvh.primitive_indices.get(), prim, 8 * n);
     bvh.node_count = m;
     Camera<float> cam{ceres::vec3<float>(0, -15, 2), ceres::vec3<float>(0, 1, 0), ceres::vec3<float>(0, 0, 1), 60};
     std::vector<float> px(3 * 333 * 217);
-    auto rh = render(cam, ceres::vec3<float>(-50, -20, 0), bvh, reinterpret_cast<ceres::HostTriangle*>(tri),
-                     reinterpret_cast<std::array<ceres::vec3<float>, 3>*>(nrm), px.data(), 333, 217);
-    auto rh2 = render(cam, ceres::vec3<float>(-50, -20, 0), bvh, reinterpret_cast<ceres::HostTriangle*>(tri),
-                      reinterpret_cast<std::array<ceres::vec3<float>, 3>*>(nrm), px.data(), 333, 217);
-    std::printf("%d %d %d %d\n", rh.first, rh.second, rh2.first, rh2.second);
+    auto* T = reinterpret_cast<ceres::HostTriangle*>(tri);
+    auto* N = reinterpret_cast<std::array<ceres::vec3<float>, 3>*>(nrm);
+    auto rh = render(cam, ceres::vec3<float>(-50, -20, 0), bvh, T, N, px.data(), 333, 217);
+    std::string out = argv[2];
+    if (FILE* f = std::fopen((out + ".0").c_str(), "wb")) { std::fwrite(px.data(), 4, px.size(), f); std::fclose(f); }
+    const size_t a = std::strtoul(argv[3], nullptr, 10), b = std::strtoul(argv[4], nullptr, 10);
+    for (int k = 0; k < 3; ++k) for (int c = 0; c < 3; ++c) N[a][k][c] = -N[a][k][c];
+    T[b].p0[1] += 1e-3f;
+    auto rh2 = render(cam, ceres::vec3<float>(-50, -20, 0), bvh, T, N, px.data(), 333, 217);
+    if (FILE* f = std::fopen((out + ".1").c_str(), "wb")) { std::fwrite(px.data(), 4, px.size(), f); std::fclose(f); }
+    std::printf("%d %d %d %d %d\n", rh.first, rh.second, rh2.first, rh2.second, int(CERES_DROPIN_ARITH));
     return 0;
 }
-''')
+"""
+
+
+@pytest.mark.parametrize("arith", ["default", "exact"])
+def test_dropin_render_hpp_per_call_contract(gpu, oracle_mod, tmp_path, arith):
+    """A static.cpp-style program on include/ceres/render.hpp: render<float>()'s host float
+    framebuffer equals the reference's (fixture records) and the oracle's bit for bit; after the
+    caller edits one triangle's normals and another triangle's p0 IN PLACE (neither at a 4096th
+    index), the next render() call sees the edited scene -- its framebuffer equals the oracle's
+    render of the edited arrays.  Compiled with g++ -O2 -mfma (default: the reference CMake build's
+    FMA arithmetic, CERES_DROPIN_ARITH) and with -DCERES_DROPIN_ARITH=CERES_ARITH_EXACT."""
+    pkg = gpu
+    name = "dragon_333x217"
+    meta, rec, _ = load_golden(name)
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    contract = arith == "default"
+    # two visible lit triangles from the fixture's records, neither a multiple of 4096
+    lit = rec["prim"][(rec["prim"] >= 0) & (rec["shadow"] == 0)]
+    cand = [int(p) for p in np.unique(lit) if p % 4096 and p > 0]
+    t_norm, t_move = cand[len(cand) // 3], cand[2 * len(cand) // 3]
+    src = tmp_path / "app.cpp"
+    src.write_text(DROPIN_APP)
     exe = tmp_path / "app"
     pkgdir = os.path.dirname(pkg.LIB_PATH)
-    r = subprocess.run(["g++", "-std=c++17", "-O1", "-I" + os.path.join(REPO, "include"), str(src), "-o", str(exe),
+    flags = ["-O2", "-mfma"] + ([] if contract else ["-DCERES_DROPIN_ARITH=CERES_ARITH_EXACT"])
+    r = subprocess.run(["g++", "-std=c++17"] + flags + ["-I" + os.path.join(REPO, "include"), str(src), "-o", str(exe),
                         "-L" + pkgdir, "-lceres_hip", "-Wl,-rpath," + pkgdir], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    r = subprocess.run([str(exe), os.path.join(REPO, "data", "dragon.obj")], capture_output=True, text=True, timeout=120)
+    stem = str(tmp_path / "px")
+    r = subprocess.run([str(exe), os.path.join(REPO, "data", "dragon.obj"), stem, str(t_norm), str(t_move)],
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    rays, hits, rays2, hits2 = map(int, r.stdout.split())
-    assert (rays, hits) == (rays2, hits2) == (meta["exact"]["rays"], meta["exact"]["hits"])
+    rays, hits, rays2, hits2, ar = map(int, r.stdout.split())
+    build = "ref" if contract else "exact"
+    assert ar == (1 if contract else 0)
+    assert (rays, hits) == (meta[build]["rays"], meta[build]["hits"])
+    px0 = np.fromfile(stem + ".0", np.float32)
+    px1 = np.fromfile(stem + ".1", np.float32)
+    recb = load_ref_records(name) if contract else rec
+    pix = recb["pixel"].astype(np.int64)
+    np.testing.assert_array_equal(px0.reshape(-1, 3)[pix].view(np.uint32), recb["rgb"].view(np.uint32))
+    sc = oracle_mod.prepare(cfg, contract=contract)
+    o0 = oracle_mod.render(sc, cfg, want_ppm=False)
+    np.testing.assert_array_equal(px0.view(np.uint32), o0["pixels"].view(np.uint32))
+    sc["norm"][t_norm] = -sc["norm"][t_norm]
+    sc["tri"][t_move, 1] += np.float32(1e-3)
+    o1 = oracle_mod.render(sc, cfg, want_ppm=False)
+    assert not np.array_equal(o0["pixels"], o1["pixels"])          # the edits are visible
+    np.testing.assert_array_equal(px1.view(np.uint32), o1["pixels"].view(np.uint32))
+    assert (rays2, hits2) == (o1["rays"], o1["hits"])
 
 
 @pytest.mark.parametrize("world,row_block", [(1, 8), (2, 8), (3, 5), (5, 16)])
@@ -525,20 +577,21 @@ def test_render_multi_rejects_shared_scene(gpu):
         pkg.render_multi([sc, sc], pinned_basis(meta, cfg), pinned_sun(meta, cfg), cfg["W"], cfg["H"])
 
 
-def test_cli_gpus_splits_frame(gpu, tmp_path):
+@pytest.mark.parametrize("build", ["ref", "exact"])
+def test_cli_gpus_splits_frame(gpu, tmp_path, build):
     """./render --gpus 3 --row-block 5: the frame split over 3 ranks (device 0 reused on a one-GPU
     box) writes the reference's PPM and counts."""
     pkg = gpu
     name = "bunny_640"
     meta, _, ppm = load_golden(name)
     out = tmp_path / "bunny3.ppm"
-    args = configs.cli_args(configs.CONFIGS[name])
+    args = configs.cli_args(configs.CONFIGS[name]) + CLI_ARITH[build]
     r = subprocess.run([pkg.CLI_PATH] + args + ["--gpus", "3", "--row-block", "5", "-o", str(out)], capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "on 3 HIP ranks" in r.stdout
-    assert "Rays: %d\tHits: %d" % (meta["exact"]["rays"], meta["exact"]["hits"]) in r.stdout
-    assert out.read_bytes() == ppm["exact"]
+    assert "Rays: %d\tHits: %d" % (meta[build]["rays"], meta[build]["hits"]) in r.stdout
+    assert out.read_bytes() == ppm[build]
 
 
 def test_concurrent_streams_render_identical_frames(gpu):
@@ -647,17 +700,18 @@ def test_fused_batch_allocates_no_shadow_queue(gpu):
     assert grown < 32 << 20, f"device memory grew by {grown / 2**20:.1f} MiB for one fused batch"
 
 
+@pytest.mark.parametrize("build", ["ref", "exact"])
 @pytest.mark.parametrize("name", ["quad_65x49_robust", "bunny_97x61_primary_robust", "dragon_orbit3_333x217"])
-def test_cli_modes_write_reference_ppm(gpu, tmp_path, name):
+def test_cli_modes_write_reference_ppm(gpu, tmp_path, name, build):
     """./render with --robust / --primary-only / --orbit (configs.cli_args) writes the
-    reference's PPM byte for byte."""
+    reference's PPM byte for byte (each build's arithmetic)."""
     pkg = gpu
     meta, _, ppm = load_golden(name)
     out = tmp_path / "out.ppm"
-    r = subprocess.run([pkg.CLI_PATH] + configs.cli_args(configs.CONFIGS[name]) + ["-o", str(out)],
+    r = subprocess.run([pkg.CLI_PATH] + configs.cli_args(configs.CONFIGS[name]) + CLI_ARITH[build] + ["-o", str(out)],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    assert out.read_bytes() == ppm["exact"]
+    assert out.read_bytes() == ppm[build]
 
 
 def test_robust_mode_rejected_for_double_scenes(gpu):

@@ -134,26 +134,34 @@ def test_golden_tiny_meshes_exist():
         assert os.path.exists(os.path.join(GOLDEN, f))
 
 
+@pytest.mark.parametrize("arith", [0, 1], ids=["exact", "fma"])
 @pytest.mark.parametrize("name", ["bunny_640", "dragon_1080", "bunny_1080", "bunny_1080_primary", "dragon_4096", "proc_c5"])
-def test_bench_views_are_the_pinned_reference_poses(pkg, name):
+def test_bench_views_are_the_pinned_reference_poses(pkg, name, arith):
     """Every view bench.py can time at N = 1, 2, 4, 8 (pkg.bench_views, F = 16N) is pinned in
-    tests/golden/orbit/<cfg>.json, and the host's orbit pose (ceres_orbit_cameras, eye and sun)
-    equals the reference Transform's bits for it (anim.cpp:76-88, transform.hpp:67-112)."""
+    tests/golden/orbit/<cfg>.json for both reference builds, with its traversal statistics, and
+    the host's orbit pose (ceres_orbit_cameras, eye and sun) equals the reference Transform's bits
+    for it in that build's arithmetic (anim.cpp:76-88, transform.hpp:67-112)."""
     from conftest import load_orbit
     fx = load_orbit(name)
     by = fx["by_step_bits"]
     assert len(by) == fx["views"] == pkg.configs.ORBIT_FIXTURE_VIEWS
     cfg = pkg.configs.CONFIGS[name]
     meta, _, _ = load_golden(name)
-    cam = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"])
-    v0 = [e for e in by.values() if e["k"] == 0][0]
-    assert v0["sha256"] == meta["ppm_sha256"]["exact"] and v0["rays"] == meta["exact"]["rays"]
+    build = "ref" if arith else "exact"
+    view = (lambda e: e["ref"]) if arith else (lambda e: e)
+    cam = pkg.Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"], arith=arith)
+    v0 = view([e for e in by.values() if e["k"] == 0][0])
+    assert v0["sha256"] == meta["ppm_sha256"][build] and v0["rays"] == meta[build]["rays"]
+    for k in ("primary_pairs", "primary_tests", "shadow_pairs", "shadow_tests"):
+        assert v0["stats"][k] == meta[build][k]
     for n in (1, 2, 4, 8):
         F = 16 * n
         b12, s3, steps = pkg.bench_views(cam, cfg["sun"], cfg["W"], cfg["H"], F)
         for f in range(F):
-            e = by["%08x" % int(np.asarray(steps[f], np.float32).view(np.uint32))]
-            assert e["k"] == f * 128 // F
+            e0 = by["%08x" % int(np.asarray(steps[f], np.float32).view(np.uint32))]
+            e = view(e0)
+            assert e0["k"] == f * 128 // F
+            assert e["stats"]["loop_vs_render_mismatch"] == 0 and e["stats"]["primary_pairs"] > 0
             if f:
                 assert hexbits(b12[f, :3]) == e["eye"], (n, f)
                 assert hexbits(s3[f]) == e["sun"], (n, f)

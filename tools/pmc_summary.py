@@ -6,7 +6,9 @@ WRITE_SIZE are KiB (TCC_EA0_RDREQ/WRREQ x 64 B); on gfx950 FETCH_SIZE reads 1/2 
 of wide (16 B/lane) reads, so the read side is doubled ("gfx950 x2 correction").  Our loads
 are 16-B per lane (global_load_dwordx4), the calibrated case.
 
-usage: tools/pmc_summary.py <config> <prof_dir> [<out.json>]
+usage: tools/pmc_summary.py <config> <prof_dir> [<out.json>] [<kernel-key suffix>]
+(the suffix, e.g. "_batch16_fma", names the launch profiled; entries of other kernels / suffixes
+of the same config are kept)
 """
 import csv
 import glob
@@ -47,6 +49,7 @@ def load(prof_dir):
 def main():
     cfg, prof = sys.argv[1], sys.argv[2]
     dst = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_summary.json")
+    suffix = sys.argv[4] if len(sys.argv) > 4 else ""
     data = load(prof)
     summ = json.load(open(dst)) if os.path.exists(dst) else {}
     entry = {}
@@ -78,8 +81,8 @@ def main():
                            ("SQ_ACTIVE_INST_ANY", "active_inst_frac")):
                 if n in c:
                     e[key] = round(c[n] / c["SQ_WAVE_CYCLES"], 4)
-        entry[k] = e
-    summ[cfg] = entry
+        entry[k + suffix] = e
+    summ.setdefault(cfg, {}).update(entry)
     with open(dst, "w") as f:
         json.dump(summ, f, indent=1, sort_keys=True)
         f.write("\n")
