@@ -57,6 +57,8 @@ EXPORTED_SYMBOLS = (
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
     "ceres_obj_load_arith", "ceres_proc_mesh_arith", "ceres_rotate_triangles_arith", "ceres_bvh_build_arith",
     "ceres_camera_basis_arith", "ceres_orbit_cameras_arith", "ceres_content_hash",
+    "ceres_bvh_build_gpu_arith", "ceres_bvh_build_device_arith", "ceres_obj_load_gpu_arith",
+    "ceres_obj_parse_device_arith", "ceres_rotate_triangles_device_arith",
 )
 
 
@@ -173,6 +175,11 @@ def lib():
     L.ceres_bvh_build_arith.argtypes = L.ceres_bvh_build.argtypes + [ctypes.c_int]
     L.ceres_camera_basis_arith.argtypes = L.ceres_camera_basis.argtypes + [ctypes.c_int]
     L.ceres_orbit_cameras_arith.argtypes = L.ceres_orbit_cameras.argtypes + [ctypes.c_int]
+    L.ceres_bvh_build_gpu_arith.argtypes = L.ceres_bvh_build_gpu.argtypes + [ctypes.c_int]
+    L.ceres_bvh_build_device_arith.argtypes = L.ceres_bvh_build_device.argtypes + [ctypes.c_int]
+    L.ceres_obj_load_gpu_arith.argtypes = L.ceres_obj_load_gpu.argtypes + [ctypes.c_int]
+    L.ceres_obj_parse_device_arith.argtypes = L.ceres_obj_parse_device.argtypes + [ctypes.c_int]
+    L.ceres_rotate_triangles_device_arith.argtypes = L.ceres_rotate_triangles_device.argtypes + [ctypes.c_int]
     _lib = L
     return L
 
@@ -270,26 +277,27 @@ def proc_mesh_f64(n):
     return Mesh(_take(t, c * 12, np.float64).reshape(c, 12), _take(nn, c * 9, np.float64).reshape(c, 9))
 
 
-def load_obj_gpu(path, device=0):
+def load_obj_gpu(path, device=0, arith=ARITH_EXACT):
     """load_obj with the text parsed on the GPU (ceres_obj_load_gpu): the same bits."""
     t, n, cnt = _fp(), _fp(), _sz()
-    _check(lib().ceres_obj_load_gpu(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt), int(device)))
+    _check(lib().ceres_obj_load_gpu_arith(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt),
+                                          int(device), int(arith)))
     c = cnt.value
     return Mesh(_take(t, c * 12, np.float32).reshape(c, 12), _take(n, c * 9, np.float32).reshape(c, 9))
 
 
-def parse_obj_device(d_text, length, stream=0):
+def parse_obj_device(d_text, length, stream=0, arith=ARITH_EXACT):
     """ceres_obj_parse_device on a device text buffer (int pointer): returns (d_tri48, d_norm36, n_tri)
     device pointers (free with device_free)."""
     t, n, cnt = _vp(), _vp(), _sz()
-    _check(lib().ceres_obj_parse_device(d_text, length, ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt),
-                                        stream or None))
+    _check(lib().ceres_obj_parse_device_arith(d_text, length, ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt),
+                                              stream or None, int(arith)))
     return t.value or 0, n.value or 0, cnt.value
 
 
-def rotate_triangles_device(d_tri48, n_tri, axis, degrees, stream=0):
+def rotate_triangles_device(d_tri48, n_tri, axis, degrees, stream=0, arith=ARITH_EXACT):
     ax = {"x": 0, "y": 1, "z": 2}[axis] if isinstance(axis, str) else int(axis)
-    _check(lib().ceres_rotate_triangles_device(d_tri48, n_tri, ax, float(degrees), stream or None))
+    _check(lib().ceres_rotate_triangles_device_arith(d_tri48, n_tri, ax, float(degrees), stream or None, int(arith)))
 
 
 def device_free(d_ptr):
@@ -325,18 +333,19 @@ def build_bvh(mesh, arith=ARITH_EXACT):
     return Bvh(_take(nodes, m.value * 8, np.uint32).reshape(-1, 8), _take(prim, len(mesh), np.uint64))
 
 
-def build_bvh_gpu(mesh, device=0):
+def build_bvh_gpu(mesh, device=0, arith=ARITH_EXACT):
     """The same binned-SAH BVH as build_bvh, built on the GPU (ceres_bvh_build_gpu)."""
     nodes, prim, m = _u32p(), _u64p(), _sz()
-    _check(lib().ceres_bvh_build_gpu(_p(mesh.tri, ctypes.c_float), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
-                                     ctypes.byref(prim), int(device)))
+    _check(lib().ceres_bvh_build_gpu_arith(_p(mesh.tri, ctypes.c_float), len(mesh), ctypes.byref(nodes),
+                                           ctypes.byref(m), ctypes.byref(prim), int(device), int(arith)))
     return Bvh(_take(nodes, m.value * 8, np.uint32).reshape(-1, 8), _take(prim, len(mesh), np.uint64))
 
 
-def build_bvh_device(d_tri48, n_tri, d_nodes32, d_prim32, stream=0):
+def build_bvh_device(d_tri48, n_tri, d_nodes32, d_prim32, stream=0, arith=ARITH_EXACT):
     """ceres_bvh_build_device on device pointers (ints); returns the node count."""
     m = _sz()
-    _check(lib().ceres_bvh_build_device(d_tri48, n_tri, d_nodes32, d_prim32, ctypes.byref(m), stream or None))
+    _check(lib().ceres_bvh_build_device_arith(d_tri48, n_tri, d_nodes32, d_prim32, ctypes.byref(m), stream or None,
+                                              int(arith)))
     return m.value
 
 

@@ -19,8 +19,9 @@
 //   * small items (<= kSmall): one wavefront builds the whole subtree in LDS, binning in the
 //     reference's sequential order (lane = axis x bin), partition via __ballot prefix counts.
 //
-// Compiled with -ffp-contract=off; the only fma is the reference's fast_multiply_add in the bin
-// index (binned_sah_builder.hpp:144-147, a true fmaf under -mfma).
+// Compiled with -ffp-contract=off; the only fma in the exact flavour is the reference's
+// fast_multiply_add in the bin index (binned_sah_builder.hpp:144-147, a true fmaf under -mfma);
+// the CERES_ARITH_FMA flavour adds the SAH-cost contractions of the reference's CMake build.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -123,12 +124,28 @@ __device__ __forceinline__ float half_area(const float lo[3], const float hi[3])
     const float d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
     return (d0 + d1) * d2 + d0 * d1;
 }
+// The reference CMake build (g++ -O3 -mfma, CERES_ARITH_FMA: G = true) contracts half_area's FIRST
+// product in find_split's sweeps (binned_sah_builder.hpp:98,109), its SECOND in the node's
+// max_split_cost (:179), and the sweep cost into fma(count, half_area, right_cost)
+// (oracle/contraction_sites.txt)
+template <bool G> __device__ __forceinline__ float half_area_sweep(const float lo[3], const float hi[3]) {
+    const float d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
+    return G ? fmaf(d0 + d1, d2, d0 * d1) : (d0 + d1) * d2 + d0 * d1;
+}
+template <bool G> __device__ __forceinline__ float half_area_node(const float lo[3], const float hi[3]) {
+    const float d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
+    return G ? fmaf(d0, d1, (d0 + d1) * d2) : (d0 + d1) * d2 + d0 * d1;
+}
+template <bool G> __device__ __forceinline__ float sweep_cost(float ha, uint32_t cnt, float right) {
+    return G ? fmaf(float(cnt), ha, right) : ha * float(cnt) + right;
+}
 
 struct BinF { float lo[3], hi[3]; uint32_t count; uint32_t pad; };
 
 // The split decision of BinnedSahBuildTask::build for one node (binned_sah_builder.hpp:86-114,
 // 166-196): SAH sweeps per axis, axis choice, leaf test, 0.4-quantile fallback.  `nb` is the
 // node box in RefNode order.  Returns false for "make a leaf now".
+template <bool G>
 __device__ bool sah_decide(const BinF* bins, uint32_t m, const float nb[6], uint32_t& axis_out,
                            uint32_t& split_out, uint32_t& sah_split_out) {
     float best_cost[3];
@@ -141,7 +158,7 @@ __device__ bool sah_decide(const BinF* bins, uint32_t m, const float nb[6], uint
         for (int i = kBins - 1; i > 0; --i) {
             for (int k = 0; k < 3; ++k) { lo[k] = lesser(lo[k], row[i].lo[k]); hi[k] = greater(hi[k], row[i].hi[k]); }
             cnt += row[i].count;
-            right[i] = half_area(lo, hi) * float(cnt);
+            right[i] = half_area_sweep<G>(lo, hi) * float(cnt);
         }
         for (int k = 0; k < 3; ++k) { lo[k] = FLT_MAX; hi[k] = -FLT_MAX; }
         cnt = 0;
@@ -150,7 +167,7 @@ __device__ bool sah_decide(const BinF* bins, uint32_t m, const float nb[6], uint
         for (int i = 0; i < kBins - 1; ++i) {
             for (int k = 0; k < 3; ++k) { lo[k] = lesser(lo[k], row[i].lo[k]); hi[k] = greater(hi[k], row[i].hi[k]); }
             cnt += row[i].count;
-            const float cost = half_area(lo, hi) * float(cnt) + right[i + 1];
+            const float cost = sweep_cost<G>(half_area_sweep<G>(lo, hi), cnt, right[i + 1]);
             if (cost < best_cost[a]) { best_cost[a] = cost; best_split[a] = uint32_t(i + 1); }
         }
     }
@@ -159,7 +176,7 @@ __device__ bool sah_decide(const BinF* bins, uint32_t m, const float nb[6], uint
     if (best_cost[axis] > best_cost[2]) axis = 2;
     uint32_t split = best_split[axis];
     const float nlo[3] = {nb[0], nb[2], nb[4]}, nhi[3] = {nb[1], nb[3], nb[5]};
-    const float leaf_cost = half_area(nlo, nhi) * (float(m) - 1.0f);      // traversal_cost = 1
+    const float leaf_cost = half_area_node<G>(nlo, nhi) * (float(m) - 1.0f);      // traversal_cost = 1
     if (best_split[axis] == kBins || best_cost[axis] >= leaf_cost) {
         if (m <= kMaxLeaf) return false;
         const float d0 = nhi[0] - nlo[0], d1 = nhi[1] - nlo[1], d2 = nhi[2] - nlo[2];   // largest_axis
@@ -415,6 +432,7 @@ __device__ void decode_bins(const BinKeys* g, BinF* out) {
 }
 
 // Split decision per large item (one thread each); leaves are final here.
+template <bool G>
 __global__ void __launch_bounds__(64) k_split(Item* items, uint32_t n_items, RefNode* nodes, const BinKeys* bins) {
     const uint32_t s = blockIdx.x * 64u + threadIdx.x;
     if (s >= n_items) return;
@@ -431,7 +449,7 @@ __global__ void __launch_bounds__(64) k_split(Item* items, uint32_t n_items, Ref
     float nb[6];
     for (int k = 0; k < 6; ++k) nb[k] = nd.bounds[k];
     uint32_t axis, split, sah;
-    if (!sah_decide(b, m, nb, axis, split, sah)) {
+    if (!sah_decide<G>(b, m, nb, axis, split, sah)) {
         nd.primitive_count = m; nd.first_child_or_primitive = it.begin;
         it.state = 0;
         return;
@@ -614,12 +632,13 @@ __device__ __forceinline__ LaneBox suffix16(LaneBox v, uint32_t i) {           /
     }
     return v;
 }
-__device__ __forceinline__ float lane_half_area(const LaneBox& b) { return half_area(b.lo, b.hi); }
+template <bool G> __device__ __forceinline__ float lane_half_area(const LaneBox& b) { return half_area_sweep<G>(b.lo, b.hi); }
 
 // One wavefront builds the whole subtree of a small item.  Bins: keyed LDS atomics (position =
 // order of the reference's sequential loop); SAH sweeps: segmented scans, 16 lanes per axis
 // (the costs depend only on box values and counts, so they are bit-identical to the sequential
 // sweeps of binned_sah_builder.hpp:89-114); the first minimal cost wins (strict <).
+template <bool G>
 __global__ void __launch_bounds__(64) k_small(PrimRec* __restrict__ rec, const SmallItem* __restrict__ small, uint32_t n_small,
                                               RefNode* __restrict__ nodes, RefNode* __restrict__ tnodes,
                                               uint32_t* __restrict__ small_count, uint32_t* __restrict__ prim_out) {
@@ -685,9 +704,9 @@ __global__ void __launch_bounds__(64) k_small(PrimRec* __restrict__ rec, const S
             }
         }
         const LaneBox L = prefix16(v, bi), Rs = suffix16(v, bi);
-        const float rcost = lane_half_area(Rs) * float(Rs.cnt);
+        const float rcost = lane_half_area<G>(Rs) * float(Rs.cnt);
         const float rnext = __shfl_down(rcost, 1, 16);
-        const float cost = lane_half_area(L) * float(L.cnt) + rnext;
+        const float cost = sweep_cost<G>(lane_half_area<G>(L), L.cnt, rnext);
         // first minimal valid cost of this axis (sequential "if (cost < best)" from FLT_MAX)
         const bool valid = bi < 15u && cost < FLT_MAX;
         float bc = valid ? cost : INFINITY;
@@ -705,7 +724,7 @@ __global__ void __launch_bounds__(64) k_small(PrimRec* __restrict__ rec, const S
         if (comp3(bcost[0], bcost[1], bcost[2], axis) > bcost[2]) axis = 2;
         uint32_t split = sel3(bsplit[0], bsplit[1], bsplit[2], axis);
         const float nlo[3] = {e.box[0], e.box[2], e.box[4]}, nhi[3] = {e.box[1], e.box[3], e.box[5]};
-        const float leaf_cost = half_area(nlo, nhi) * (float(m) - 1.0f);
+        const float leaf_cost = half_area_node<G>(nlo, nhi) * (float(m) - 1.0f);
         bool make_leaf = false;
         if (split == uint32_t(kBins) || comp3(bcost[0], bcost[1], bcost[2], axis) >= leaf_cost) {
             if (m <= kMaxLeaf) {
@@ -837,9 +856,11 @@ extern "C" {
 // Device build: d_tri48 = n_tri bvh::Triangle<float> in device memory; d_nodes32 must hold
 // 2 * n_tri - 1 RefNodes, d_prim32 n_tri u32.  Stream-ordered; returns after the build
 // (the node count is read back).  Workspace comes from hipMallocAsync on `stream`.
-int ceres_bvh_build_device(const float* d_tri48, size_t n_tri, uint32_t* d_nodes32, uint32_t* d_prim32,
-                           size_t* n_nodes, void* stream_) {
+int ceres_bvh_build_device_arith(const float* d_tri48, size_t n_tri, uint32_t* d_nodes32, uint32_t* d_prim32,
+                                 size_t* n_nodes, void* stream_, int arith) {
     if (!d_tri48 || !d_nodes32 || !d_prim32 || !n_nodes) return set_error(CERES_EINVAL, "ceres_bvh_build_device: null argument");
+    if (arith != CERES_ARITH_EXACT && arith != CERES_ARITH_FMA) return set_error(CERES_EINVAL, "unknown arithmetic %d", arith);
+    const bool gfma = arith == CERES_ARITH_FMA;
     if (n_tri == 0) return set_error(CERES_EINVAL, "The given scene is empty or cannot be loaded");
     if (n_tri > 0x7fffffffu) return set_error(CERES_EUNSUPPORTED, "more than 2^31 triangles");
     hipStream_t stream = static_cast<hipStream_t>(stream_);
@@ -904,7 +925,8 @@ int ceres_bvh_build_device(const float* d_tri48, size_t n_tri, uint32_t* d_nodes
             Item* it = items[cur];
             hipLaunchKernelGGL(k_item_prep, dim3(n_items), dim3(64), 0, stream, it, n_items, nodes, bins);
             hipLaunchKernelGGL(k_bin, dim3(chunks), dim3(256), 0, stream, rec, seg, n, it, bins);
-            hipLaunchKernelGGL(k_split, dim3((n_items + 63) / 64), dim3(64), 0, stream, it, n_items, nodes, bins);
+            if (gfma) hipLaunchKernelGGL(k_split<true>, dim3((n_items + 63) / 64), dim3(64), 0, stream, it, n_items, nodes, bins);
+            else hipLaunchKernelGGL(k_split<false>, dim3((n_items + 63) / 64), dim3(64), 0, stream, it, n_items, nodes, bins);
             hipLaunchKernelGGL(k_flags, dim3(g256), dim3(256), 0, stream, rec, seg, n, it, flag);
             hipLaunchKernelGGL(k_scan_reduce, dim3(scan_blocks), dim3(256), 0, stream, flag, n, part);
             hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(256), 0, stream, part, scan_blocks);
@@ -924,7 +946,8 @@ int ceres_bvh_build_device(const float* d_tri48, size_t n_tri, uint32_t* d_nodes
         hipLaunchKernelGGL(k_prim_out, dim3(g256), dim3(256), 0, stream, rec, n, d_prim32);
         uint32_t sub_total = 0;
         if (n_small) {                                   // all-large-leaf builds have no subtrees
-            hipLaunchKernelGGL(k_small, dim3(n_small), dim3(64), 0, stream, rec, small, n_small, nodes, tnodes, scount, d_prim32);
+            if (gfma) hipLaunchKernelGGL(k_small<true>, dim3(n_small), dim3(64), 0, stream, rec, small, n_small, nodes, tnodes, scount, d_prim32);
+            else hipLaunchKernelGGL(k_small<false>, dim3(n_small), dim3(64), 0, stream, rec, small, n_small, nodes, tnodes, scount, d_prim32);
             BVH_TRY(hipGetLastError());
             // exclusive scan of the subtree node counts (n_small + 1 entries)
             BVH_TRY(hipMemcpyAsync(part, scount, size_t(n_small) * 4, hipMemcpyDeviceToDevice, stream));
@@ -943,8 +966,13 @@ done:
 
 // Host-buffer convenience with ceres_bvh_build's signature and output: the same BVH as the
 // host builder (canonical topology + leaf order), built on `device`.
-int ceres_bvh_build_gpu(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64,
-                        int device) {
+int ceres_bvh_build_device(const float* d_tri48, size_t n_tri, uint32_t* d_nodes32, uint32_t* d_prim32,
+                           size_t* n_nodes, void* stream_) {
+    return ceres_bvh_build_device_arith(d_tri48, n_tri, d_nodes32, d_prim32, n_nodes, stream_, CERES_ARITH_EXACT);
+}
+
+int ceres_bvh_build_gpu_arith(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64,
+                              int device, int arith) {
     if (!tri48 || !nodes32 || !n_nodes || !prim64) return set_error(CERES_EINVAL, "ceres_bvh_build_gpu: null argument");
     if (n_tri == 0) return set_error(CERES_EINVAL, "The given scene is empty or cannot be loaded");
     if (n_tri > 0x7fffffffu) return set_error(CERES_EUNSUPPORTED, "more than 2^31 triangles");
@@ -963,7 +991,7 @@ int ceres_bvh_build_gpu(const float* tri48, size_t n_tri, uint32_t** nodes32, si
     BVH_TRY(hipMalloc(&d_nodes, cap_nodes * sizeof(RefNode)));
     BVH_TRY(hipMalloc(&d_prim, n_tri * 4));
     BVH_TRY(hipMemcpyAsync(d_tri, tri48, n_tri * 48, hipMemcpyHostToDevice, stream));
-    if ((rc = ceres_bvh_build_device(d_tri, n_tri, d_nodes, d_prim, &m, stream)) != CERES_OK) goto done;
+    if ((rc = ceres_bvh_build_device_arith(d_tri, n_tri, d_nodes, d_prim, &m, stream, arith)) != CERES_OK) goto done;
     *nodes32 = static_cast<uint32_t*>(std::malloc(m * sizeof(RefNode)));
     *prim64 = static_cast<uint64_t*>(std::malloc(n_tri * 8));
     hp = static_cast<uint32_t*>(std::malloc(n_tri * 4));
@@ -981,6 +1009,11 @@ done:
     if (d_prim) (void)hipFree(d_prim);
     if (stream) (void)hipStreamDestroy(stream);
     return rc;
+}
+
+int ceres_bvh_build_gpu(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64,
+                        int device) {
+    return ceres_bvh_build_gpu_arith(tri48, n_tri, nodes32, n_nodes, prim64, device, CERES_ARITH_EXACT);
 }
 
 }  // extern "C"

@@ -205,14 +205,27 @@ __device__ __forceinline__ float fsub(float a, float b) { return x86_nan(a - b, 
 __device__ __forceinline__ float fmul(float a, float b) { return x86_nan(a * b, a, b); }
 __device__ __forceinline__ float fdiv(float a, float b) { return x86_nan(a / b, a, b); }
 
+// fused a*b + c with the same NaN convention (x86 FMA: the first NaN operand, in a, b, c order --
+// the operand order of GCC's vfmadd form is assumed; only NaN/inf OBJ coordinates can reach it)
+__device__ __forceinline__ float ffma(float a, float b, float c) {
+    const float r = fmaf(a, b, c);
+    if (r == r) return r;
+    if (a != a) return __uint_as_float(__float_as_uint(a) | 0x00400000u);
+    return x86_nan(r, b, c);
+}
+
 struct F3 { float x, y, z; };
 __device__ __forceinline__ F3 sub(F3 a, F3 b) { return {fsub(a.x, b.x), fsub(a.y, b.y), fsub(a.z, b.z)}; }
+// cross (vector.hpp:159-167); G: the reference CMake build's contraction fma(a_j, b_k, -(a_k b_j))
+template <bool G>
 __device__ __forceinline__ F3 cross(F3 a, F3 b) {
+    if (G) return {ffma(a.y, b.z, -fmul(a.z, b.y)), ffma(a.z, b.x, -fmul(a.x, b.z)), ffma(a.x, b.y, -fmul(a.y, b.x))};
     return {fsub(fmul(a.y, b.z), fmul(a.z, b.y)), fsub(fmul(a.z, b.x), fmul(a.x, b.z)), fsub(fmul(a.x, b.y), fmul(a.y, b.x))};
 }
 __device__ __forceinline__ F3 load3(const float* p) { return {p[0], p[1], p[2]}; }
 
 // Triangle(p0, p1, p2) (triangle.hpp:30-34); corner values for the normal sort
+template <bool G>
 __global__ void __launch_bounds__(256) k_tris(const float* __restrict__ verts, const uint32_t* __restrict__ corners, uint32_t n_tri,
                                               Tri48* __restrict__ tris, uint32_t* __restrict__ cidx,
                                               uint32_t* __restrict__ vcount) {
@@ -220,13 +233,15 @@ __global__ void __launch_bounds__(256) k_tris(const float* __restrict__ verts, c
     if (t >= n_tri) return;
     const uint32_t a = corners[3 * size_t(t)], b = corners[3 * size_t(t) + 1], c = corners[3 * size_t(t) + 2];
     const F3 p0 = load3(verts + 3 * size_t(a)), p1 = load3(verts + 3 * size_t(b)), p2 = load3(verts + 3 * size_t(c));
-    const F3 e1 = sub(p0, p1), e2 = sub(p2, p0), n = cross(e1, e2);
+    const F3 e1 = sub(p0, p1), e2 = sub(p2, p0), n = cross<G>(e1, e2);
     tris[t] = Tri48{{p0.x, p0.y, p0.z}, {e1.x, e1.y, e1.z}, {e2.x, e2.y, e2.z}, {n.x, n.y, n.z}};
     for (int k = 0; k < 3; ++k) { cidx[3 * size_t(t) + k] = 3 * t + k; }
     atomicAdd(&vcount[a], 1u); atomicAdd(&vcount[b], 1u); atomicAdd(&vcount[c], 1u);
 }
 
-// normals[v] += n in face order, then normalize (obj_norms.hpp:91-94, 109-111)
+// normals[v] += n in face order, then normalize (obj_norms.hpp:91-94, 109-111); G: the dot of
+// normalize contracted as fma(z, z, fma(x, x, y y))
+template <bool G>
 __global__ void __launch_bounds__(256) k_vnorm(const uint32_t* __restrict__ vstart, const uint32_t* __restrict__ sorted_c,
                                                const Tri48* __restrict__ tris, uint32_t nverts, float* __restrict__ vnorm) {
     const uint32_t v = blockIdx.x * 256u + threadIdx.x;
@@ -236,9 +251,14 @@ __global__ void __launch_bounds__(256) k_vnorm(const uint32_t* __restrict__ vsta
         const Tri48& t = tris[sorted_c[i] / 3u];
         x = fadd(x, t.n[0]); y = fadd(y, t.n[1]); z = fadd(z, t.n[2]);
     }
-    float s = fmul(x, x);
-    s = fadd(s, fmul(y, y));
-    s = fadd(s, fmul(z, z));
+    float s;
+    if (G) {
+        s = ffma(z, z, ffma(x, x, fmul(y, y)));
+    } else {
+        s = fmul(x, x);
+        s = fadd(s, fmul(y, y));
+        s = fadd(s, fmul(z, z));
+    }
     const float r = sqrtf(s);                              // sqrt of a NaN propagates; s >= 0 otherwise
     const float inv = fdiv(1.0f, x86_nan(r, s, s));
     vnorm[3 * size_t(v)] = fmul(x, inv); vnorm[3 * size_t(v) + 1] = fmul(y, inv); vnorm[3 * size_t(v) + 2] = fmul(z, inv);
@@ -254,7 +274,9 @@ __global__ void __launch_bounds__(256) k_trinorm(const uint32_t* __restrict__ co
     }
 }
 
-// rotate_triangles<Axis> (render.hpp:24-44): rebuild each Triangle from rotated p0, p1(), p2()
+// rotate_triangles<Axis> (render.hpp:24-44): rebuild each Triangle from rotated p0, p1(), p2();
+// G: each rotated coordinate's first product fused (p1 c - p2 s -> fma(p1, c, -(p2 s)), ...)
+template <bool G>
 __global__ void __launch_bounds__(256) k_rotate(Tri48* __restrict__ tris, uint32_t n_tri, int axis, float c, float s) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n_tri) return;
@@ -264,11 +286,15 @@ __global__ void __launch_bounds__(256) k_rotate(Tri48* __restrict__ tris, uint32
     F3 r[3];
     for (int k = 0; k < 3; ++k) {
         const F3 p = q[k];
-        if (axis == 0) r[k] = {p.x, fsub(fmul(p.y, c), fmul(p.z, s)), fadd(fmul(p.y, s), fmul(p.z, c))};
-        else if (axis == 1) r[k] = {fadd(fmul(p.x, c), fmul(p.z, s)), p.y, fadd(fmul(-p.x, s), fmul(p.z, c))};
-        else r[k] = {fsub(fmul(p.x, c), fmul(p.y, s)), fadd(fmul(p.x, s), fmul(p.y, c)), p.z};
+        auto mad = [&](float a, float b, float x, float y, bool minus) {   // a*b -/+ x*y
+            if (G) return ffma(a, b, minus ? -fmul(x, y) : fmul(x, y));
+            return minus ? fsub(fmul(a, b), fmul(x, y)) : fadd(fmul(a, b), fmul(x, y));
+        };
+        if (axis == 0) r[k] = {p.x, mad(p.y, c, p.z, s, true), mad(p.y, s, p.z, c, false)};
+        else if (axis == 1) r[k] = {mad(p.x, c, p.z, s, false), p.y, mad(-p.x, s, p.z, c, false)};
+        else r[k] = {mad(p.x, c, p.y, s, true), mad(p.x, s, p.y, c, false), p.z};
     }
-    const F3 ne1 = sub(r[0], r[1]), ne2 = sub(r[2], r[0]), n = cross(ne1, ne2);
+    const F3 ne1 = sub(r[0], r[1]), ne2 = sub(r[2], r[0]), n = cross<G>(ne1, ne2);
     tris[i] = Tri48{{r[0].x, r[0].y, r[0].z}, {ne1.x, ne1.y, ne1.z}, {ne2.x, ne2.y, ne2.z}, {n.x, n.y, n.z}};
 }
 
@@ -299,25 +325,35 @@ void ceres_device_free(void* d_ptr) {
     if (d_ptr) (void)hipFree(d_ptr);
 }
 
-int ceres_rotate_triangles_device(float* d_tri48, size_t n_tri, int axis, float degrees, void* stream) {
+int ceres_rotate_triangles_device_arith(float* d_tri48, size_t n_tri, int axis, float degrees, void* stream, int arith) {
     if ((!d_tri48 && n_tri) || axis < 0 || axis > 2) return set_error(CERES_EINVAL, "ceres_rotate_triangles_device: bad argument");
+    if (arith != CERES_ARITH_EXACT && arith != CERES_ARITH_FMA) return set_error(CERES_EINVAL, "unknown arithmetic %d", arith);
     if (n_tri > 0xffffffffu) return set_error(CERES_EUNSUPPORTED, "too many triangles");
     if (!n_tri) return CERES_OK;
     // the angle's cos/sin on the host, as the reference evaluates them (render.hpp:27-28)
     const float pi = float(3.14159265359);
     const float c = std::cos(degrees * pi / float(180));
     const float s = std::sin(degrees * pi / float(180));
-    hipLaunchKernelGGL(k_rotate, dim3((n_tri + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
-                       reinterpret_cast<Tri48*>(d_tri48), uint32_t(n_tri), axis, c, s);
+    if (arith == CERES_ARITH_FMA)
+        hipLaunchKernelGGL(k_rotate<true>, dim3((n_tri + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                           reinterpret_cast<Tri48*>(d_tri48), uint32_t(n_tri), axis, c, s);
+    else
+        hipLaunchKernelGGL(k_rotate<false>, dim3((n_tri + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                           reinterpret_cast<Tri48*>(d_tri48), uint32_t(n_tri), axis, c, s);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? CERES_OK : set_error(CERES_EHIP, "k_rotate: %s", hipGetErrorString(e));
 }
 
+int ceres_rotate_triangles_device(float* d_tri48, size_t n_tri, int axis, float degrees, void* stream) {
+    return ceres_rotate_triangles_device_arith(d_tri48, n_tri, axis, degrees, stream, CERES_ARITH_EXACT);
+}
+
 // obj::load_from_stream on device text [d_text, d_text + len).  Outputs are hipMalloc'd device
 // arrays (free with ceres_device_free); an empty mesh returns n_tri = 0 and NULL arrays.
-int ceres_obj_parse_device(const char* d_text, size_t len, float** d_tri48, float** d_norm36, size_t* n_tri,
-                           void* stream_) {
+int ceres_obj_parse_device_arith(const char* d_text, size_t len, float** d_tri48, float** d_norm36, size_t* n_tri,
+                                 void* stream_, int arith) {
     if ((!d_text && len) || !d_tri48 || !d_norm36 || !n_tri) return set_error(CERES_EINVAL, "ceres_obj_parse_device: null argument");
+    if (arith != CERES_ARITH_EXACT && arith != CERES_ARITH_FMA) return set_error(CERES_EINVAL, "unknown arithmetic %d", arith);
     *d_tri48 = *d_norm36 = nullptr;
     *n_tri = 0;
     if (len >= 0xffffffffu) return set_error(CERES_EUNSUPPORTED, "OBJ text of 4 GiB or more");
@@ -393,7 +429,10 @@ int ceres_obj_parse_device(const char* d_text, size_t len, float** d_tri48, floa
         OBJ_TRY(dalloc(&vcount, nverts, stream));
         OBJ_TRY(dalloc(&vstart, nverts + 1, stream));
         OBJ_TRY(hipMemsetAsync(vcount, 0, 4 * size_t(nverts), stream));
-        hipLaunchKernelGGL(k_tris, dim3((ntris + 255) / 256), dim3(256), 0, stream, verts, corners, ntris, tris, cidx, vcount);
+        if (arith == CERES_ARITH_FMA)
+            hipLaunchKernelGGL(k_tris<true>, dim3((ntris + 255) / 256), dim3(256), 0, stream, verts, corners, ntris, tris, cidx, vcount);
+        else
+            hipLaunchKernelGGL(k_tris<false>, dim3((ntris + 255) / 256), dim3(256), 0, stream, verts, corners, ntris, tris, cidx, vcount);
         OBJ_TRY(hipGetLastError());
         // stable sort of the corners by vertex: each vertex's corners stay in face order
         ckey = corners;
@@ -410,7 +449,10 @@ int ceres_obj_parse_device(const char* d_text, size_t len, float** d_tri48, floa
         OBJ_TRY(dalloc(&part, scan_blocks(std::max(nverts, 1u)) + 2, stream));
         OBJ_TRY(exclusive_scan(vcount, nverts, vstart, part, stream));
         OBJ_TRY(dalloc(&vnorm, 3 * size_t(nverts), stream));
-        hipLaunchKernelGGL(k_vnorm, dim3((nverts + 255) / 256), dim3(256), 0, stream, vstart, sval, tris, nverts, vnorm);
+        if (arith == CERES_ARITH_FMA)
+            hipLaunchKernelGGL(k_vnorm<true>, dim3((nverts + 255) / 256), dim3(256), 0, stream, vstart, sval, tris, nverts, vnorm);
+        else
+            hipLaunchKernelGGL(k_vnorm<false>, dim3((nverts + 255) / 256), dim3(256), 0, stream, vstart, sval, tris, nverts, vnorm);
         hipLaunchKernelGGL(k_trinorm, dim3((ntris + 255) / 256), dim3(256), 0, stream, corners, vnorm, ntris, norm36);
         OBJ_TRY(hipGetLastError());
         OBJ_TRY(hipStreamSynchronize(stream));
@@ -431,9 +473,14 @@ done:
     return rc;
 }
 
+int ceres_obj_parse_device(const char* d_text, size_t len, float** d_tri48, float** d_norm36, size_t* n_tri,
+                           void* stream_) {
+    return ceres_obj_parse_device_arith(d_text, len, d_tri48, d_norm36, n_tri, stream_, CERES_ARITH_EXACT);
+}
+
 // Host-buffer form with ceres_obj_load's contract: the file is read on the host, parsed on
 // HIP `device`, and the arrays come back malloc'd (free with ceres_free).
-int ceres_obj_load_gpu(const char* path, float** tri48, float** norm36, size_t* n_tri, int device) {
+int ceres_obj_load_gpu_arith(const char* path, float** tri48, float** norm36, size_t* n_tri, int device, int arith) {
     if (!path || !tri48 || !norm36 || !n_tri) return set_error(CERES_EINVAL, "ceres_obj_load_gpu: null argument");
     *tri48 = *norm36 = nullptr;
     *n_tri = 0;
@@ -459,7 +506,7 @@ int ceres_obj_load_gpu(const char* path, float** tri48, float** norm36, size_t* 
     OBJ_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     OBJ_TRY(hipMalloc(&d_text, len));
     OBJ_TRY(hipMemcpyAsync(d_text, h_text, len, hipMemcpyHostToDevice, stream));
-    if ((rc = ceres_obj_parse_device(d_text, len, &d_tri, &d_norm, &n, stream)) != CERES_OK) goto done;
+    if ((rc = ceres_obj_parse_device_arith(d_text, len, &d_tri, &d_norm, &n, stream, arith)) != CERES_OK) goto done;
     if (n) {
         *tri48 = static_cast<float*>(std::malloc(n * 48));
         *norm36 = static_cast<float*>(std::malloc(n * 36));
@@ -478,6 +525,10 @@ done:
     if (h_text) (void)hipHostFree(h_text);
     if (stream) (void)hipStreamDestroy(stream);
     return rc;
+}
+
+int ceres_obj_load_gpu(const char* path, float** tri48, float** norm36, size_t* n_tri, int device) {
+    return ceres_obj_load_gpu_arith(path, tri48, norm36, n_tri, device, CERES_ARITH_EXACT);
 }
 
 }  // extern "C"

@@ -145,11 +145,7 @@ template <> struct Api<float> {
     static int proc(int k, float** t, float** n, size_t* c, int ar) { return ceres_proc_mesh_arith(k, t, n, c, ar); }
     static int rotate(float* t, size_t c, int ax, float deg, int ar) { return ceres_rotate_triangles_arith(t, c, ax, deg, ar); }
     static int bvh(const float* t, size_t c, Node** nodes, size_t* m, uint64_t** prim, bool gpu, int dev, int ar) {
-        if (gpu && ar != CERES_ARITH_EXACT) {
-            std::fprintf(stderr, "error: --gpu-bvh builds the contraction-free BVH only: add --exact\n");
-            return CERES_EUNSUPPORTED;
-        }
-        return gpu ? ceres_bvh_build_gpu(t, c, nodes, m, prim, dev) : ceres_bvh_build_arith(t, c, nodes, m, prim, ar);
+        return gpu ? ceres_bvh_build_gpu_arith(t, c, nodes, m, prim, dev, ar) : ceres_bvh_build_arith(t, c, nodes, m, prim, ar);
     }
     static ceres_scene* scene(const float* t, size_t c, const float* n, const Node* nodes, size_t m, const uint64_t* prim, int dev) {
         return ceres_scene_create(t, c, n, nodes, m, prim, dev, 0);

@@ -133,6 +133,17 @@ int ceres_obj_parse_device(const char* d_text, size_t len, float** d_tri48, floa
 /* rotate_triangles<Axis> on device triangles (cos/sin of the angle taken on the host). */
 int ceres_rotate_triangles_device(float* d_tri48, size_t n_tri, int axis, float degrees, void* stream);
 void ceres_device_free(void* d_ptr);
+/* The GPU scene preparation above in a chosen arithmetic (CERES_ARITH_EXACT = the calls above,
+ * CERES_ARITH_FMA = the reference's CMake build: contracted triangle normals, vertex-normal
+ * normalisation, rotation and SAH costs; bit-identical to the *_arith host calls below). */
+int ceres_bvh_build_gpu_arith(const float* tri48, size_t n_tri, uint32_t** nodes32, size_t* n_nodes, uint64_t** prim64,
+                              int device, int arith);
+int ceres_bvh_build_device_arith(const float* d_tri48, size_t n_tri, uint32_t* d_nodes32, uint32_t* d_prim32,
+                                 size_t* n_nodes, void* stream, int arith);
+int ceres_obj_load_gpu_arith(const char* path, float** tri48, float** norm36, size_t* n_tri, int device, int arith);
+int ceres_obj_parse_device_arith(const char* d_text, size_t len, float** d_tri48, float** d_norm36, size_t* n_tri,
+                                 void* stream, int arith);
+int ceres_rotate_triangles_device_arith(float* d_tri48, size_t n_tri, int axis, float degrees, void* stream, int arith);
 /* Camera basis of render.hpp:91-97: out = {dir[3], image_u*w[3], image_v*w*ratio[3]}. */
 int ceres_camera_basis(const float eye[3], const float dir[3], const float up[3], float fov_deg,
                        size_t width, size_t height, float out9[9]);

@@ -12,7 +12,7 @@ import time
 import numpy as np
 import pytest
 
-from conftest import golden_names, load_golden
+from conftest import golden_names, load_golden, ref_scene_hashes
 
 import configs
 
@@ -32,10 +32,10 @@ def canon(bvh):
     return oracle.canonical_bvh_sha(bvh.nodes, bvh.prim)
 
 
-def _mesh(pkg, cfg):
-    mesh = pkg.proc_mesh(cfg["proc"]) if cfg.get("proc") else pkg.load_obj(configs.obj_path(cfg))
+def _mesh(pkg, cfg, arith=0):
+    mesh = pkg.proc_mesh(cfg["proc"], arith) if cfg.get("proc") else pkg.load_obj(configs.obj_path(cfg), arith)
     if cfg.get("rotate"):
-        pkg.rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1])
+        pkg.rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1], arith)
     return mesh
 
 
@@ -47,14 +47,17 @@ for _n in golden_names():
 MESH_CONFIGS = sorted(_MESHES.values())
 
 
+@pytest.mark.parametrize("arith", [0, 1], ids=["exact", "fma"])
 @pytest.mark.parametrize("name", MESH_CONFIGS)
-def test_gpu_bvh_matches_reference_fixture(gpu, name):
+def test_gpu_bvh_matches_reference_fixture(gpu, name, arith):
+    """Both reference builds: the contraction-free one and the CMake-flag one, whose SAH costs
+    (binned_sah_builder.hpp:98,109,179) contract into FMA -- the FMA flavour of the GPU builder."""
     pkg = gpu
     meta, _, _ = load_golden(name)
-    mesh = _mesh(pkg, configs.CONFIGS[name])
-    bvh = pkg.build_bvh_gpu(mesh)
-    assert bvh.nodes.shape[0] == meta["n_nodes"]
-    assert canon(bvh) == meta["bvh_canonical_sha256"]
+    mesh = _mesh(pkg, configs.CONFIGS[name], arith)
+    bvh = pkg.build_bvh_gpu(mesh, arith=arith)
+    assert bvh.nodes.shape[0] == meta["ref_n_nodes" if arith else "n_nodes"]
+    assert canon(bvh) == ref_scene_hashes(meta, arith)[2]
     assert sorted(bvh.prim.tolist()) == list(range(len(mesh)))
 
 
@@ -92,11 +95,12 @@ def test_gpu_bvh_matches_host_builder(gpu, kind, n):
     rng = np.random.default_rng(1234 + n)
     tri = _soup(rng, n, kind)
     mesh = pkg.Mesh(tri, np.zeros((n, 9), np.float32))
-    host = pkg.build_bvh(mesh)
-    dev = pkg.build_bvh_gpu(mesh)
-    assert dev.nodes.shape == host.nodes.shape
-    assert np.array_equal(dev.prim, host.prim)          # primitive_indices: same permutation, same order
-    assert canon(dev) == canon(host)
+    for arith in (0, 1):
+        host = pkg.build_bvh(mesh, arith=arith)
+        dev = pkg.build_bvh_gpu(mesh, arith=arith)
+        assert dev.nodes.shape == host.nodes.shape, arith
+        assert np.array_equal(dev.prim, host.prim), arith    # primitive_indices: same permutation, same order
+        assert canon(dev) == canon(host), arith
 
 
 def test_render_over_gpu_bvh_matches_reference(gpu):
@@ -115,30 +119,31 @@ def test_render_over_gpu_bvh_matches_reference(gpu):
     scene.close()
 
 
-def test_gpu_bvh_c5_matches_reference_and_is_faster(gpu):
+@pytest.mark.parametrize("arith", [0, 1], ids=["exact", "fma"])
+def test_gpu_bvh_c5_matches_reference_and_is_faster(gpu, arith):
     """C5 (9,999,392 triangles): canonical topology equal to the reference's; timing reported."""
     import torch
     pkg = gpu
     meta, _, _ = load_golden("proc_c5")
-    mesh = _mesh(pkg, configs.CONFIGS["proc_c5"])
+    mesh = _mesh(pkg, configs.CONFIGS["proc_c5"], arith)
     n = len(mesh)
     d_tri = torch.from_numpy(mesh.tri.reshape(-1)).to("cuda:0")
     d_nodes = torch.empty((2 * n - 1) * 8, dtype=torch.int32, device="cuda:0")
     d_prim = torch.empty(n, dtype=torch.int32, device="cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
-    pkg.build_bvh_device(d_tri.data_ptr(), n, d_nodes.data_ptr(), d_prim.data_ptr(), stream)   # warm-up
+    pkg.build_bvh_device(d_tri.data_ptr(), n, d_nodes.data_ptr(), d_prim.data_ptr(), stream, arith)   # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    m = pkg.build_bvh_device(d_tri.data_ptr(), n, d_nodes.data_ptr(), d_prim.data_ptr(), stream)
+    m = pkg.build_bvh_device(d_tri.data_ptr(), n, d_nodes.data_ptr(), d_prim.data_ptr(), stream, arith)
     torch.cuda.synchronize()
     gpu_ms = (time.perf_counter() - t0) * 1e3
     nodes = d_nodes[: m * 8].cpu().numpy().view(np.uint32).reshape(-1, 8)
     prim = d_prim.cpu().numpy().view(np.uint32).astype(np.uint64)
-    assert m == meta["n_nodes"]
+    assert m == meta["ref_n_nodes" if arith else "n_nodes"]
     import oracle
-    assert oracle.canonical_bvh_sha(nodes, prim) == meta["bvh_canonical_sha256"]
+    assert oracle.canonical_bvh_sha(nodes, prim) == ref_scene_hashes(meta, arith)[2]
     t0 = time.perf_counter()
-    pkg.build_bvh(mesh)
+    pkg.build_bvh(mesh, arith=arith)
     host_ms = (time.perf_counter() - t0) * 1e3
     print(f"C5 BVH build: gpu {gpu_ms:.1f} ms, host {host_ms:.1f} ms ({n} triangles, {m} nodes)")
     assert gpu_ms < host_ms

@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import REPO, golden_names, load_golden
+from conftest import ref_scene_hashes, REPO, golden_names, load_golden
 
 import configs
 
@@ -36,29 +36,33 @@ def same(a, b):
 OBJ_CONFIGS = sorted({configs.CONFIGS[n]["obj"]: n for n in golden_names() if configs.CONFIGS[n]["obj"]}.values())
 
 
+@pytest.mark.parametrize("arith", [0, 1], ids=["exact", "fma"])
 @pytest.mark.parametrize("name", OBJ_CONFIGS)
-def test_gpu_obj_matches_reference_fixture(gpu, name):
-    """GPU parse + GPU rotation == the reference's loaded and rotated scene (fixture hashes)."""
+def test_gpu_obj_matches_reference_fixture(gpu, name, arith):
+    """GPU parse + GPU rotation == the reference's loaded and rotated scene (fixture hashes), in
+    both builds' arithmetic (the CMake-flag build contracts the triangle normals, the vertex-normal
+    normalisation and the rotation)."""
     import torch
     pkg = gpu
     cfg = configs.CONFIGS[name]
     meta, _, _ = load_golden(name)
     path = configs.obj_path(cfg)
-    host = pkg.load_obj(path)
-    dev = pkg.load_obj_gpu(path)
+    host = pkg.load_obj(path, arith)
+    dev = pkg.load_obj_gpu(path, arith=arith)
     assert same(dev, host)
     # rotate on the device (torch-owned HBM), compare with the reference's rotated triangles
     d_tri = torch.from_numpy(dev.tri.reshape(-1).copy()).to("cuda:0")
     if cfg.get("rotate"):
         pkg.rotate_triangles_device(d_tri.data_ptr(), len(dev), cfg["rotate"][0], cfg["rotate"][1],
-                                    torch.cuda.current_stream().cuda_stream)
+                                    torch.cuda.current_stream().cuda_stream, arith)
     torch.cuda.synchronize()
     tri = d_tri.cpu().numpy()
     norm = dev.norm
     n = len(dev)
     assert n == meta["n_tri"]
-    assert hashlib.sha256(tri.tobytes()).hexdigest() == meta["tri48_sha256"]
-    assert hashlib.sha256(norm.tobytes()).hexdigest() == meta["norm36_sha256"]
+    tri_h, norm_h, _ = ref_scene_hashes(meta, arith)
+    assert hashlib.sha256(tri.tobytes()).hexdigest() == tri_h
+    assert hashlib.sha256(norm.tobytes()).hexdigest() == norm_h
 
 
 def _num(rng):

@@ -31,22 +31,22 @@ def _hexf(hx):
     return np.asarray([int(h, 16) for h in hx], np.uint32).view(np.float32)
 
 
-def basis_of(meta, cfg):
-    eye = _hexf(meta["pose"]["eye"]) if "pose" in meta else np.asarray(cfg["eye"], np.float32)
-    return np.concatenate([eye, _hexf(meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"])])
+def basis_of(meta, cfg, build="exact"):
+    pose, basis = (meta["ref_pose"], meta["ref_basis"]) if build == "ref" else (meta["pose"], meta["basis"])
+    return np.concatenate([_hexf(pose["eye"]), _hexf(basis["dir"] + basis["u"] + basis["v"])])
 
 
-def sun_of(meta, cfg):
-    return _hexf(meta["pose"]["sun"]) if "pose" in meta else np.asarray(cfg["sun"], np.float32)
+def sun_of(meta, cfg, build="exact"):
+    return _hexf((meta["ref_pose"] if build == "ref" else meta["pose"])["sun"])
 
 
-def device_scene(pkg, d_tri, n, d_norm):
+def device_scene(pkg, d_tri, n, d_norm, arith=0):
     """GPU BVH + GPU relayout over device triangles/normals (int pointers)."""
     import torch
     d_nodes = torch.empty((2 * n - 1) * 8 if n > 1 else 8, dtype=torch.int32, device="cuda:0")
     d_prim = torch.empty(n, dtype=torch.int32, device="cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
-    m = pkg.build_bvh_device(d_tri, n, d_nodes.data_ptr(), d_prim.data_ptr(), stream)
+    m = pkg.build_bvh_device(d_tri, n, d_nodes.data_ptr(), d_prim.data_ptr(), stream, arith)
     scene = pkg.Scene.from_device(d_tri, n, d_norm, d_nodes.data_ptr(), m, d_prim.data_ptr(), stream=stream)
     return scene, m
 
@@ -79,35 +79,42 @@ def test_device_scene_renders_reference_frame(gpu, name):
         host_scene.close()
 
 
-def test_obj_text_to_frame_on_device(gpu):
-    """dragon.obj text in HBM -> parse -> rotate -> BVH -> scene -> C3 frame, all on the GPU."""
+@pytest.mark.parametrize("build", ["ref", "exact"])
+def test_obj_text_to_frame_on_device(gpu, build):
+    """dragon.obj text in HBM -> parse -> rotate -> BVH -> scene -> C3 frame, all on the GPU; in the
+    reference CMake build's arithmetic (build "ref": CERES_ARITH_FMA + CERES_MODE_FMA) and the
+    contraction-free one."""
     import torch
     pkg = gpu
     name = "dragon_1080"
     cfg = configs.CONFIGS[name]
     meta, _, _ = load_golden(name)
+    arith = 1 if build == "ref" else 0
     text = open(configs.obj_path(cfg), "rb").read()
     d_text = torch.frombuffer(bytearray(text), dtype=torch.uint8).to("cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
-    d_tri, d_norm, n = pkg.parse_obj_device(d_text.data_ptr(), len(text), stream)
+    d_tri, d_norm, n = pkg.parse_obj_device(d_text.data_ptr(), len(text), stream, arith)
     try:
-        pkg.rotate_triangles_device(d_tri, n, cfg["rotate"][0], cfg["rotate"][1], stream)
-        scene, _ = device_scene(pkg, d_tri, n, d_norm)
-        _, rgb, st = scene.render(basis_of(meta, cfg), sun_of(meta, cfg), cfg["W"], cfg["H"], want_pixels=False)
+        pkg.rotate_triangles_device(d_tri, n, cfg["rotate"][0], cfg["rotate"][1], stream, arith)
+        scene, _ = device_scene(pkg, d_tri, n, d_norm, arith)
+        _, rgb, st = scene.render(basis_of(meta, cfg, build), sun_of(meta, cfg, build), cfg["W"], cfg["H"],
+                                  mode=pkg.cfg_mode(cfg, arith), want_pixels=False)
         scene.close()
     finally:
         pkg.device_free(d_tri)
         pkg.device_free(d_norm)
     assert n == meta["n_tri"]
-    assert (st["rays"], st["hits"]) == (meta["exact"]["rays"], meta["exact"]["hits"])
-    assert hashlib.sha256(pkg.ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
+    assert (st["rays"], st["hits"]) == (meta[build]["rays"], meta[build]["hits"])
+    assert hashlib.sha256(pkg.ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"][build]
 
 
-def test_c5_obj_text_to_frame_on_device(gpu):
+@pytest.mark.parametrize("build", ["ref", "exact"])
+def test_c5_obj_text_to_frame_on_device(gpu, build):
     """C5: the 10M-triangle heightfield as OBJ text -> device pipeline -> the reference's 4K frame."""
     import torch
     pkg = gpu
     name = "proc_c5"
+    arith = 1 if build == "ref" else 0
     cfg = configs.CONFIGS[name]
     meta, _, _ = load_golden(name)
     with tempfile.TemporaryDirectory() as td:
@@ -117,18 +124,19 @@ def test_c5_obj_text_to_frame_on_device(gpu):
     d_text = torch.frombuffer(bytearray(text), dtype=torch.uint8).to("cuda:0")
     del text
     stream = torch.cuda.current_stream().cuda_stream
-    d_tri, d_norm, n = pkg.parse_obj_device(d_text.data_ptr(), d_text.numel(), stream)
+    d_tri, d_norm, n = pkg.parse_obj_device(d_text.data_ptr(), d_text.numel(), stream, arith)
     del d_text
     try:
-        scene, m = device_scene(pkg, d_tri, n, d_norm)
-        _, rgb, st = scene.render(basis_of(meta, cfg), sun_of(meta, cfg), cfg["W"], cfg["H"], want_pixels=False)
+        scene, m = device_scene(pkg, d_tri, n, d_norm, arith)
+        _, rgb, st = scene.render(basis_of(meta, cfg, build), sun_of(meta, cfg, build), cfg["W"], cfg["H"],
+                                  mode=pkg.cfg_mode(cfg, arith), want_pixels=False)
         scene.close()
     finally:
         pkg.device_free(d_tri)
         pkg.device_free(d_norm)
-    assert (n, m) == (meta["n_tri"], meta["n_nodes"])
-    assert (st["rays"], st["hits"]) == (meta["exact"]["rays"], meta["exact"]["hits"])
-    assert hashlib.sha256(pkg.ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
+    assert (n, m) == (meta["n_tri"], meta["ref_n_nodes" if arith else "n_nodes"])
+    assert (st["rays"], st["hits"]) == (meta[build]["rays"], meta[build]["hits"])
+    assert hashlib.sha256(pkg.ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"][build]
 
 
 def test_device_scene_rejects_malformed_bvh(gpu):

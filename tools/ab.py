@@ -3,7 +3,8 @@
 
 usage: python tools/ab.py [config] [rounds] [lib.so[@qbvh][#tag] ...]
 Each argument is a build of libceres_hip.so (default: the in-tree one), e.g. one made with
-`make -C ceres-raytracer_amd/csrc variant VARIANT=x DEFS=-DFOO`.  Every build is loaded as its
+`make -C ceres-raytracer_amd/csrc variant VARIANT=x DEFS=-DFOO`.  AB_ARITH=fma|exact (default fma,
+bench.py's default): the reference CMake build's arithmetic or the contraction-free one.  Every build is loaded as its
 own module instance (own ctypes handle, own HIP code object) and renders the config
 alternately; prints device ms per frame (HIP events), median and min, and PPM parity.
 """
@@ -47,15 +48,18 @@ def main():
     qflag = {k: (m.MODE_QBVH4 if "@qbvh" in k else 0) for k, m in builds.items()}
     first = next(iter(builds.values()))
     cfg = first.configs.CONFIGS[name]
-    mesh, bvh, cam = first.prepare(cfg)
-    bits = [int(h, 16) for h in meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]]
+    build = "ref" if os.environ.get("AB_ARITH", "fma") == "fma" else "exact"
+    arith = 1 if build == "ref" else 0
+    mesh, bvh, cam = first.prepare(cfg, arith=arith)
+    bb = meta["ref_basis"] if build == "ref" else meta["basis"]
+    bits = [int(h, 16) for h in bb["dir"] + bb["u"] + bb["v"]]
     basis = np.concatenate([np.asarray(cfg["eye"], np.float32), np.asarray(bits, np.uint32).view(np.float32)])
-    mode0 = first.cfg_mode(cfg)
+    mode0 = first.cfg_mode(cfg, arith)
     scenes = {k: m.Scene(mesh, bvh) for k, m in builds.items()}
     ok = {}
     for k, sc in scenes.items():
         _, rgb, st = sc.render(basis, cfg["sun"], cfg["W"], cfg["H"], mode=mode0 | qflag[k], want_pixels=False)
-        ok[k] = hashlib.sha256(builds[k].ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"]["exact"]
+        ok[k] = hashlib.sha256(builds[k].ppm(cfg["W"], cfg["H"], rgb)).hexdigest() == meta["ppm_sha256"][build]
     want_px = os.environ.get("AB_FLOAT", "1") == "1"
     res = {k: [] for k in scenes}
     n_streams = int(os.environ.get("AB_STREAMS", "0"))
@@ -96,9 +100,9 @@ def main():
                                  want_rgb8=True)
             res[k].append(st["ms"])
     out = {k: {"median_ms": round(float(np.median(r)), 4), "min_ms": round(float(np.min(r)), 4),
-               "mrays_s_median": round(meta["exact"]["rays"] / (np.median(r) * 1e3), 1), "parity": ok[k]}
+               "mrays_s_median": round(meta[build]["rays"] / (np.median(r) * 1e3), 1), "parity": ok[k]}
            for k, r in res.items()}
-    print(json.dumps({"config": name, "rounds": rounds, "streams": n_streams, "results": out}))
+    print(json.dumps({"config": name, "arith": build, "rounds": rounds, "streams": n_streams, "results": out}))
 
 
 if __name__ == "__main__":
