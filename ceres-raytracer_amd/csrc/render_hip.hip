@@ -79,6 +79,13 @@
 #ifndef CERES_LOCAL_CHUNK_SOLO
 #define CERES_LOCAL_CHUNK_SOLO 16              // ... and single large frames of a DRAM-resident scene
 #endif
+#ifndef CERES_RCP_UNIFORM
+#define CERES_RCP_UNIFORM 2                    // rcp_exact's IEEE-division fallback behind a wave-uniform branch
+#endif                                         // (ballot) instead of a divergent one: 0 nowhere, 1 in every
+                                               // kernel, 2 in the single-frame kernel only
+#ifndef CERES_TRI_SELECT
+#define CERES_TRI_SELECT 1                     // triangle test without control flow (t always computed, one
+#endif                                         // predicate) and closest-hit updates as selects
 
 namespace ceres {
 
@@ -174,8 +181,20 @@ __device__ __forceinline__ TriV load_tri_u(const Tri48* tris, uint32_t idx) {
 // exhaustively over all 2^32 inputs on gfx950 (tools/probes/rcp_exhaustive.hip,
 // tests/test_gpu_parity.py::test_fast_reciprocal_is_exact).  Zero, denormal, huge, inf and NaN
 // inputs take the full v_div_scale/fmas/fixup division.
+// kU: the division fallback behind a wave-uniform branch (the estimate and the Newton step run in
+// every lane; only a wavefront with an out-of-range input pays the division) -- used where
+// CERES_RCP_UNIFORM selects it (2: the single-frame kernel, where it measured -1..-2 %; in the
+// multi-frame kernel it measured neutral alone and +12 % together with CERES_TRI_SELECT)
+template <bool kU = false>
 __device__ __forceinline__ float rcp_exact(float x) {
     const uint32_t m = __float_as_uint(x) & 0x7fffffffu;
+    if (kU) {
+        const bool slow = m - 0x00800000u >= 0x7e000000u - 0x00800000u;
+        const float r0 = __builtin_amdgcn_rcpf(x);
+        const float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+        if (__builtin_expect(__ballot(slow) != 0, 0)) return slow ? 1.0f / x : r;   // wave-uniform branch
+        return r;
+    }
     if (__builtin_expect(m - 0x00800000u >= 0x7e000000u - 0x00800000u, 0)) return 1.0f / x;
     const float r0 = __builtin_amdgcn_rcpf(x);
     return __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
@@ -199,15 +218,22 @@ struct Stk24 {
 struct Hit { uint32_t slot; float t, u, v; };
 
 // Triangle::intersect (triangle.hpp:95-115, left-handed normal).
-template <bool kG = false>
+template <bool kG = false, bool kU = false>
 __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin, float tmax, float& t_out,
                                          float& u_out, float& v_out) {
     const F3 c = tr.p0 - o;
     const F3 r = crossG<kG>(d, c);
-    const float inv_det = rcp_exact(dotA<kG>(tr.n, d));
+    const float inv_det = rcp_exact<kU>(dotA<kG>(tr.n, d));
     const float u = dotA<kG>(r, tr.e2) * inv_det;
     const float v = dotB<kG>(r, tr.e1) * inv_det;
     const float w = 1.0f - u - v;
+    if (CERES_TRI_SELECT) {
+        // the same values and the same decision, without control flow: t is computed whether or not
+        // (u, v, w) pass, and the comparisons (false on NaN) are combined with bitwise ands
+        const float t = dotA<kG>(tr.n, c) * inv_det;
+        t_out = t; u_out = u; v_out = v;
+        return (u >= 0) & (v >= 0) & (w >= 0) & (t >= tmin) & (t <= tmax);
+    }
     if (u >= 0 && v >= 0 && w >= 0) {
         const float t = dotA<kG>(tr.n, c) * inv_det;
         if (t >= tmin && t <= tmax) { t_out = t; u_out = u; v_out = v; return true; }
@@ -218,13 +244,13 @@ __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin,
 // tri_test on triangle `idx`, the wave-uniform case with its own copy of the test: the test
 // then reads the record from SGPRs instead of first copying the 12 scalar-loaded words into
 // VGPRs to join the vector path (12 v_mov per uniform test; CERES_SPLIT_UNIFORM)
-template <bool kG = false>
+template <bool kG = false, bool kU = false>
 __device__ __forceinline__ bool tri_test_u(const Tri48* tris, uint32_t idx, F3 o, F3 d, float tmin, float tmax,
                                            float& t_out, float& u_out, float& v_out) {
-    if (!CERES_SPLIT_UNIFORM) return tri_test<kG>(load_tri_u(tris, idx), o, d, tmin, tmax, t_out, u_out, v_out);
+    if (!CERES_SPLIT_UNIFORM) return tri_test<kG, kU>(load_tri_u(tris, idx), o, d, tmin, tmax, t_out, u_out, v_out);
     uint32_t r;
-    if (uniform_id(idx, r)) return tri_test<kG>(load_tri_s(tris + r), o, d, tmin, tmax, t_out, u_out, v_out);
-    return tri_test<kG>(load_tri(tris + idx), o, d, tmin, tmax, t_out, u_out, v_out);
+    if (uniform_id(idx, r)) return tri_test<kG, kU>(load_tri_s(tris + r), o, d, tmin, tmax, t_out, u_out, v_out);
+    return tri_test<kG, kU>(load_tri(tris + idx), o, d, tmin, tmax, t_out, u_out, v_out);
 }
 
 // Per-ray constants of the ray-box (slab) test and the test of one box.
@@ -330,11 +356,13 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     const float tmin = 0.0f;
     float tmax = FLT_MAX;                                           // ray.hpp:17-21
     bool have = false;
+    // kOct -2 = the single-frame kernel's generic loop
+    constexpr bool kU = CERES_RCP_UNIFORM == 1 || (CERES_RCP_UNIFORM == 2 && kOct == -2);
     if (P.root_leaf_count) {                                          // root is a leaf, :72-73
         if (kStats) n_tests += P.root_leaf_count;
         for (uint32_t k = P.root_leaf_first; k < P.root_leaf_first + P.root_leaf_count; ++k) {
             float t, u, v;
-            if (tri_test<kG>(load_tri(P.tris + k), o, d, tmin, tmax, t, u, v)) {
+            if (tri_test<kG, kU>(load_tri(P.tris + k), o, d, tmin, tmax, t, u, v)) {
                 best = {k, t, u, v}; have = true;
                 if (kAnyHit) return true;
                 tmax = t;
@@ -409,7 +437,15 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         while (k < k_end || k2 < k2_end) {
             const uint32_t idx = k < k_end ? k++ : k2++;
             float t, u, v;
-            if (tri_test_u<kG>(P.tris, idx, o, d, tmin, tmax, t, u, v)) {
+            if (CERES_TRI_SELECT && !kAnyHit) {                          // closest hit: selects, no branch
+                const bool h = tri_test_u<kG, kU>(P.tris, idx, o, d, tmin, tmax, t, u, v);
+                best.slot = h ? idx : best.slot; best.t = h ? t : best.t;
+                best.u = h ? u : best.u; best.v = h ? v : best.v;
+                have |= h;
+                tmax = h ? t : tmax;
+                continue;
+            }
+            if (tri_test_u<kG, kU>(P.tris, idx, o, d, tmin, tmax, t, u, v)) {
                 best = {idx, t, u, v}; have = true;
                 if (kAnyHit) return true;
                 tmax = t;
@@ -541,7 +577,7 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
                 if (kStats) n_tests += k_end - k;
             }
             float t, u, v;
-            if (tri_test_u<kG>(P.tris, k, o, d, tmin, tmax, t, u, v)) return true;
+            if (tri_test_u<kG, CERES_RCP_UNIFORM == 1>(P.tris, k, o, d, tmin, tmax, t, u, v)) return true;
             ++k;
         }
         if (inner_mask) {
@@ -624,7 +660,7 @@ __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<fal
                 // all 48 B in flight before the first use (one scalar-load wait per triangle, not two)
                 __asm__ volatile("" ::"s"(a.x), "s"(b.x), "s"(g.x));
                 const TriV tr{{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, g.x}, {g.y, g.z, g.w}};
-                const bool h = tri_test<kG>(tr, o, d, tmin, tmax, t, u, v);
+                const bool h = tri_test<kG, CERES_RCP_UNIFORM == 1>(tr, o, d, tmin, tmax, t, u, v);
                 occ |= __ballot(h) & lm;
                 lm &= ~occ;
             }
@@ -909,7 +945,7 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
                     if (kStats) n_tests += k_end - k;
                 }
                 float t, u, v;
-                if (tri_test_u<kG>(P.tris, k, w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
+                if (tri_test_u<kG, CERES_RCP_UNIFORM != 0>(P.tris, k, w.o, w.d, tmin, tmax, t, u, v)) { found = true; break; }
                 ++k;
             }
             if (found) {
