@@ -12,15 +12,22 @@ sixteen frames' work per GPU from the same orbit at every N (one batch launch pe
 Every one of those views has its reference PPM sha256 and rays/hits in
 tests/golden/orbit/<config>.json (made by the reference's own render(), make_golden.py --orbit),
 and every frame the validation step assembles is checked against it.
-Every frame's rows are interleaved over the ranks in blocks of --row-block rows (balanced
-load); each rank renders its rows of all F frames with one ceres_render_batch_device launch,
-RGB8 + float framebuffers in HBM, then ONE RCCL collective per step: by default each frame is
-gathered to one owner rank (rank q owns 16 of the 16N frames; all the per-frame gathers are one
-all-to-all, so no rank's xGMI ingress carries the whole step; ceres_assemble_rgb8_packed
-un-interleaves a rank's frames), or with
---collect gather all F frames go to rank 0.  Steps rotate over --streams HIP streams (own
-buffers each): the collective/assembly of step k and the tail of its render overlap later
-steps; the timed region ends when every step's frames are assembled.
+At N > 1 (--collect, default auto):
+  frames    the frames are the units: rank q renders orbit frames q, q + N, q + 2N, ... (16 of the
+            16N) whole, with one ceres_render_batch_device launch, into its own HBM -- no
+            collective, nothing on the xGMI links (frames are independent: render.hpp:104-153);
+  exchange  every frame's rows are interleaved over the ranks in blocks of --row-block rows; each
+            rank renders its rows of all F frames, then ONE RCCL all-to-all per step gathers each
+            frame to its owner rank (rank q owns the same 16 frames as above) and
+            ceres_assemble_rgb8_packed un-interleaves them -- the tiled framebuffer of BASELINE's
+            C4 ("framebuffer tiled across 8x MI355X with RCCL gather");
+  gather    rows interleaved, all F frames to rank 0.
+  auto = exchange for configs defined as a tiled framebuffer (configs.py "tiled": C4) except at
+  N = 2, where the exchange would put 16 frames' worth of rows on one xGMI link per step and
+  outlast the render (DESIGN.md "Multi-GPU"); frames otherwise.
+RGB8 + float framebuffers in HBM.  Steps rotate over --streams HIP streams (own buffers each):
+the collective/assembly of step k and the tail of its render overlap later steps; the timed
+region ends when every step's frames are assembled.
 Scene upload, OBJ load and BVH build are outside the timed region, as in the reference
 (static.cpp:129-133).  value = (primary + shadow rays of all F frames) x steps / wall time
 (max over ranks).  One process per GPU (torch.distributed, backend nccl = RCCL).
@@ -285,9 +292,12 @@ def main():
     ap.add_argument("--no-view0-only", action="store_true",
                     help="skip the second timed loop with every frame = frame 0's view (C3 itself)")
     ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
-    ap.add_argument("--collect", choices=("exchange", "gather"), default="exchange",
-                    help="N > 1: every frame of a step to one owner rank in one all-to-all (exchange; frames a "
-                         "multiple of N) or all frames to rank 0 (gather)")
+    ap.add_argument("--collect", choices=("auto", "frames", "exchange", "gather"), default="auto",
+                    help="N > 1: frames = unsplit frames, each rank renders its F/N frames whole (no collective); "
+                         "exchange = every frame's rows dealt over the ranks, each frame gathered to one owner rank "
+                         "in one all-to-all; gather = rows dealt, all frames to rank 0; auto = exchange for "
+                         "configs defined as a tiled framebuffer (C4) except at N = 2, where one link would carry "
+                         "it (DESIGN.md \"Multi-GPU\"), else frames")
     ap.add_argument("--prime-s", type=float, default=0.3,
                     help="untimed setup: seconds of steps before the W warmup steps (GPU clock ramp)")
     ap.add_argument("--streams", type=int, default=8,
@@ -333,7 +343,13 @@ def main():
     scene = pkg.Scene(mesh, bvh, device=local_rank)
     # F views of the orbit, frame f rotated once by f x 360 / F degrees (frame 0 = C3, fixture bits)
     b12, s3, steps_deg = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=pinned_basis(meta, cfg, cam, build))
-    exchange = world > 1 and args.collect == "exchange" and F % world == 0
+    collect = args.collect
+    if collect == "auto":
+        collect = "exchange" if cfg.get("tiled") and world != 2 else "frames"
+    if collect in ("frames", "exchange") and F % world:
+        collect = "gather"
+    owner = world > 1 and collect == "frames"              # unsplit frames: no collective
+    exchange = world > 1 and collect in ("exchange", "frames")
     if exchange:
         # batch order for the all-to-all: rank q owns batch frames q*k .. q*k+k-1, which are orbit
         # frames q, q + N, q + 2N, ... (batch frame 0 = orbit frame 0 = C3)
@@ -341,15 +357,23 @@ def main():
         b12, s3, steps_deg = b12[order], s3[order], steps_deg[order]
     mode = pkg.cfg_mode(cfg, arith)
     full_mode = (mode & 0xf) == pkg.MODE_FULL
-    row_block = args.row_block if world > 1 else H
-    tiling = pkg.Tiling(row_block, rank, world)
+    row_block = args.row_block if world > 1 and not owner else H
+    tiling = pkg.Tiling(row_block, rank, world) if not owner else pkg.Tiling(H, 0, 1)
     S = max(1, args.streams)
-    if exchange:     # each frame to one owner rank: a rank's ingress is (N-1)/N of its k frames per step
+    job_steps = steps_deg                        # the whole job's views, in batch order
+    Fl = F                                       # frames this rank's launches render
+    if owner:        # rank q renders batch frames q*k .. q*k+k-1 whole
+        gather = D.FrameOwner(W, H, rank, world, frames=F, device=dev, slots=max(2, S))
+        mine_f = gather.owned_frames()
+        Fl = len(mine_f)
+        b12_all, s3_all = b12, s3
+        b12, s3, steps_deg = b12[mine_f], s3[mine_f], steps_deg[mine_f]
+    elif exchange:   # each frame to one owner rank: a rank's ingress is (N-1)/N of its k frames per step
         gather = D.FrameExchange(W, H, row_block, rank, world, frames=F, device=dev, slots=max(2, S))
     else:            # every frame -> rank 0
         gather = D.BatchGather(W, H, row_block, rank, world, frames=F, device=dev, slots=max(2, S))
     rows = gather.local_rows
-    d_px = [None if args.no_float else torch.empty(F * 3 * W * max(rows, 1), dtype=torch.float32, device=dev)
+    d_px = [None if args.no_float else torch.empty(Fl * 3 * W * max(rows, 1), dtype=torch.float32, device=dev)
             for _ in range(S)]
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -362,16 +386,17 @@ def main():
     pending = [False] * slots
 
     MAXF = 64                                    # frames per ceres_render_batch_device launch (kMaxFrames)
-    chunk_counters = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range((F + MAXF - 1) // MAXF)]
-    views = {"b12": b12, "s3": s3, "steps": steps_deg}      # what every step renders
+    chunk_counters = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range((Fl + MAXF - 1) // MAXF)]
+    views = {"b12": b12, "s3": s3, "steps": steps_deg,       # what this rank renders every step
+             "job": job_steps}                               # ... and the whole step's views (batch order)
 
     def render(slot, st, with_counters=False):
         # one launch per (at most) 64 frames of the step; frame f's rows at f * 3 * W * rows
         px = d_px[slot % S]
         fb = 3 * W * max(rows, 1)
         vb, vs = views["b12"], views["s3"]
-        for c, f0 in enumerate(range(0, F, MAXF)):
-            f1 = min(F, f0 + MAXF)
+        for c, f0 in enumerate(range(0, Fl, MAXF)):
+            f1 = min(Fl, f0 + MAXF)
             scene.render_batch_device(vb[f0:f1], vs[f0:f1], W, H, mode=mode, tiling=tiling,
                                       d_pixels=0 if px is None else px.data_ptr() + 4 * fb * f0,
                                       d_rgb8=gather.local_ptr(slot) + fb * f0,
@@ -429,7 +454,7 @@ def main():
         head = b"P6 %d %d 255\n" % (W, H)
         n = [0, 0, 0]                                            # [checked, matched, unpinned]
         for f, body in mine:
-            e = None if orbit_fx is None else view_entry(orbit_fx.get(step_key(views["steps"][f])), build)
+            e = None if orbit_fx is None else view_entry(orbit_fx.get(step_key(views["job"][f])), build)
             if e is None:
                 n[2] += 1
                 continue
@@ -439,7 +464,7 @@ def main():
         if world > 1:
             dist.all_reduce(stat)
         stat = stat.cpu().numpy()
-        keys = [None if orbit_fx is None else view_entry(orbit_fx.get(step_key(x)), build) for x in views["steps"]]
+        keys = [None if orbit_fx is None else view_entry(orbit_fx.get(step_key(x)), build) for x in views["job"]]
         ref_rays = sum(e["rays"] for e in keys) if all(keys) else None
         ref_hits = sum(e["hits"] for e in keys) if all(keys) else None
         checks = {"frames": F, "frames_checked": int(stat[0]), "frames_unpinned": int(stat[2]),
@@ -523,17 +548,18 @@ def main():
 
     T = timed(prime=True)
     value = rays_step * args.steps / T / 1e6
-    bytes_step = step_bytes(views["steps"])
+    bytes_step = step_bytes(views["job"])
     primary_step = F * W * H
     view0 = None
     if not args.no_view0_only:
         # the same loop with every frame = frame 0's view (C3 itself for dragon_1080): the orbit mix
         # has fewer shadow rays per frame than C3, so report both
-        views.update(b12=np.repeat(b12[:1], F, 0), s3=np.repeat(s3[:1], F, 0),
-                     steps=np.repeat(steps_deg[:1], F))
+        v0b, v0s, v0d = (b12_all[:1], s3_all[:1], job_steps[:1]) if owner else (b12[:1], s3[:1], steps_deg[:1])
+        views.update(b12=np.repeat(v0b, Fl, 0), s3=np.repeat(v0s, Fl, 0), steps=np.repeat(v0d, Fl),
+                     job=np.repeat(v0d, F))
         rays0, hits0, checks0 = validate()
         T0 = timed(prime=False)
-        b0 = step_bytes(views["steps"])
+        b0 = step_bytes(views["job"])
         view0 = {"value": round(rays0 * args.steps / T0 / 1e6, 3), "unit": "Mrays/s",
                  "roofline_step": roofline_step_block(b0, T0 / args.steps * 1e3, world),
                  "ms_per_step": round(T0 / args.steps * 1e3, 5), "rays_per_step": rays0, "hits_per_step": hits0,
@@ -624,14 +650,19 @@ def main():
                        "W": W, "H": H, "frames_per_step": F, "rays_per_step": rays_step, "hits_per_step": hits_step,
                        "shadow_ray_frac": round((rays_step - primary_step) / rays_step, 4)
                        if full_mode else 0.0,
-                       "row_block": row_block, "parallelism": f"row-interleaved frames x{world}"
-                       + ((" + one RCCL all-to-all per step: frame f gathered to rank f (pipelined)" if exchange
-                           else " + one RCCL gather per step to rank 0 (pipelined)") if world > 1 else ""),
+                       "row_block": row_block,
+                       "parallelism": (f"unsplit frames x{world}: rank q renders orbit frames q, q+{world}, ... whole, "
+                                       "no collective" if owner else
+                                       f"row-interleaved frames x{world}"
+                                       + ((" + one RCCL all-to-all per step: frame f gathered to rank f (pipelined)"
+                                           if exchange else " + one RCCL gather per step to rank 0 (pipelined)")
+                                          if world > 1 else "")),
+                       "collect": collect if world > 1 else None,
                        "float_framebuffer": d_px[0] is not None, "streams": S},
             # the step's one collective against the xGMI budget (DESIGN.md "Multi-GPU"): bytes one rank
             # receives per step, 1/N of them from each peer over that peer's direct link (one link per
             # peer in a fully connected 8-GPU node) at 76.8 GB/s per link and direction
-            "collective": None if world == 1 else {
+            "collective": None if world == 1 or owner else {
                 "kind": "all_to_all" if exchange else "gather",
                 "recv_bytes_per_rank_step": (world - 1) * (F // world if exchange else F) * H * 3 * W // world,
                 "xgmi_link_ms_est": round((F // world if exchange else F) * H * 3 * W / world / 76.8e6, 4),

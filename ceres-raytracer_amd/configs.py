@@ -35,6 +35,7 @@ def _cfg(base, **kw):
     d.setdefault("proc", 0)
     d.setdefault("orbit", None)
     d.setdefault("robust", False)
+    d.setdefault("tiled", False)       # a multi-GPU config defined as ONE framebuffer tiled over the GPUs
     return d
 
 
@@ -47,15 +48,16 @@ CONFIGS = {
     # C3: dragon 1920x1080 primary+shadow -- the BASELINE.json headline metric config
     "dragon_1080": _cfg(_DRAGON, W=1920, H=1080),
     "dragon_640": _cfg(_DRAGON, W=640, H=480),
-    # C4: dragon 4096x4096
-    "dragon_4096": _cfg(_DRAGON, W=4096, H=4096),
+    # C4: dragon 4096x4096 ("framebuffer tiled across 8x MI355X with RCCL gather": bench.py's
+    # --collect auto deals its rows over the ranks)
+    "dragon_4096": _cfg(_DRAGON, W=4096, H=4096, tiled=True),
     # ragged sizes (not multiples of any tile), single pixel
     "dragon_333x217": _cfg(_DRAGON, W=333, H=217),
     "bunny_97x61_primary": _cfg(_BUNNY, W=97, H=61, mode="primary"),
     "bunny_1x1": _cfg(_BUNNY, W=1, H=1),
     # procedural heightfield, small (101x101 vertices = 20,000 tris) and C5 (2237^2 = 9,999,392 tris)
     "proc_101": _cfg(_PROC, proc=101, W=320, H=240),
-    "proc_c5": _cfg(_PROC, proc=2237, W=3840, H=2160),
+    "proc_c5": _cfg(_PROC, proc=2237, W=3840, H=2160, tiled=True),
     # tiny hand-written meshes: root-is-leaf, fan triangulation / negative indices / v/vt/vn, degenerate tris
     "tri1": _cfg(_TINY, obj="@golden/tri1.obj", W=64, H=48),
     "quad": _cfg(_TINY, obj="@golden/quad.obj", W=64, H=48),

@@ -12,7 +12,8 @@ bench's default, F = k N -- each frame is gathered to one owner rank (k frames p
 those gathers as one all-to-all (FrameExchange), so no single rank's ingress carries the whole
 step.  Both are
 multi-buffered: the gather (RCCL stream) and assembly (side stream) of step k overlap the
-render of step k + 1.  The scene is replicated (uploaded per device, outside the timed
+render of step k + 1.  FrameOwner is the collective-free partition of the same step: each rank
+renders its k frames whole (no row split, nothing to gather).  The scene is replicated (uploaded per device, outside the timed
 region).  The reference has no distributed code (render.hpp:104 is an OpenMP loop).
 """
 import numpy as np
@@ -266,6 +267,51 @@ class FrameExchange:
             for s, used in enumerate(self.reused):
                 if used:
                     torch.cuda.current_stream(self.device).wait_event(self.assembled[s])
+
+
+class FrameOwner:
+    """Unsplit frames (no collective): rank q renders its k = F/N frames of the step WHOLE, straight
+    into PPM bodies in its own HBM -- batch frames q*k .. q*k+k-1 of exchange_order, i.e. orbit
+    frames q, q + N, q + 2N, ..., so every rank samples the whole orbit and the ranks' loads stay
+    balanced.  Frames are independent (render.hpp:104-153 touches one frame's pixels), so the step
+    has no data-path exchange at all: the xGMI links carry nothing, and a rank's work is k whole
+    frames at every N.  Same interface as FrameExchange (start/finish/wait_assembled are no-ops
+    beyond handing back the rank's own buffer).
+    """
+
+    def __init__(self, W, H, rank, world, frames=None, device="cpu", slots=2):
+        import torch
+        frames = world if frames is None else frames
+        if frames % world:
+            raise ValueError("FrameOwner: frames (%d) must be a multiple of world (%d)" % (frames, world))
+        self.W, self.H, self.rank, self.world = W, H, rank, world
+        self.frames, self.slots = frames, slots
+        self.k = frames // world
+        self.device = torch.device(device)
+        self.local_rows = H                  # whole frames
+        self.row_bytes = 3 * W
+        self.is_dst = True
+        self.bufs = [torch.zeros((self.k * H, self.row_bytes), dtype=torch.uint8, device=self.device)
+                     for _ in range(slots)]
+
+    def owned_frames(self):
+        """Batch frame indices (exchange_order) this rank renders, in buffer order."""
+        return list(range(self.rank * self.k, (self.rank + 1) * self.k))
+
+    def local_ptr(self, slot=0):
+        return self.bufs[slot].data_ptr()
+
+    def frame_view(self, slot=0):
+        return self.bufs[slot].view(self.k, self.H, self.row_bytes)
+
+    def start(self, slot=0):
+        return None
+
+    def finish(self, slot=0):
+        return self.frame_view(slot)
+
+    def wait_assembled(self):
+        return None
 
 
 class FrameGather(BatchGather):

@@ -252,3 +252,91 @@ def test_packed_permutation_matches_padded():
         off = np.cumsum([0] + [frames * len(r) for r in rows])
         r_of = padded // (frames * maxrows)
         np.testing.assert_array_equal(packed, off[r_of] + padded % (frames * maxrows))
+
+
+@pytest.mark.parametrize("world,k", [(1, 16), (2, 16), (3, 2), (4, 16), (8, 16), (8, 1)])
+def test_frame_owner_partition(world, k):
+    """bench.py --collect frames (the default except for tiled C4/C5 at N != 2): rank q renders
+    batch frames q*k .. q*k+k-1 of exchange_order WHOLE -- orbit frames q, q+N, q+2N, ... -- so
+    the ranks' frames partition the step, each rank samples the whole orbit (consecutive frames
+    of a rank are N orbit frames apart), and the rank's buffer already holds its k PPM bodies
+    (finish() hands back the buffer itself: no collective, no copy)."""
+    import_package()
+    import ceres_raytracer_amd.distributed as D
+    W, H = 13, 7
+    F = k * world
+    order = D.exchange_order(F, world)
+    seen = []
+    for q in range(world):
+        g = D.FrameOwner(W, H, q, world, frames=F, device="cpu", slots=2)
+        assert g.local_rows == H and g.k == k
+        own = g.owned_frames()
+        orbit = [int(order[f]) for f in own]
+        assert orbit == [q + m * world for m in range(k)]
+        seen += orbit
+        assert tuple(g.bufs[1].shape) == (k * H, 3 * W)
+        assert g.start(1) is None
+        out = g.finish(1)
+        assert tuple(out.shape) == (k, H, 3 * W) and out.data_ptr() == g.bufs[1].data_ptr()
+    assert sorted(seen) == list(range(F))
+    with pytest.raises(ValueError):
+        D.FrameOwner(W, H, 0, world + 1, frames=(world + 1) * k + 1)
+
+
+def _owner_worker(rank, world, port, W, H, k, q):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import import_package as ip
+    ip()
+    import hashlib
+    import torch
+    import torch.distributed as dist
+    import ceres_raytracer_amd.distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        F = k * world
+        order = D.exchange_order(F, world)
+        ok = True
+        g = D.FrameOwner(W, H, rank, world, frames=F, device="cpu", slots=2)
+
+        def body(orbit_f, step):                    # the frame a renderer would produce for this view
+            rng = np.random.default_rng(1000 * step + orbit_f)
+            return rng.integers(0, 256, size=(H, 3 * W), dtype=np.uint8)
+
+        for step in range(4):                        # bench.py's protocol: render into the slot, start, finish
+            slot = step % 2
+            for m, f in enumerate(g.owned_frames()):
+                g.bufs[slot][m * H:(m + 1) * H] = torch.from_numpy(body(int(order[f]), step))
+            g.start(slot)
+            full = g.finish(slot)
+            g.wait_assembled()
+            # validation as bench.py does it: every rank checks its own frames, then one all_reduce
+            got = torch.zeros(F, dtype=torch.int64)
+            for m, f in enumerate(g.owned_frames()):
+                h = hashlib.sha256(full[m].numpy().tobytes()).hexdigest()
+                got[int(order[f])] += int(h == hashlib.sha256(body(int(order[f]), step).tobytes()).hexdigest())
+            dist.all_reduce(got)
+            ok &= bool((got == 1).all())
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k", [(2, 16), (4, 3)])
+def test_frame_owner_gloo_step(world, k):
+    """The collective-free partition through bench.py's step protocol on `world` gloo ranks: every
+    orbit frame of every step is produced by exactly one rank and checked there (all_reduce of the
+    per-frame matches = 1 for every frame)."""
+    import_package()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, 17, 9, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert all(res.values()), res

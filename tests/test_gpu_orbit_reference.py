@@ -101,3 +101,56 @@ def test_bench_step_frames_match_reference(pkg, name, world, build):
             bad.append((f, e0["k"]))
     assert not bad, f"frames differing from the reference (batch frame, orbit view k): {bad}"
     assert (rays, hits) == (ref_rays, ref_hits)
+
+
+FRAMES_CASES = [("dragon_1080", 2, "ref"), ("dragon_1080", 4, "exact"), ("dragon_1080", 8, "ref"),
+                ("bunny_1080", 2, "ref"), ("dragon_4096", 2, "ref"), ("proc_c5", 2, "ref")]
+
+
+@pytest.mark.parametrize("name,world,build", FRAMES_CASES)
+def test_bench_frames_partition_matches_reference(pkg, name, world, build):
+    """bench.py --collect frames (its default for C3 at every N and for the tiled C4 / C5 at N = 2):
+    rank q renders batch frames q*k .. q*k+k-1 of exchange_order (orbit frames q, q+N, ...) WHOLE
+    with one batch launch; its k PPM bodies are the reference's, and the ranks' rays / hits add up
+    to the step's reference counts."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device (no CPU fallback exists)")
+    import ceres_raytracer_amd.distributed as D
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    meta, _, _ = load_golden(name)
+    fx = load_orbit(name)["by_step_bits"]
+    arith = pkg.ARITH_FMA if build == "ref" else pkg.ARITH_EXACT
+    scene, cam = _scene(pkg, name, arith)
+    F = 16 * world
+    b12, s3, steps = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=_basis0(meta, cfg, build))
+    order = D.exchange_order(F, world)
+    b12, s3, steps = b12[order], s3[order], steps[order]
+    mode = pkg.cfg_mode(cfg, arith)
+    st = torch.cuda.current_stream().cuda_stream
+    head = b"P6 %d %d 255\n" % (W, H)
+    counters = torch.zeros(8, dtype=torch.int64, device="cuda")
+    rays = hits = 0
+    bad = []
+    for r in range(world):
+        g = D.FrameOwner(W, H, r, world, frames=F, device="cuda", slots=1)
+        mine = g.owned_frames()
+        counters.zero_()
+        scene.render_batch_device(b12[mine], s3[mine], W, H, mode=mode, tiling=pkg.Tiling(H, 0, 1),
+                                  d_rgb8=g.local_ptr(0), d_counters=counters.data_ptr(), stream=st)
+        torch.cuda.synchronize()
+        c = counters.cpu().numpy()
+        assert c[6] == 0, "traversal stack overflow"
+        rays += int(c[0]); hits += int(c[1])
+        full = g.finish(0)
+        for m, f in enumerate(mine):
+            e0 = fx["%08x" % int(np.asarray(steps[f], np.float32).view(np.uint32))]
+            e = e0["ref"] if build == "ref" else e0
+            if hashlib.sha256(head + full[m].cpu().numpy().tobytes()).hexdigest() != e["sha256"]:
+                bad.append((r, f, e0["k"]))
+        del g, full
+    assert not bad, f"frames differing from the reference (rank, batch frame, orbit view k): {bad}"
+    ref = [fx["%08x" % int(np.asarray(x, np.float32).view(np.uint32))] for x in steps]
+    ref = [e["ref"] if build == "ref" else e for e in ref]
+    assert (rays, hits) == (sum(e["rays"] for e in ref), sum(e["hits"] for e in ref))

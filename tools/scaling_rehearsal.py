@@ -17,6 +17,12 @@ traffic and CU time.  The link time is budgeted separately: 1/N of the rank's k 
 peer over its own xGMI link at XGMI_GBS per link and direction (default 76.8 GB/s: 153.6 GB/s
 bidirectional).
 
+Round 4 adds the collective-free partition bench.py uses by default (--collect frames): rank q
+renders its k frames of the step (batch frames q*k .. q*k+k-1 of exchange_order = orbit frames q,
+q+N, ...) whole, one launch per step, pipelined over the 8 streams -- nothing to exchange, so its
+predicted efficiency is the slowest rank's render against N = 1.  Arithmetic: CERES_ARITH=fma
+(default, bench.py's) or exact.
+
     python tools/scaling_rehearsal.py [config] [reps] [frames per GPU] [row block] > gpurun_out/scaling_rehearsal.json
 """
 import json
@@ -46,17 +52,21 @@ def main():
     W, H = cfg["W"], cfg["H"]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    mesh, bvh, cam = pkg.prepare(cfg)
+    build = "ref" if os.environ.get("CERES_ARITH", "fma") == "fma" else "exact"
+    arith = pkg.ARITH_FMA if build == "ref" else pkg.ARITH_EXACT
+    mesh, bvh, cam = pkg.prepare(cfg, arith=arith)
     scene = pkg.Scene(mesh, bvh, device=0)
-    mode = pkg.cfg_mode(cfg)
+    mode = pkg.cfg_mode(cfg, arith)
     stream = torch.cuda.current_stream(dev)
     S = 8
     streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
-    out = {"config": name, "W": W, "H": H, "reps": reps, "frames_per_gpu": k, "device": torch.cuda.get_device_name(0), "by_n": {}}
+    out = {"config": name, "W": W, "H": H, "reps": reps, "frames_per_gpu": k, "arith": build,
+           "device": torch.cuda.get_device_name(0), "by_n": {}}
     base = None
+    import ceres_raytracer_amd.distributed as D
     for N in (1, 2, 4, 8):
         F = k * N
-        b12, s3 = step_views(pkg, cfg, meta, cam, F, k)      # the same arc at every N, as bench.py
+        b12, s3 = step_views(pkg, cfg, meta, cam, F, k, build=build)      # the same arc at every N, as bench.py
         row_block = rb if N > 1 else H
         per_rank = []
         rank_rays = []
@@ -131,6 +141,32 @@ def main():
                         copied[q % S] = ev
                     torch.cuda.synchronize(dev)
                 piped_x.append((time.perf_counter() - t0) * 1e3 / (reps * S // 2))
+        # --collect frames: rank q's k frames whole (exchange_order batch frames q*k ..), pipelined
+        order = D.exchange_order(F, N)
+        ob12, os3 = b12[order], s3[order]
+        whole = pkg.Tiling(H, 0, 1)
+        fpx = [torch.empty(k * 3 * W * H, dtype=torch.float32, device=dev) for _ in range(S)]
+        frgb = [torch.empty(k * 3 * W * H, dtype=torch.uint8, device=dev) for _ in range(S)]
+        piped_f = []
+        for r in range(N):
+            rb12, rs3 = ob12[r * k:(r + 1) * k], os3[r * k:(r + 1) * k]
+            for it in range(2):                          # warm, then timed
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for q in range(reps * S // 2):
+                    for f0 in range(0, k, 64):
+                        f1 = min(k, f0 + 64)
+                        scene.render_batch_device(rb12[f0:f1], rs3[f0:f1], W, H, mode=mode, tiling=whole,
+                                                  d_pixels=fpx[q % S].data_ptr() + 4 * 3 * W * H * f0,
+                                                  d_rgb8=frgb[q % S].data_ptr() + 3 * W * H * f0,
+                                                  stream=streams[q % S].cuda_stream)
+                torch.cuda.synchronize(dev)
+            piped_f.append((time.perf_counter() - t0) * 1e3 / (reps * S // 2))
+        del fpx, frgb
+        pipe_f_ms = max(piped_f)
+        mrays_f = rays / (pipe_f_ms * 1e3)
+        if N == 1:
+            base_f = mrays_f
         asm_ms = 0.0
         if N > 1:
             recv = torch.zeros((N, F * maxrows, 3 * W), dtype=torch.uint8, device=dev)
@@ -168,7 +204,10 @@ def main():
                           "xgmi_link_ms_per_step": round(k * H * 3 * W / N / (XGMI_GBS * 1e6), 4),
                           "pipelined_with_exchange_rank_ms": [round(x, 5) for x in piped_x],
                           "predicted_mrays_s_pipelined_with_exchange": round(mrays_x, 1),
-                          "predicted_weak_efficiency_pipelined_with_exchange": round(mrays_x / (N * base_p), 3)}
+                          "predicted_weak_efficiency_pipelined_with_exchange": round(mrays_x / (N * base_p), 3),
+                          "frames_partition_rank_ms": [round(x, 5) for x in piped_f],
+                          "predicted_mrays_s_frames_partition": round(mrays_f, 1),
+                          "predicted_weak_efficiency_frames_partition": round(mrays_f / (N * base_f), 3)}
         print(json.dumps({"N": N, **out["by_n"][N]}), file=sys.stderr, flush=True)
     scene.close()
     print(json.dumps(out))
