@@ -343,6 +343,12 @@ def main():
     scene = pkg.Scene(mesh, bvh, device=local_rank)
     # F views of the orbit, frame f rotated once by f x 360 / F degrees (frame 0 = C3, fixture bits)
     b12, s3, steps_deg = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=pinned_basis(meta, cfg, cam, build))
+    view0_step = bool(cfg.get("bench_view0"))
+    if view0_step:
+        # C5: the orbit about z through the origin leaves the [0,1]^2 heightfield for views 40..96 of
+        # 128 (no triangle in view), which would flatter the step; its step is F copies of the
+        # config's own view instead (each checked against the reference's PPM of that view)
+        b12, s3, steps_deg = np.repeat(b12[:1], F, 0), np.repeat(s3[:1], F, 0), np.repeat(steps_deg[:1], F)
     collect = args.collect
     if collect == "auto":
         collect = "exchange" if cfg.get("tiled") and world != 2 else "frames"
@@ -551,7 +557,7 @@ def main():
     bytes_step = step_bytes(views["job"])
     primary_step = F * W * H
     view0 = None
-    if not args.no_view0_only:
+    if not args.no_view0_only and not view0_step:
         # the same loop with every frame = frame 0's view (C3 itself for dragon_1080): the orbit mix
         # has fewer shadow rays per frame than C3, so report both
         v0b, v0s, v0d = (b12_all[:1], s3_all[:1], job_steps[:1]) if owner else (b12[:1], s3[:1], steps_deg[:1])
@@ -643,10 +649,12 @@ def main():
             "data": ("real mesh from the reference repo (data/%s)" % cfg["obj"] if cfg["obj"] else
                      "procedural %dx%d-vertex heightfield generated in-process (SURVEY.md §8(d) C5 definition)"
                      % (cfg["proc"], cfg["proc"]))
-                    + "; frame 0 = the config camera, frames 1.. = the anim.cpp-style orbit about z",
+                    + ("; every frame = the config camera" if view0_step else
+                       "; frame 0 = the config camera, frames 1.. = the anim.cpp-style orbit about z"),
             "config": {"workload": f"{args.config}: {cfg['obj'] or 'proc'} {W}x{H} "
                                    f"{'primary+shadow' if full_mode else 'primary only'}, "
-                                   f"{F} orbit frame(s) per step",
+                                   + (f"{F} copies of the config view per step" if view0_step
+                                      else f"{F} orbit frame(s) per step"),
                        "W": W, "H": H, "frames_per_step": F, "rays_per_step": rays_step, "hits_per_step": hits_step,
                        "shadow_ray_frac": round((rays_step - primary_step) / rays_step, 4)
                        if full_mode else 0.0,

@@ -57,7 +57,8 @@ CONFIGS = {
     "bunny_1x1": _cfg(_BUNNY, W=1, H=1),
     # procedural heightfield, small (101x101 vertices = 20,000 tris) and C5 (2237^2 = 9,999,392 tris)
     "proc_101": _cfg(_PROC, proc=101, W=320, H=240),
-    "proc_c5": _cfg(_PROC, proc=2237, W=3840, H=2160, tiled=True),
+    # (bench_view0: bench.py's step is 16 copies of this view -- the z orbit leaves the heightfield)
+    "proc_c5": _cfg(_PROC, proc=2237, W=3840, H=2160, tiled=True, bench_view0=True),
     # tiny hand-written meshes: root-is-leaf, fan triangulation / negative indices / v/vt/vn, degenerate tris
     "tri1": _cfg(_TINY, obj="@golden/tri1.obj", W=64, H=48),
     "quad": _cfg(_TINY, obj="@golden/quad.obj", W=64, H=48),

@@ -83,6 +83,24 @@
 #define CERES_RCP_UNIFORM 2                    // rcp_exact's IEEE-division fallback behind a wave-uniform branch
 #endif                                         // (ballot) instead of a divergent one: 0 nowhere, 1 in every
                                                // kernel, 2 in the single-frame kernel only
+#ifndef CERES_PACKET_LEAN
+#define CERES_PACKET_LEAN 0                    // packet leaf loop: do-while, hit masks from ballots
+#endif
+#ifndef CERES_LOAD_ALWAYS
+#define CERES_LOAD_ALWAYS 0                    // trace(): finished lanes load a (cached) record too -- no branch
+#endif
+#ifndef CERES_RCP_UNIFORM_TRACE
+#define CERES_RCP_UNIFORM_TRACE 0              // ... and in every primary (closest-hit) traversal
+#endif
+#ifndef CERES_RCP_UNIFORM_PACKET
+#define CERES_RCP_UNIFORM_PACKET 0             // ... and in the shadow packets' triangle tests
+#endif
+#ifndef CERES_STRIP_ORDER
+#define CERES_STRIP_ORDER 0                    // batches: a wavefront's tiles = one horizontal strip (ensure_tile_order)
+#endif
+#ifndef CERES_DEFER_MISS_STORE
+#define CERES_DEFER_MISS_STORE 1               // missed pixels stored at the end of the tile (fused kernel)
+#endif
 #ifndef CERES_TRI_SELECT
 #define CERES_TRI_SELECT 1                     // triangle test without control flow (t always computed, one
 #endif                                         // predicate) and closest-hit updates as selects
@@ -104,6 +122,43 @@ __device__ __forceinline__ F3 operator-(F3 a, F3 b) { return {a.x - b.x, a.y - b
 __device__ __forceinline__ F3 operator*(F3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
 __device__ __forceinline__ float dot(F3 a, F3 b) { float s = a.x * b.x; s += a.y * b.y; s += a.z * b.z; return s; }
 __device__ __forceinline__ F3 cross(F3 a, F3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+// Correctly rounded 1/x (IEEE division: the reference's `1 / dot(n, d)`), fast path: one
+// Newton step r1 = fma(fma(-x, r0, 1), r0, r0) on the hardware estimate r0 = v_rcp_f32(x) is
+// bit-identical to the IEEE quotient for every normal |x| in [2^-126, 2^126) -- checked
+// exhaustively over all 2^32 inputs on gfx950 (tools/probes/rcp_exhaustive.hip,
+// tests/test_gpu_parity.py::test_fast_reciprocal_is_exact).  Zero, denormal, huge, inf and NaN
+// inputs take the full v_div_scale/fmas/fixup division.
+// kU: the division fallback behind a wave-uniform branch (the estimate and the Newton step run in
+// every lane; only a wavefront with an out-of-range input pays the division) -- used where
+// CERES_RCP_UNIFORM selects it (2: the single-frame kernel, where it measured -1..-2 %; in the
+// multi-frame kernel it measured neutral alone and +12 % together with CERES_TRI_SELECT)
+template <bool kU = false>
+__device__ __forceinline__ float rcp_exact(float x) {
+    const uint32_t m = __float_as_uint(x) & 0x7fffffffu;
+    if (kU) {
+        // only x is live at the wave-uniform branch: each side computes its own quotient
+        const bool slow = m - 0x00800000u >= 0x7e000000u - 0x00800000u;
+        if (__builtin_expect(__ballot(slow) != 0, 0)) {
+            const float q = 1.0f / x;
+            const float r0 = __builtin_amdgcn_rcpf(x);
+            return slow ? q : __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+        }
+        const float r0 = __builtin_amdgcn_rcpf(x);
+        return __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+    }
+    if (__builtin_expect(m - 0x00800000u >= 0x7e000000u - 0x00800000u, 0)) return 1.0f / x;
+    const float r0 = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+}
+
+// rcp_exact's fast path alone, for an x known to be a normal float with |x| < 2^126 or NaN: then
+// it IS the IEEE quotient (NaN in, NaN out -- its payload may differ from the division's, so only
+// where a NaN can reach nothing but comparisons).  safe_inverse's argument: |d| <= 1 (d is
+// normalized), clamped to >= FLT_EPSILON.
+__device__ __forceinline__ float rcp_fast(float x) {
+    const float r0 = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+}
 __device__ __forceinline__ F3 normalize(F3 v) { float inv = 1.0f / sqrtf(dot(v, v)); return v * inv; }
 __device__ __forceinline__ F3 f3(const float* p) { return {p[0], p[1], p[2]}; }
 
@@ -175,31 +230,6 @@ __device__ __forceinline__ TriV load_tri_u(const Tri48* tris, uint32_t idx) {
     return load_tri(tris + idx);
 }
 
-// Correctly rounded 1/x (IEEE division, as the reference's `1 / dot(n, d)`), fast path: one
-// Newton step r1 = fma(fma(-x, r0, 1), r0, r0) on the hardware estimate r0 = v_rcp_f32(x) is
-// bit-identical to the IEEE quotient for every normal |x| in [2^-126, 2^126) -- checked
-// exhaustively over all 2^32 inputs on gfx950 (tools/probes/rcp_exhaustive.hip,
-// tests/test_gpu_parity.py::test_fast_reciprocal_is_exact).  Zero, denormal, huge, inf and NaN
-// inputs take the full v_div_scale/fmas/fixup division.
-// kU: the division fallback behind a wave-uniform branch (the estimate and the Newton step run in
-// every lane; only a wavefront with an out-of-range input pays the division) -- used where
-// CERES_RCP_UNIFORM selects it (2: the single-frame kernel, where it measured -1..-2 %; in the
-// multi-frame kernel it measured neutral alone and +12 % together with CERES_TRI_SELECT)
-template <bool kU = false>
-__device__ __forceinline__ float rcp_exact(float x) {
-    const uint32_t m = __float_as_uint(x) & 0x7fffffffu;
-    if (kU) {
-        const bool slow = m - 0x00800000u >= 0x7e000000u - 0x00800000u;
-        const float r0 = __builtin_amdgcn_rcpf(x);
-        const float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
-        if (__builtin_expect(__ballot(slow) != 0, 0)) return slow ? 1.0f / x : r;   // wave-uniform branch
-        return r;
-    }
-    if (__builtin_expect(m - 0x00800000u >= 0x7e000000u - 0x00800000u, 0)) return 1.0f / x;
-    const float r0 = __builtin_amdgcn_rcpf(x);
-    return __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
-}
-
 // 24-bit LDS stack entries for scenes whose node indices need more than 16 bits but fewer
 // than 24 (C5: 5.3M pairs): a u16 plane + a u8 plane, [entry][lane] each.  3 B per entry
 // instead of 4 keeps a 28-deep stack's LDS under the 6-waves/SIMD budget.
@@ -216,6 +246,7 @@ struct Stk24 {
 
 // Per-ray hit; closest hit keeps the LAST accepted hit with t <= tmax (intersect_leaf :54-60).
 struct Hit { uint32_t slot; float t, u, v; };
+constexpr uint32_t kNoSlot = 0xffffffffu;                            // no hit yet (slots are < 2^32 - 1)
 
 // Triangle::intersect (triangle.hpp:95-115, left-handed normal).
 template <bool kG = false, bool kU = false>
@@ -253,6 +284,26 @@ __device__ __forceinline__ bool tri_test_u(const Tri48* tris, uint32_t idx, F3 o
     return tri_test<kG, kU>(load_tri(tris + idx), o, d, tmin, tmax, t_out, u_out, v_out);
 }
 
+// tri_test's decision for every lane as a wave mask (the packet's any-hit): one ballot per
+// comparison, and'ed as masks -- the same predicate without materialising a per-lane boolean
+template <bool kG = false, bool kU = false>
+__device__ __forceinline__ uint64_t tri_mask(const TriV& tr, F3 o, F3 d, float tmin, float tmax) {   // tmin > -1
+    const F3 c = tr.p0 - o;
+    const F3 r = crossG<kG>(d, c);
+    const float inv_det = rcp_exact<kU>(dotA<kG>(tr.n, d));
+    const float u = dotA<kG>(r, tr.e2) * inv_det;
+    const float v = dotB<kG>(r, tr.e1) * inv_det;
+    const float w = 1.0f - u - v;
+    const float t = dotA<kG>(tr.n, c) * inv_det;
+    // the conjunction as a chain of selects (VALU) rather than and-ed lane masks (SALU): each stage
+    // passes its next operand only while every earlier comparison held (-1 fails all later ones,
+    // t >= tmin included since tmin > -1; a NaN fails them as the comparison it replaces would)
+    const float x1 = u >= 0 ? v : -1.0f;
+    const float x2 = x1 >= 0 ? w : -1.0f;
+    const float x3 = x2 >= 0 ? t : -1.0f;
+    return __ballot((x3 >= tmin) & (x3 <= tmax));
+}
+
 // Per-ray constants of the ray-box (slab) test and the test of one box.
 //   kRobust = false: FastNodeIntersector (node_intersectors.hpp:83-103): inv = safe_inverse(d)
 //     (vector.hpp:69-74), s = -o * inv, slab = fma(bound, inv, s) -- restated octant-free below.
@@ -278,7 +329,10 @@ __device__ __forceinline__ Slab<kRobust> make_slab(F3 o, F3 d) {
         s.ix = 1.0f / d.x; s.iy = 1.0f / d.y; s.iz = 1.0f / d.z;
         s.sx = pad_ulps2(s.ix); s.sy = pad_ulps2(s.iy); s.sz = pad_ulps2(s.iz);
     } else {
-        auto safe_inv = [](float x) { return 1.0f / (fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
+        // safe_inverse (vector.hpp:69-74): 1 / d, |d| clamped to >= FLT_EPSILON; d is normalized, so the
+        // quotient's argument lies in [FLT_EPSILON, 1 + ulp] (or is NaN, which every slab comparison
+        // rejects whatever its payload): rcp_fast is the IEEE quotient there
+        auto safe_inv = [](float x) { return rcp_fast(fabsf(x) < FLT_EPSILON ? copysignf(FLT_EPSILON, x) : x); };
         s.ix = safe_inv(d.x); s.iy = safe_inv(d.y); s.iz = safe_inv(d.z);
         s.sx = (-o.x) * s.ix; s.sy = (-o.y) * s.iy; s.sz = (-o.z) * s.iz;
     }
@@ -357,7 +411,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     float tmax = FLT_MAX;                                           // ray.hpp:17-21
     bool have = false;
     // kOct -2 = the single-frame kernel's generic loop
-    constexpr bool kU = CERES_RCP_UNIFORM == 1 || (CERES_RCP_UNIFORM == 2 && kOct == -2);
+    constexpr bool kU = CERES_RCP_UNIFORM == 1 || (CERES_RCP_UNIFORM == 2 && kOct == -2) || CERES_RCP_UNIFORM_TRACE;
     if (P.root_leaf_count) {                                          // root is a leaf, :72-73
         if (kStats) n_tests += P.root_leaf_count;
         for (uint32_t k = P.root_leaf_first; k < P.root_leaf_first + P.root_leaf_count; ++k) {
@@ -388,6 +442,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         }
     }
     uint32_t sp = 0;
+    if (CERES_TRI_SELECT && !kAnyHit) best.slot = kNoSlot;
     // Software-pipelined steps: the next record (near child or stack top) follows from this
     // step's box tests alone (the leaf hits only lower tmax for LATER steps, :89-121), so its
     // load is issued before this step's triangle tests and overlaps them.
@@ -424,24 +479,29 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         }
         // leaves of this step, left then right (intersect_leaf on each, :89-107), one loop so a
         // wavefront runs max(left + right) trips rather than max(left) + max(right)
-        uint32_t k = 0, k_end = 0, k2 = 0, k2_end = 0;
-        if (hit_l && L.x) { k = L.y; k_end = L.y + L.x; }
-        if (hit_r && L.z) { k2 = L.w; k2_end = L.w + L.z; }
-        if (kStats) n_tests += (k_end - k) + (k2_end - k2);
+        // (one counter over the left leaf's then the right leaf's triangles: a single loop bound)
+        const uint32_t nl = hit_l ? L.x : 0u, nr = hit_r ? L.z : 0u;
+        const uint32_t n_leaf = nl + nr, k2 = L.w - nl;
+        if (kStats) n_tests += n_leaf;
         float4 nA, nB, nC;                                            // undefined for done lanes
         uint4 nL;
-        if (!done) {
+        if (CERES_LOAD_ALWAYS) {
+            // every lane loads (a done lane the root's pair, cached), so no exec-mask branch
+            const float4* nq = reinterpret_cast<const float4*>(P.pairs + (done ? 0u : nxt));
+            nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
+        } else if (!done) {
             const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
             nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
         }
-        while (k < k_end || k2 < k2_end) {
-            const uint32_t idx = k < k_end ? k++ : k2++;
+        for (uint32_t j = 0; j < n_leaf; ++j) {
+            const uint32_t idx = (j < nl ? L.y : k2) + j;
             float t, u, v;
             if (CERES_TRI_SELECT && !kAnyHit) {                          // closest hit: selects, no branch
+                // (no separate "have" flag: a boolean carried through the loop costs exec-mask
+                // merges at every join; best.slot starts at kNoSlot instead)
                 const bool h = tri_test_u<kG, kU>(P.tris, idx, o, d, tmin, tmax, t, u, v);
                 best.slot = h ? idx : best.slot; best.t = h ? t : best.t;
                 best.u = h ? u : best.u; best.v = h ? v : best.v;
-                have |= h;
                 tmax = h ? t : tmax;
                 continue;
             }
@@ -454,6 +514,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         if (done) break;
         A = nA; B = nB; C = nC; L = nL;
     }
+    if (CERES_TRI_SELECT && !kAnyHit) return best.slot != kNoSlot;
     return have;
 }
 
@@ -653,6 +714,22 @@ __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<fal
             const uint32_t n = n4_count(chw[c]);
             uint64_t lm = cm[c] & ~occ;
             if (!n || !lm) continue;
+            if (CERES_PACKET_LEAN) {
+                // do-while (n > 0 and lm != 0 on entry), the hit mask straight from the compares
+                const Tri48* tp = P.tris + n4_first(chw[c]);
+                uint32_t left = n;
+                while (true) {                                          // two plain exits: no combined predicate
+                    const float4 a = sload_f4(tp, 0), b = sload_f4(tp, 1), g = sload_f4(tp, 2);
+                    __asm__ volatile("" ::"s"(a.x), "s"(b.x), "s"(g.x));
+                    const TriV tr{{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, g.x}, {g.y, g.z, g.w}};
+                    occ |= tri_mask<kG, CERES_RCP_UNIFORM == 1 || CERES_RCP_UNIFORM_PACKET>(tr, o, d, tmin, tmax) & lm;
+                    lm &= ~occ;
+                    if (!lm) break;
+                    if (--left == 0) break;
+                    ++tp;
+                }
+                continue;
+            }
             for (uint32_t k = n4_first(chw[c]), ke = k + n; k < ke && lm; ++k) {
                 float t, u, v;
                 const Tri48* tp = P.tris + k;
@@ -660,7 +737,7 @@ __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<fal
                 // all 48 B in flight before the first use (one scalar-load wait per triangle, not two)
                 __asm__ volatile("" ::"s"(a.x), "s"(b.x), "s"(g.x));
                 const TriV tr{{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, g.x}, {g.y, g.z, g.w}};
-                const bool h = tri_test<kG, CERES_RCP_UNIFORM == 1>(tr, o, d, tmin, tmax, t, u, v);
+                const bool h = tri_test<kG, CERES_RCP_UNIFORM == 1 || CERES_RCP_UNIFORM_PACKET>(tr, o, d, tmin, tmax, t, u, v);
                 occ |= __ballot(h) & lm;
                 lm &= ~occ;
             }
@@ -1162,9 +1239,11 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
             P.rec_tuv[3 * size_t(px) + 2] = hit ? h.v : 0.f;
             P.rec_shadow[px] = -1;
         }
-        if (!hit) {
-            store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);                 // render.hpp:116-117
-        } else {                                                     // render.hpp:127-135
+        // a missed pixel (render.hpp:116-117) is stored with the tile's lit ones, at the end: a
+        // store here would sit in the in-order vector-memory counter ahead of the hit lanes'
+        // triangle fetch below, which would then wait for the store's write acknowledgement
+        if (!CERES_DEFER_MISS_STORE && !hit) store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);
+        if (hit) {                                                   // render.hpp:127-135
             const TriV tr = load_tri(P.tris + h.slot);
             const F3 normal = normalizeG<kG>(tr.n);
             w = make_shadow_ray<kRobust, kG>(hit_point<kG>(tr, normal, h.u, h.v), f3(P.cam[f].sun));
@@ -1191,6 +1270,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
         L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust, kQ, kPacketsCompiled ? -2 : -1, kG>(
                                     P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
     if (hit) finish_pixel<kG>(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
+    else if (CERES_DEFER_MISS_STORE && active) store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);   // render.hpp:116-117
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
         // primary hits, wave primary pairs, wave shadow pairs
@@ -1458,6 +1538,48 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
                 src = g * grp + (wl % 8) * c + (wl / 8) * tpw + i;
             }
             order[p] = mk[src].second;
+        }
+        return upload_tile_order(s, W, H, t, frames, tile, order, stream, out);
+    }
+    const uint32_t tpw_b = uint32_t(CERES_TILES_PER_WAVE);
+    if (CERES_STRIP_ORDER && frames > 1 && tpw_b > 1 && bx >= tpw_b) {
+        // Strips: a wavefront's tpw consecutive order entries are tpw horizontally adjacent tiles
+        // of one row of tiles (a 32x8-pixel strip for 4 tiles per wave), strips centre-first and
+        // shuffled in windows of 64 tiles like single tiles.  A strip's float rows are 384-B runs
+        // (three whole 128-B lines when the row pitch is a multiple of 128 B) written by one
+        // wavefront, instead of 96-B pieces of lines that other wavefronts complete much later in
+        // a batch (each written back twice); its tiles also share BVH paths.  Tiles of a partial
+        // strip (bx not a multiple of tpw) follow all full strips.
+        const uint32_t sx = bx / tpw_b;
+        std::vector<std::pair<double, uint32_t>> sk;
+        sk.reserve(size_t(sx) * by * frames);
+        for (uint32_t f = 0; f < frames; ++f)
+            for (uint32_t y = 0; y < by; ++y) {
+                const size_t lr = std::min<size_t>(size_t(y) * tile + tile / 2, rows - 1);
+                const size_t j = ((lr / t.row_block) * t.world + t.rank) * t.row_block + lr % t.row_block;
+                for (uint32_t x = 0; x < sx; ++x) {
+                    const double dx = (double(x) * tpw_b + 0.5 * tpw_b) * tile - cx, dy = double(j) - cy;
+                    sk.push_back({dx * dx + dy * dy, (f * by + y) * sx + x});
+                }
+            }
+        std::stable_sort(sk.begin(), sk.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+        uint64_t st = 0x9e3779b97f4a7c15ull;
+        const size_t win = std::max<size_t>(1, dev::kTileShuffleWindow / tpw_b);
+        for (size_t b0 = 0; b0 < sk.size(); b0 += win) {
+            const size_t len = std::min<size_t>(win, sk.size() - b0);
+            for (size_t q = len - 1; q > 0; --q) {
+                st = st * 6364136223846793005ull + 1442695040888963407ull;
+                std::swap(sk[b0 + q], sk[b0 + size_t((st >> 33) % (q + 1))]);
+            }
+        }
+        size_t p = 0;
+        for (const auto& e : sk) {
+            const uint32_t fy = e.second / sx, x = e.second - fy * sx;
+            for (uint32_t i = 0; i < tpw_b; ++i) order[p++] = fy * bx + x * tpw_b + i;
+        }
+        for (size_t q = 0; q < n; ++q) {                               // partial strips, centre-first
+            const uint32_t id = k[q].second, x = id % bx;
+            if (x >= sx * tpw_b) order[p++] = id;
         }
         return upload_tile_order(s, W, H, t, frames, tile, order, stream, out);
     }
@@ -1948,7 +2070,11 @@ int ceres_assemble_rgb8_packed(const uint8_t* d_gathered, uint8_t* d_out, uint32
 // 1.32 -> 1.04 ms with 4 bands; at 1080p the bands' own tails cost what the overlap saves (floats
 // +-2 %, RGB8 +60 %), so frames under kBandMinBytes stay one launch.  CERES_HOST_BANDS overrides
 // the count (1 = one launch, then the copy).
-constexpr uint32_t kMaxHostBands = 16;
+// at most half the tile-order cache: each band caches its own order ({rb, k, bands} keys), and a
+// band count near kMaxTileOrders would evict every cached order on each call (each eviction
+// round ends in a bulk free behind a device synchronise)
+constexpr uint32_t kMaxHostBands = 8;
+static_assert(2 * kMaxHostBands <= ceres::kMaxTileOrders, "host bands must leave room in the tile-order cache");
 constexpr size_t kBandMinBytes = size_t(32) << 20;     // below this a frame is one launch (measured: 1080p floats ±2 %, 1080p RGB8 +60 %)
 
 static uint32_t host_bands(size_t W, size_t H, bool pixels, bool rgb8) {
