@@ -108,6 +108,11 @@ struct FrameCam {              // one frame of a batch: eye + the render.hpp:91-
     float eye[3], dir[3], iu[3], iv[3], sun[3];
 };
 
+// A fused-kernel tile-order entry: frame, tile row and tile column in one word (decoded with bit
+// extracts instead of two integer divisions per tile); used when the batch fits the fields.
+constexpr uint32_t kTileXBits = 13, kTileYBits = 13;
+constexpr uint32_t pack_tile(uint32_t f, uint32_t y, uint32_t x) { return (f << (kTileXBits + kTileYBits)) | (y << kTileXBits) | x; }
+
 struct KParams {
     FrameCam cam[kMaxFrames];
     uint32_t frames;                             // frames in this batch (1..kMaxFrames)
@@ -122,6 +127,7 @@ struct KParams {
     uint32_t packets;                            // batch kernel: wave-wide packets (L2-resident scenes, render_hip.hip)
     uint32_t tiles_x;                            // tile columns per row (fused kernel)
     uint32_t lds_entries;                        // fused kernel: LDS stack slots per lane (24-bit planes)
+    uint32_t tile_packed;                        // fused kernel: tile_order entries are pack_tile() words
     const uint32_t* tile_order;                  // fused kernel: block -> batch tile (centre first)
     const SiblingPair* pairs;
     const Node4* nodes4;                         // shadow-ray BVH4 over the same leaf slots

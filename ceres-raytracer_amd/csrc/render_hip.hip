@@ -83,6 +83,18 @@
 #define CERES_RCP_UNIFORM 2                    // rcp_exact's IEEE-division fallback behind a wave-uniform branch
 #endif                                         // (ballot) instead of a divergent one: 0 nowhere, 1 in every
                                                // kernel, 2 in the single-frame kernel only
+#ifndef CERES_TRI_CHAIN
+#define CERES_TRI_CHAIN 0                      // tri_test's predicate as a chain of selects (tmin > -1)
+#endif
+#ifndef CERES_UNIFORM_LOOP
+#define CERES_UNIFORM_LOOP 0                   // trace(): batch-kernel traversal as one wave-uniform loop
+#endif
+#ifndef CERES_TILE_PACKED
+#define CERES_TILE_PACKED 0                    // tile-order entries as bit fields; one-rank row shortcut
+#endif
+#ifndef CERES_FAST_PIXQUOT
+#define CERES_FAST_PIXQUOT 0                   // primary_dir: exact fast quotients (pix_quot, rcp_exact)
+#endif
 #ifndef CERES_PACKET_LEAN
 #define CERES_PACKET_LEAN 0                    // packet leaf loop: do-while, hit masks from ballots
 #endif
@@ -263,6 +275,14 @@ __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin,
         // (u, v, w) pass, and the comparisons (false on NaN) are combined with bitwise ands
         const float t = dotA<kG>(tr.n, c) * inv_det;
         t_out = t; u_out = u; v_out = v;
+        if (CERES_TRI_CHAIN) {
+            // the conjunction as selects (VALU) instead of and-ed lane masks (SALU): each stage passes
+            // its operand on only while the earlier comparisons held; -1 fails every later one (tmin > -1)
+            const float x1 = u >= 0 ? v : -1.0f;
+            const float x2 = x1 >= 0 ? w : -1.0f;
+            const float x3 = x2 >= 0 ? t : -1.0f;
+            return (x3 >= tmin) & (x3 <= tmax);
+        }
         return (u >= 0) & (v >= 0) & (w >= 0) & (t >= tmin) & (t <= tmax);
     }
     if (u >= 0 && v >= 0 && w >= 0) {
@@ -449,6 +469,47 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     const float4* q = reinterpret_cast<const float4*>(P.pairs);       // pair of the root's children (:81)
     float4 A = q[0], B = q[1], C = q[2];
     uint4 L = reinterpret_cast<const uint4*>(q)[3];
+    constexpr bool kUL = CERES_UNIFORM_LOOP && !kAnyHit && !kStats && CERES_TRUST_STACK_BOUND && CERES_TRI_SELECT &&
+                         kOct != -2;
+    if constexpr (kUL) {
+        // The same steps in ONE wave-uniform loop: a lane that has finished keeps stepping without
+        // effect -- its boxes count as missed (no leaf test, no push; sp stays 0, so it stays done)
+        // and it loads the root's pair -- until every lane has finished.  The exit is one ballot
+        // instead of a per-lane exit mask merged into exec every step.
+        bool fin = false;
+        while (true) {
+            const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];
+            float le, lx, re, rx;
+            slab_box<kRobust, kOct>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
+            slab_box<kRobust, kOct>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
+            const bool hit_l = le <= lx && !fin, hit_r = re <= rx && !fin;
+            const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
+            const bool both = go_l && go_r, none = !go_l && !go_r;
+            const bool swap = le > re;
+            const bool done = none && sp == 0;                        // :118-121
+            const uint32_t near = both ? (swap ? L.w : L.y) : (go_l ? L.y : L.w);
+            const uint32_t nxt = done ? 0u : none ? top : near;
+            stk[sp * kS] = swap ? L.y : L.w;                          // a finished lane: slot 0 of its own stack
+            sp = sp + (both ? 1u : 0u) - ((none && sp != 0) ? 1u : 0u);
+            const uint32_t nl = hit_l ? L.x : 0u, nr = hit_r ? L.z : 0u;
+            const uint32_t n_leaf = nl + nr, k2 = L.w - nl;
+            const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
+            const float4 nA = nq[0], nB = nq[1], nC = nq[2];
+            const uint4 nL = reinterpret_cast<const uint4*>(nq)[3];
+            for (uint32_t j = 0; j < n_leaf; ++j) {
+                const uint32_t idx = (j < nl ? L.y : k2) + j;
+                float t, u, v;
+                const bool h = tri_test_u<kG, kU>(P.tris, idx, o, d, tmin, tmax, t, u, v);
+                best.slot = h ? idx : best.slot; best.t = h ? t : best.t;
+                best.u = h ? u : best.u; best.v = h ? v : best.v;
+                tmax = h ? t : tmax;
+            }
+            fin = done;
+            if (__ballot(!done) == 0) break;
+            A = nA; B = nB; C = nC; L = nL;
+        }
+        return best.slot != kNoSlot;
+    }
     while (true) {                                                    // :82-123
         if (kStats) ++n_pairs;
         const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];             // popped if this step descends nowhere
@@ -485,7 +546,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
         if (kStats) n_tests += n_leaf;
         float4 nA, nB, nC;                                            // undefined for done lanes
         uint4 nL;
-        if (CERES_LOAD_ALWAYS) {
+        if (CERES_LOAD_ALWAYS && kOct != -2) {                        // (not the single-frame kernel: measured +1.4 % there)
             // every lane loads (a done lane the root's pair, cached), so no exec-mask branch
             const float4* nq = reinterpret_cast<const float4*>(P.pairs + (done ? 0u : nxt));
             nA = nq[0]; nB = nq[1]; nC = nq[2]; nL = reinterpret_cast<const uint4*>(nq)[3];
@@ -797,20 +858,36 @@ __device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32
 }
 
 __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t lr) {
+    if (CERES_TILE_PACKED && P.world == 1) return lr;                 // one rank: local rows are the frame's rows
     return ((lr / P.row_block) * P.world + P.rank) * P.row_block + lr % P.row_block;
+}
+
+// render.hpp:109-110's 2 * (i + 0.5) / n for image sizes n <= 65536: the quotient a / n as
+// fma(fma(-n, q0, a), r0, q0), q0 = a * r0, r0 = v_rcp_f32(n) -- the correctly rounded quotient
+// for EVERY i < n <= 65536, checked exhaustively (2^31 pairs) on gfx950
+// (tools/probes/pixquot_exhaustive.hip, tests/test_gpu_parity.py); larger n take the division
+// (n is wave-uniform: no divergence)
+__device__ __forceinline__ float pix_quot(uint32_t i, uint32_t n) {
+    const float a = 2 * (float(i) + 0.5f), fn = float(n);
+    if (!CERES_FAST_PIXQUOT || n > 65536u) return a / fn;
+    const float r0 = __builtin_amdgcn_rcpf(fn);
+    const float q0 = a * r0;
+    return __builtin_fmaf(__builtin_fmaf(-fn, q0, a), r0, q0);
 }
 
 // Primary ray direction of pixel (i, j) of frame f, render.hpp:109-111 (GCC: dir + fma(iv, v, iu u)).
 template <bool kG = false>
 __device__ __forceinline__ F3 primary_dir(const KParams& P, uint32_t f, uint32_t i, uint32_t j) {
-    const float u = 2 * (float(i) + 0.5f) / float(P.W) - 1.0f;
-    const float v = 2 * (float(j) + 0.5f) / float(P.H) - 1.0f;
+    const float u = pix_quot(i, P.W) - 1.0f;
+    const float v = pix_quot(j, P.H) - 1.0f;
     const FrameCam& c = P.cam[f];
+    F3 a;
     if constexpr (kG)
-        return normalizeG<kG>(F3{c.dir[0] + __builtin_fmaf(c.iv[0], v, c.iu[0] * u),
-                                 c.dir[1] + __builtin_fmaf(c.iv[1], v, c.iu[1] * u),
-                                 c.dir[2] + __builtin_fmaf(c.iv[2], v, c.iu[2] * u)});
-    else return normalize(f3(c.iu) * u + f3(c.iv) * v + f3(c.dir));
+        a = F3{c.dir[0] + __builtin_fmaf(c.iv[0], v, c.iu[0] * u), c.dir[1] + __builtin_fmaf(c.iv[1], v, c.iu[1] * u),
+               c.dir[2] + __builtin_fmaf(c.iv[2], v, c.iu[2] * u)};
+    else a = f3(c.iu) * u + f3(c.iv) * v + f3(c.dir);
+    if (CERES_FAST_PIXQUOT) return a * rcp_exact<true>(sqrtf(dotA<kG>(a, a)));   // normalize, the quotient via rcp_exact
+    return kG ? normalizeG<kG>(a) : normalize(a);
 }
 
 // Hit point + self-intersection offset, render.hpp:127-133 (p1() = p0 - e1, p2() = p0 + e2).
@@ -1211,9 +1288,16 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     const uint4 tq = q < 4 ? tiles4 : tiles4b;
     const uint32_t qq = q & 3;
     const uint32_t t = kTPW == 1 ? tiles4.x : qq == 0 ? tq.x : qq == 1 ? tq.y : qq == 2 ? tq.z : tq.w;
-    const uint32_t f = t / per_frame;
-    const uint32_t rem = t - f * per_frame;
-    const uint32_t by = rem / P.tiles_x, bx = rem - by * P.tiles_x;
+    uint32_t f, by, bx;
+    if (CERES_TILE_PACKED && P.tile_packed) {                        // bit fields (pack_tile), wave-uniform
+        bx = t & ((1u << kTileXBits) - 1u);
+        by = (t >> kTileXBits) & ((1u << kTileYBits) - 1u);
+        f = t >> (kTileXBits + kTileYBits);
+    } else {
+        f = t / per_frame;
+        const uint32_t rem = t - f * per_frame;
+        by = rem / P.tiles_x; bx = rem - by * P.tiles_x;
+    }
     // lanes in Morton order over the tile: every quad of lanes (4k..4k+3) is a 2x2 pixel block,
     // so the quads the texture addresser processes together hold neighbouring rays (A/B: solo
     // C3 -2.4 %, C5 batches -1.5 %)
@@ -1419,8 +1503,16 @@ int ensure_workspace(ceres_scene* s, size_t px, bool want_px, bool want_rgb) {
 
 // Caches `order` on the scene under its key (see ensure_tile_order) and uploads it.
 int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, uint32_t frames, uint32_t tile,
-                      const std::vector<uint32_t>& order, hipStream_t stream, const uint32_t** out) {
+                      std::vector<uint32_t>& order, hipStream_t stream, const uint32_t** out, bool packed,
+                      uint32_t bx, uint32_t by) {
     const size_t n = order.size();
+    if (packed) {                                                    // linear ids -> pack_tile words
+        const uint32_t per_frame = bx * by;
+        for (auto& id : order) {
+            const uint32_t f = id / per_frame, rem = id - f * per_frame, y = rem / bx;
+            id = pack_tile(f, y, rem - y * bx);
+        }
+    }
     ceres_scene::TileOrder o;
     if (s->orders.size() >= ceres::kMaxTileOrders) {
         auto lru = std::min_element(s->orders.begin(), s->orders.end(),
@@ -1436,6 +1528,7 @@ int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
         }
     }
     o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile;
+    o.packed = packed;
     // padded to a multiple of 8 entries (zeros): the fused kernel reads its tile-order entries
     // up to eight at a time through the scalar cache
     const size_t padded = (n + 7) / 8 * 8;
@@ -1462,10 +1555,10 @@ int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
 // orders; the least recently used one is retired (freed later, see ceres_scene::retired), so
 // eviction neither rewrites an order a launch in flight reads nor stalls the streams.
 int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, size_t rows, uint32_t frames,
-                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out) {
+                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out, bool packed) {
     for (auto& o : s->orders)
         if (o.W == W && o.H == H && o.row_block == t.row_block && o.rank == t.rank && o.world == t.world &&
-            o.frames == frames && o.tile == tile) {
+            o.frames == frames && o.tile == tile && o.packed == packed) {
             o.used = ++s->order_clock;
             *out = o.d;
             return CERES_OK;
@@ -1539,7 +1632,7 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
             }
             order[p] = mk[src].second;
         }
-        return upload_tile_order(s, W, H, t, frames, tile, order, stream, out);
+        return upload_tile_order(s, W, H, t, frames, tile, order, stream, out, packed, bx, by);
     }
     const uint32_t tpw_b = uint32_t(CERES_TILES_PER_WAVE);
     if (CERES_STRIP_ORDER && frames > 1 && tpw_b > 1 && bx >= tpw_b) {
@@ -1581,7 +1674,7 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
             const uint32_t id = k[q].second, x = id % bx;
             if (x >= sx * tpw_b) order[p++] = id;
         }
-        return upload_tile_order(s, W, H, t, frames, tile, order, stream, out);
+        return upload_tile_order(s, W, H, t, frames, tile, order, stream, out, packed, bx, by);
     }
     uint64_t st = 0x9e3779b97f4a7c15ull;
     for (size_t b0 = 0; b0 < n; b0 += dev::kTileShuffleWindow) {
@@ -1591,7 +1684,7 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
             std::swap(order[b0 + q], order[b0 + size_t((st >> 33) % (q + 1))]);
         }
     }
-    return upload_tile_order(s, W, H, t, frames, tile, order, stream, out);
+    return upload_tile_order(s, W, H, t, frames, tile, order, stream, out, packed, bx, by);
 }
 
 // CERES_MODE_QBVH4: the exact shadow BVH4 (Node4) -> compressed QNode4 records.  Per node and
@@ -1738,8 +1831,10 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     constexpr uint32_t ftile = 8;                                    // fused kernel: 8x8 tiles
     const uint32_t fbx = uint32_t((W + ftile - 1) / ftile), fby = uint32_t((rows + ftile - 1) / ftile);
     const uint32_t* tile_order = nullptr;
+    const bool packed = CERES_TILE_PACKED && frames <= (1u << (32 - kTileXBits - kTileYBits)) &&
+                        fbx <= (1u << kTileXBits) && fby <= (1u << kTileYBits);
     if (full && rows)
-        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order)) return rc;
+        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order, packed)) return rc;
     // The shards must start at zero when they are read back (counters) or count primary-only hits;
     // the fused kernel without counters only adds to them, so its steady-state frames skip the
     // memset (ceres_finalize re-zeroes them after every counted render).
@@ -1756,6 +1851,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
             P.lds_entries = uint32_t(std::max(s->stack_entries + 1, s->shadow_stack_entries));
             const size_t flds = size_t(P.lds_entries) * dev::kFusedB * stw;
             P.tile_order = tile_order;
+            P.tile_packed = packed ? 1u : 0u;
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
             // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
@@ -1844,7 +1940,7 @@ namespace ceres {
 int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out) {
     const ceres_tiling t{uint32_t(H), 0, 1};
     return ensure_tile_order(s, W, H, t, H, 1, uint32_t((W + tile - 1) / tile), uint32_t((H + tile - 1) / tile), tile,
-                             stream, out);
+                             stream, out, false);
 }
 }  // namespace ceres
 
