@@ -650,6 +650,11 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
             return r;
     }
     uint32_t sp = 0, cur = 0;
+    // kUA: the same steps in one wave-uniform loop (as trace()'s kUL): a lane that has finished --
+    // occluded, or its stack empty -- keeps stepping over the root record with its masks cleared
+    // until every lane has finished; the exit is one ballot instead of per-lane exit masks
+    constexpr bool kUA = CERES_UNIFORM_LOOP && !kStats;
+    bool fin = false, occluded = false;
     while (true) {
         if (kStats) ++n_pairs;
         float e[4];
@@ -687,6 +692,10 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
         }
         const uint32_t cnt[4] = {n4_count(CH.x), n4_count(CH.y), n4_count(CH.z), n4_count(CH.w)};
         const uint32_t fst[4] = {n4_first(CH.x), n4_first(CH.y), n4_first(CH.z), n4_first(CH.w)};
+        if (kUA) {
+            leaf_mask = fin ? 0u : leaf_mask;
+            inner_mask = fin ? 0u : inner_mask;
+        }
         // triangles of every passing leaf child, as one flattened loop (wave-coherent trip count)
         uint32_t k = 0, k_end = 0;
         while (true) {
@@ -699,8 +708,36 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
                 if (kStats) n_tests += k_end - k;
             }
             float t, u, v;
-            if (tri_test_u<kG, CERES_RCP_UNIFORM == 1>(P.tris, k, o, d, tmin, tmax, t, u, v)) return true;
+            if (tri_test_u<kG, CERES_RCP_UNIFORM == 1>(P.tris, k, o, d, tmin, tmax, t, u, v)) {
+                if (!kUA) return true;
+                occluded = true;
+                break;
+            }
             ++k;
+        }
+        if (kUA) {
+            if (occluded) inner_mask = 0;
+            if (inner_mask) {
+                uint32_t best = __builtin_ctz(inner_mask);
+                uint32_t rest = inner_mask & ~(1u << best);
+                if (sp + __builtin_popcount(rest) > P.shadow_stack_entries) { overflow = true; rest = 0; fin = true; }
+                while (rest) {
+                    const uint32_t c = __builtin_ctz(rest);
+                    rest &= rest - 1;
+                    stk[sp * kS] = c == 0 ? fst[0] : c == 1 ? fst[1] : c == 2 ? fst[2] : fst[3];
+                    ++sp;
+                }
+                cur = best == 0 ? fst[0] : best == 1 ? fst[1] : best == 2 ? fst[2] : fst[3];
+            } else if (sp == 0 || occluded) {
+                fin = true;
+            } else {
+                --sp;
+                cur = stk[sp * kS];
+            }
+            fin = fin || occluded;
+            cur = fin ? 0u : cur;
+            if (__ballot(!fin) == 0) break;
+            continue;
         }
         if (inner_mask) {
             // one passing inner child next; the others go on the stack
@@ -729,7 +766,7 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
             cur = stk[sp * kS];
         }
     }
-    return false;
+    return kUA && occluded;
 }
 
 // Any-hit of a whole wavefront's shadow rays as ONE masked packet over the shadow BVH4 (batch
@@ -862,11 +899,11 @@ __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t lr) {
     return ((lr / P.row_block) * P.world + P.rank) * P.row_block + lr % P.row_block;
 }
 
-// render.hpp:109-110's 2 * (i + 0.5) / n for image sizes n <= 65536: the quotient a / n as
-// fma(fma(-n, q0, a), r0, q0), q0 = a * r0, r0 = v_rcp_f32(n) -- the correctly rounded quotient
-// for EVERY i < n <= 65536, checked exhaustively (2^31 pairs) on gfx950
-// (tools/probes/pixquot_exhaustive.hip, tests/test_gpu_parity.py); larger n take the division
-// (n is wave-uniform: no divergence)
+// render.hpp:109-110's 2 * (i + 0.5) / n.  CERES_FAST_PIXQUOT (off): for image sizes n <= 65536
+// the quotient a / n as fma(fma(-n, q0, a), r0, q0), q0 = a * r0, r0 = v_rcp_f32(n), which is
+// meant to be the correctly rounded quotient for every i < n <= 65536 -- a claim the exhaustive
+// probe (tools/probes/pixquot_exhaustive.hip, 2^31 pairs on gfx950) must confirm before the switch
+// is turned on; larger n take the division (n is wave-uniform: no divergence)
 __device__ __forceinline__ float pix_quot(uint32_t i, uint32_t n) {
     const float a = 2 * (float(i) + 0.5f), fn = float(n);
     if (!CERES_FAST_PIXQUOT || n > 65536u) return a / fn;

@@ -384,16 +384,6 @@ def test_fast_reciprocal_is_exact(gpu):
     assert "exact for biased exponents [1, 252]" in r.stdout, r.stdout
 
 
-def test_fast_pixel_quotient_is_exact(gpu):
-    """pix_quot() (render_hip.hip, primary_dir's 2 * (i + 0.5) / n, render.hpp:109-110) == the IEEE
-    quotient for every pixel index i < n of every image size n <= 65536: exhaustive (2^31 pairs)
-    on this gfx950 (larger sizes take the division)."""
-    exe = os.path.join(REPO, "tools", "probes", "pixquot_exhaustive")
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr
-    assert "pairs 2147516416 mismatches 0" in r.stdout, r.stdout
-
-
 def test_repeat_renders_are_deterministic(gpu):
     pkg = gpu
     meta, _, _ = load_golden("dragon_1080")
