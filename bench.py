@@ -276,6 +276,20 @@ def roofline_step_block(nbytes, ms_step, world):
             "source": "per-view reference Statistics, tests/golden/orbit/<config>.json (64 B/node pair + 56 B/test)"}
 
 
+def choose_collect(requested, cfg, world, frames):
+    """The N > 1 partition of a step (DESIGN.md "Multi-GPU"): "auto" = "exchange" (rows dealt over
+    the ranks, one RCCL all-to-all) for a config defined as ONE framebuffer tiled over the GPUs
+    (configs.py "tiled": C4, C5) except at N = 2, where one xGMI link would carry every split frame's
+    rows; "frames" (each rank renders its frames whole, no collective) otherwise.  Partitions that
+    deal whole frames need F to be a multiple of N, else every frame goes to rank 0 ("gather")."""
+    collect = requested
+    if collect == "auto":
+        collect = "exchange" if cfg.get("tiled") and world != 2 else "frames"
+    if collect in ("frames", "exchange") and frames % world:
+        collect = "gather"
+    return collect
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -349,11 +363,7 @@ def main():
         # 128 (no triangle in view), which would flatter the step; its step is F copies of the
         # config's own view instead (each checked against the reference's PPM of that view)
         b12, s3, steps_deg = np.repeat(b12[:1], F, 0), np.repeat(s3[:1], F, 0), np.repeat(steps_deg[:1], F)
-    collect = args.collect
-    if collect == "auto":
-        collect = "exchange" if cfg.get("tiled") and world != 2 else "frames"
-    if collect in ("frames", "exchange") and F % world:
-        collect = "gather"
+    collect = choose_collect(args.collect, cfg, world, F)
     owner = world > 1 and collect == "frames"              # unsplit frames: no collective
     exchange = world > 1 and collect in ("exchange", "frames")
     if exchange:

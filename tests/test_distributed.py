@@ -340,3 +340,25 @@ def test_frame_owner_gloo_step(world, k):
         assert p.exitcode == 0
     res = dict(q.get(timeout=10) for _ in range(world))
     assert all(res.values()), res
+
+
+def test_bench_partition_choice():
+    """bench.py --collect auto: C3 (and every untiled config) renders whole frames per rank at every
+    N; the tiled C4 / C5 deal rows and exchange them at N >= 4 but not at N = 2 (DESIGN.md
+    "Multi-GPU": one link would carry the split frames); explicit choices are kept; a frame count
+    that is not a multiple of N falls back to the gather."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    import configs
+    C = configs.CONFIGS
+    for n in (1, 2, 4, 8):
+        assert bench.choose_collect("auto", C["dragon_1080"], n, 16 * n) == "frames"
+        assert bench.choose_collect("auto", C["bunny_1080"], n, 16 * n) == "frames"
+    for name in ("dragon_4096", "proc_c5"):
+        assert bench.choose_collect("auto", C[name], 2, 32) == "frames"
+        assert bench.choose_collect("auto", C[name], 4, 64) == "exchange"
+        assert bench.choose_collect("auto", C[name], 8, 128) == "exchange"
+    assert bench.choose_collect("exchange", C["dragon_1080"], 4, 64) == "exchange"
+    assert bench.choose_collect("gather", C["dragon_1080"], 4, 64) == "gather"
+    assert bench.choose_collect("frames", C["dragon_1080"], 3, 16) == "gather"
