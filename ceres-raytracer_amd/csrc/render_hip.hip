@@ -899,11 +899,12 @@ __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t lr) {
     return ((lr / P.row_block) * P.world + P.rank) * P.row_block + lr % P.row_block;
 }
 
-// render.hpp:109-110's 2 * (i + 0.5) / n.  CERES_FAST_PIXQUOT (off): for image sizes n <= 65536
-// the quotient a / n as fma(fma(-n, q0, a), r0, q0), q0 = a * r0, r0 = v_rcp_f32(n), which is
-// meant to be the correctly rounded quotient for every i < n <= 65536 -- a claim the exhaustive
-// probe (tools/probes/pixquot_exhaustive.hip, 2^31 pairs on gfx950) must confirm before the switch
-// is turned on; larger n take the division (n is wave-uniform: no divergence)
+// render.hpp:109-110's 2 * (i + 0.5) / n.  CERES_FAST_PIXQUOT (off until measured): for image
+// sizes n <= 65536 the quotient a / n as fma(fma(-n, q0, a), r0, q0), q0 = a * r0,
+// r0 = v_rcp_f32(n) -- the correctly rounded quotient for every i < n <= 65536 and every r0 within
+// one ulp of 1/n, i.e. whatever the hardware estimate returns (proved by exhaustion on the CPU:
+// tests/test_pixquot_proof.py, 6.4e9 cases; tools/probes/pixquot_exhaustive.hip re-checks it on
+// gfx950); larger n take the division (n is wave-uniform: no divergence)
 __device__ __forceinline__ float pix_quot(uint32_t i, uint32_t n) {
     const float a = 2 * (float(i) + 0.5f), fn = float(n);
     if (!CERES_FAST_PIXQUOT || n > 65536u) return a / fn;
