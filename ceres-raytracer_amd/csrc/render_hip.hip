@@ -99,7 +99,8 @@
 #define CERES_PACKET_LEAN 0                    // packet leaf loop: do-while, hit masks from ballots
 #endif
 #ifndef CERES_LOAD_ALWAYS
-#define CERES_LOAD_ALWAYS 0                    // trace(): finished lanes load a (cached) record too -- no branch
+#define CERES_LOAD_ALWAYS 1                    // trace(): finished lanes load a (cached) record too -- no branch
+                                               // (batch kernel; A/B profiles/r04/s4 "ldall": batches -0.7..-1.5 %)
 #endif
 #ifndef CERES_RCP_UNIFORM_TRACE
 #define CERES_RCP_UNIFORM_TRACE 0              // ... and in every primary (closest-hit) traversal
