@@ -4,27 +4,28 @@
 Workload (default): C3 = dragon.obj 1920x1080, primary + shadow rays, static.cpp camera
 (static.cpp:38-47,72-73) -- the configuration BASELINE.json's metric is quoted on.
 
-A step renders F frames (F = --frames, default = 16 per GPU): views of the anim.cpp:76-88 orbit
-of the C3 camera + sun about z, frame f rotated once by f x 360 / F degrees (frame 0 = C3
-exactly).  At N = 1 a step is sixteen C3-size frames 22.5 degrees apart; at N GPUs it is 16N
-distinct frames over the same turn, 22.5/N degrees apart (pkg.bench_views) -- WEAK scaling,
-sixteen frames' work per GPU from the same orbit at every N (one batch launch per 64 frames).
-Every one of those views has its reference PPM sha256 and rays/hits in
-tests/golden/orbit/<config>.json (made by the reference's own render(), make_golden.py --orbit),
-and every frame the validation step assembles is checked against it.
+A step renders F frames (F = --frames, default = 16 per GPU).  --views config (default): every
+frame is the config's own view -- for dragon_1080 the C3 camera + sun with the fixture's pinned
+basis bits, so `value` is C3 itself.  --views orbit: frame f is the anim.cpp:76-88 orbit of that
+camera + sun about z, rotated once by f x 360 / F degrees (pkg.bench_views); reported beside the
+headline as `orbit_value` (a lighter mix on dragon: fewer shadow rays per frame).  WEAK scaling:
+sixteen frames' work per GPU at every N (one batch launch per 64 frames).  Every view has its
+reference PPM sha256 and rays/hits in tests/golden/orbit/<config>.json (made by the reference's
+own render(), make_golden.py --orbit), and every frame the validation step assembles is checked
+against it.
 At N > 1 (--collect, default auto):
-  frames    the frames are the units: rank q renders orbit frames q, q + N, q + 2N, ... (16 of the
-            16N) whole, with one ceres_render_batch_device launch, into its own HBM -- no
-            collective, nothing on the xGMI links (frames are independent: render.hpp:104-153);
-  exchange  every frame's rows are interleaved over the ranks in blocks of --row-block rows; each
-            rank renders its rows of all F frames, then ONE RCCL all-to-all per step gathers each
-            frame to its owner rank (rank q owns the same 16 frames as above) and
-            ceres_assemble_rgb8_packed un-interleaves them -- the tiled framebuffer of BASELINE's
-            C4 ("framebuffer tiled across 8x MI355X with RCCL gather");
+  exchange  the framebuffer partition BASELINE.json's north star names: every frame's rows are
+            interleaved over the ranks in blocks of --row-block rows; each rank renders its rows of
+            all F frames, then ONE RCCL all-to-all per step gathers each frame to its owner rank
+            (rank q owns 16 frames) and ceres_assemble_rgb8_packed un-interleaves them;
+  frames    rank q renders frames q, q + N, q + 2N, ... (16 of the 16N) whole, with one
+            ceres_render_batch_device launch, into its own HBM -- no collective (frames are
+            independent: render.hpp:104-153);
   gather    rows interleaved, all F frames to rank 0.
-  auto = exchange for configs defined as a tiled framebuffer (configs.py "tiled": C4) except at
-  N = 2, where the exchange would put 16 frames' worth of rows on one xGMI link per step and
-  outlast the render (DESIGN.md "Multi-GPU"); frames otherwise.
+  auto = exchange, except for the tiled 4096^2 / 4K configs (C4, C5) at N = 2, where the single
+  xGMI link would carry 16 split frames' rows per step and outlast the render (DESIGN.md
+  "Multi-GPU"): frames there, reported as untiled.  The other partition of the same step is timed
+  too and reported as `partition_alt`; the line carries the world size and backend RCCL ran with.
 RGB8 + float framebuffers in HBM.  Steps rotate over --streams HIP streams (own buffers each):
 the collective/assembly of step k and the tail of its render overlap later steps; the timed
 region ends when every step's frames are assembled.
@@ -40,7 +41,7 @@ contraction-free reference (-ffp-contract=off), checked against its PPMs.
 
 Also reported (rank 0):
   roofline      the dominant kernel AS THE STEP RUNS IT: one ceres_render_batch_device launch of 16
-                of the step's orbit views (whole frames), launched back to back on ONE stream
+                of the step's views (whole frames; 16 copies of C3 by default), launched back to back on ONE stream
                 between two HIP events (mean launch duration = per-kernel evidence, comparable
                 with a single-stream rocprofv3 trace).  achieved = the launch's ALGORITHMIC bytes
                 (pinned reference statistics per view, tests/golden/orbit/<cfg>.json, SURVEY.md
@@ -54,8 +55,8 @@ Also reported (rank 0):
                 / ms_per_step, per GPU, priced against the L2 and against HBM (steps overlap on
                 --streams streams, so this is a throughput, not a launch duration).
   roofline_solo one whole frame of frame 0's view per launch (the latency regime), as `roofline`.
-  c3_only       the same timed loop with all F frames = the C3 view itself (the orbit mix is
-                lighter: fewer shadow rays per frame), value + shadow-ray fractions of both.
+  orbit         the same timed loop over the orbit views (`orbit_value`), value + shadow-ray fraction.
+  partition_alt N > 1: the same step under the other partition (frames <-> exchange).
   cpu_baseline  the REFERENCE hot path (oracle/_ref/ref_render, reference CMake flags) timed
                 on this host's cores on a bounded sample of the same workload (N = 1 only);
                 falls back to the oracle restatement if the reference binary is absent.
@@ -277,17 +278,83 @@ def roofline_step_block(nbytes, ms_step, world):
 
 
 def choose_collect(requested, cfg, world, frames):
-    """The N > 1 partition of a step (DESIGN.md "Multi-GPU"): "auto" = "exchange" (rows dealt over
-    the ranks, one RCCL all-to-all) for a config defined as ONE framebuffer tiled over the GPUs
-    (configs.py "tiled": C4, C5) except at N = 2, where one xGMI link would carry every split frame's
-    rows; "frames" (each rank renders its frames whole, no collective) otherwise.  Partitions that
+    """The N > 1 partition of a step (DESIGN.md "Multi-GPU"): "auto" = "exchange" -- every frame's
+    rows dealt over the ranks and gathered with ONE RCCL all-to-all per step, the framebuffer
+    partition BASELINE.json's north star names -- at every N, except for a config defined as a
+    4096^2 / 4K framebuffer (configs.py "tiled": C4, C5) at N = 2, where the single xGMI link would
+    carry 16 split frames' rows per step and outlast the render (C4 1.23x); there each
+    rank renders its frames whole ("frames", no collective, reported as untiled).  Partitions that
     deal whole frames need F to be a multiple of N, else every frame goes to rank 0 ("gather")."""
     collect = requested
     if collect == "auto":
-        collect = "exchange" if cfg.get("tiled") and world != 2 else "frames"
+        collect = "frames" if cfg.get("tiled") and world == 2 else "exchange"
     if collect in ("frames", "exchange") and frames % world:
         collect = "gather"
     return collect
+
+
+def alt_collect(collect):
+    """The other partition bench.py reports beside the headline one at N > 1 (`partition_alt`)."""
+    return "frames" if collect in ("exchange", "gather") else "exchange"
+
+
+def result_line(*, config_name, cfg, world, backend, collect, views_kind, F, steps, warmup, T, rays_step,
+                hits_step, full_mode, row_block, streams, float_fb, arith, roofline, roofline_step, roofline_solo,
+                cpu, parity, alt=None, orbit=None):
+    """bench.py's one JSON line (rank 0).  `T` = max-over-ranks wall seconds of the `steps` timed
+    steps; value = the whole job's rays per second."""
+    W, H = cfg["W"], cfg["H"]
+    primary_step = F * W * H
+    value = rays_step * steps / T / 1e6
+    untiled = world > 1 and collect == "frames"
+    line = {
+        "metric": "Mrays/sec (primary+shadow) on dragon.obj 1920x1080; 1/2/4/8-GPU scaling"
+        if config_name == "dragon_1080" else f"Mrays/sec ({config_name})",
+        "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(T / steps * 1e3, 5), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "arith": arith,
+        "world_size": world, "backend": backend,
+        "data": ("real mesh from the reference repo (data/%s)" % cfg["obj"] if cfg["obj"] else
+                 "procedural %dx%d-vertex heightfield generated in-process (SURVEY.md §8(d) C5 definition)"
+                 % (cfg["proc"], cfg["proc"]))
+                + ("; every frame = the config camera (static.cpp:39-47 for C3)" if views_kind == "config" else
+                   "; frame 0 = the config camera, frames 1.. = the anim.cpp-style orbit about z"),
+        "config": {"workload": f"{config_name}: {cfg['obj'] or 'proc'} {W}x{H} "
+                               f"{'primary+shadow' if full_mode else 'primary only'}, "
+                               + (f"{F} copies of the config view per step" if views_kind == "config"
+                                  else f"{F} orbit frame(s) per step"),
+                   "views": views_kind,
+                   "W": W, "H": H, "frames_per_step": F, "rays_per_step": rays_step, "hits_per_step": hits_step,
+                   "shadow_ray_frac": round((rays_step - primary_step) / rays_step, 4) if full_mode else 0.0,
+                   "row_block": row_block if world > 1 and not untiled else H,
+                   "parallelism": (f"untiled: unsplit frames x{world}, rank q renders frames q, q+{world}, ... "
+                                   "whole, no collective" if untiled else
+                                   f"framebuffer rows interleaved over {world} GPU(s) in blocks of {row_block} rows"
+                                   + ((" + one RCCL all-to-all per step: frame f gathered to its owner rank "
+                                       "(pipelined)" if collect == "exchange" else
+                                       " + one RCCL gather per step to rank 0 (pipelined)")
+                                      if world > 1 else "")
+                                   if world > 1 else "one GPU, whole frames"),
+                   "collect": collect if world > 1 else None,
+                   "float_framebuffer": float_fb, "streams": streams},
+        # the step's one collective against the xGMI budget (DESIGN.md "Multi-GPU"): bytes one rank
+        # receives per step, 1/N of them from each peer over that peer's direct link (one link per
+        # peer in a fully connected 8-GPU node) at 76.8 GB/s per link and direction
+        "collective": None if world == 1 or untiled else {
+            "kind": "all_to_all" if collect == "exchange" else "gather",
+            "recv_bytes_per_rank_step": (world - 1) * (F // world if collect == "exchange" else F) * H * 3 * W
+            // world,
+            "xgmi_link_ms_est": round((F // world if collect == "exchange" else F) * H * 3 * W / world / 76.8e6, 4),
+            "ms_per_step": round(T / steps * 1e3, 5)},
+        "roofline": roofline, "roofline_step": roofline_step,
+        "roofline_solo": roofline_solo, "cpu_baseline": cpu, "parity": parity,
+    }
+    if alt is not None:
+        line["partition_alt"] = alt
+    if orbit is not None:
+        line["orbit_value"] = orbit["value"]
+        line["orbit"] = orbit
+    return line
 
 
 def main():
@@ -297,21 +364,25 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="dragon_1080")
     ap.add_argument("--frames", type=int, default=0,
-                    help="orbit frames per step (default: --frames-per-gpu x number of GPUs)")
+                    help="frames per step (default: --frames-per-gpu x number of GPUs)")
     ap.add_argument("--frames-per-gpu", type=int, default=16,
                     help="frames of work per GPU per step when --frames is not given (weak scaling)")
+    ap.add_argument("--views", choices=("config", "orbit"), default="config",
+                    help="config: every frame of the step is the config's own view (C3 = static.cpp's camera, "
+                         "the headline); orbit: frame f = the anim.cpp orbit view f x 360/F degrees about z")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--no-view0-only", action="store_true",
-                    help="skip the second timed loop with every frame = frame 0's view (C3 itself)")
+    ap.add_argument("--no-orbit", action="store_true",
+                    help="skip the second timed loop over the orbit views (`orbit_value`)")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="N > 1: skip the timed loop of the other partition (`partition_alt`)")
     ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
     ap.add_argument("--collect", choices=("auto", "frames", "exchange", "gather"), default="auto",
-                    help="N > 1: frames = unsplit frames, each rank renders its F/N frames whole (no collective); "
-                         "exchange = every frame's rows dealt over the ranks, each frame gathered to one owner rank "
-                         "in one all-to-all; gather = rows dealt, all frames to rank 0; auto = exchange for "
-                         "configs defined as a tiled framebuffer (C4) except at N = 2, where one link would carry "
-                         "it (DESIGN.md \"Multi-GPU\"), else frames")
+                    help="N > 1: exchange = every frame's rows dealt over the ranks, each frame gathered to one "
+                         "owner rank in one RCCL all-to-all; frames = each rank renders its F/N frames whole (no "
+                         "collective); gather = rows dealt, all frames to rank 0; auto = exchange, except frames "
+                         "for the tiled C4/C5 at N = 2 (DESIGN.md \"Multi-GPU\")")
     ap.add_argument("--prime-s", type=float, default=0.3,
                     help="untimed setup: seconds of steps before the W warmup steps (GPU clock ramp)")
     ap.add_argument("--streams", type=int, default=8,
@@ -342,12 +413,14 @@ def main():
     torch.cuda.set_device(dev_id)
     dev = torch.device("cuda", dev_id)
     local_rank = dev_id
+    backend = None
     if world > 1:
         backend = os.environ.get("CERES_BENCH_BACKEND", "nccl")      # gloo: shared-GPU rehearsal only
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
+        world = dist.get_world_size()
 
     W, H = cfg["W"], cfg["H"]
     F = args.frames or args.frames_per_gpu * world
@@ -355,182 +428,193 @@ def main():
     arith = pkg.ARITH_FMA if build == "ref" else pkg.ARITH_EXACT
     mesh, bvh, cam = pkg.prepare(cfg, arith=arith)
     scene = pkg.Scene(mesh, bvh, device=local_rank)
-    # F views of the orbit, frame f rotated once by f x 360 / F degrees (frame 0 = C3, fixture bits)
-    b12, s3, steps_deg = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=pinned_basis(meta, cfg, cam, build))
-    view0_step = bool(cfg.get("bench_view0"))
-    if view0_step:
-        # C5: the orbit about z through the origin leaves the [0,1]^2 heightfield for views 40..96 of
-        # 128 (no triangle in view), which would flatter the step; its step is F copies of the
-        # config's own view instead (each checked against the reference's PPM of that view)
-        b12, s3, steps_deg = np.repeat(b12[:1], F, 0), np.repeat(s3[:1], F, 0), np.repeat(steps_deg[:1], F)
-    collect = choose_collect(args.collect, cfg, world, F)
-    owner = world > 1 and collect == "frames"              # unsplit frames: no collective
-    exchange = world > 1 and collect in ("exchange", "frames")
-    if exchange:
-        # batch order for the all-to-all: rank q owns batch frames q*k .. q*k+k-1, which are orbit
-        # frames q, q + N, q + 2N, ... (batch frame 0 = orbit frame 0 = C3)
-        order = D.exchange_order(F, world)
-        b12, s3, steps_deg = b12[order], s3[order], steps_deg[order]
+    # the orbit: frame f rotated once by f x 360 / F degrees (frame 0 = the config view, fixture bits)
+    ob12, os3, osteps = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=pinned_basis(meta, cfg, cam, build))
+    # C5's z orbit leaves the [0,1]^2 heightfield for views 40..96 of 128 (no triangle in view), so
+    # its orbit is never a bench step; every config's headline step is F copies of its own view
+    views_kind = "config" if cfg.get("bench_view0") else args.views
+
+    def view_set(kind):
+        if kind == "config":
+            return np.repeat(ob12[:1], F, 0), np.repeat(os3[:1], F, 0), np.repeat(osteps[:1], F)
+        return ob12, os3, osteps
+
     mode = pkg.cfg_mode(cfg, arith)
     full_mode = (mode & 0xf) == pkg.MODE_FULL
-    row_block = args.row_block if world > 1 and not owner else H
-    tiling = pkg.Tiling(row_block, rank, world) if not owner else pkg.Tiling(H, 0, 1)
     S = max(1, args.streams)
-    job_steps = steps_deg                        # the whole job's views, in batch order
-    Fl = F                                       # frames this rank's launches render
-    if owner:        # rank q renders batch frames q*k .. q*k+k-1 whole
-        gather = D.FrameOwner(W, H, rank, world, frames=F, device=dev, slots=max(2, S))
-        mine_f = gather.owned_frames()
-        Fl = len(mine_f)
-        b12_all, s3_all = b12, s3
-        b12, s3, steps_deg = b12[mine_f], s3[mine_f], steps_deg[mine_f]
-    elif exchange:   # each frame to one owner rank: a rank's ingress is (N-1)/N of its k frames per step
-        gather = D.FrameExchange(W, H, row_block, rank, world, frames=F, device=dev, slots=max(2, S))
-    else:            # every frame -> rank 0
-        gather = D.BatchGather(W, H, row_block, rank, world, frames=F, device=dev, slots=max(2, S))
-    rows = gather.local_rows
-    d_px = [None if args.no_float else torch.empty(Fl * 3 * W * max(rows, 1), dtype=torch.float32, device=dev)
-            for _ in range(S)]
-    counters = torch.zeros(8, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    # steps rotate over S streams, each with its own framebuffers / gather slot: a step's frames
+    # steps rotate over S streams, each with its own framebuffers / collective slot: a step's frames
     # are complete when its stream is, and step k+1's kernel fills the tail of step k (a single
     # frame ends with a few long wavefronts resident, DESIGN.md "Where the time goes")
     streams = [stream] if S == 1 else [torch.cuda.Stream(device=dev) for _ in range(S)]
     slots = max(2, S)
-    pending = [False] * slots
-
     MAXF = 64                                    # frames per ceres_render_batch_device launch (kMaxFrames)
-    chunk_counters = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range((Fl + MAXF - 1) // MAXF)]
-    views = {"b12": b12, "s3": s3, "steps": steps_deg,       # what this rank renders every step
-             "job": job_steps}                               # ... and the whole step's views (batch order)
 
-    def render(slot, st, with_counters=False):
-        # one launch per (at most) 64 frames of the step; frame f's rows at f * 3 * W * rows
-        px = d_px[slot % S]
-        fb = 3 * W * max(rows, 1)
-        vb, vs = views["b12"], views["s3"]
-        for c, f0 in enumerate(range(0, Fl, MAXF)):
-            f1 = min(Fl, f0 + MAXF)
-            scene.render_batch_device(vb[f0:f1], vs[f0:f1], W, H, mode=mode, tiling=tiling,
-                                      d_pixels=0 if px is None else px.data_ptr() + 4 * fb * f0,
-                                      d_rgb8=gather.local_ptr(slot) + fb * f0,
-                                      d_counters=chunk_counters[c].data_ptr() if with_counters else 0,
-                                      stream=st.cuda_stream)
-        if with_counters:
+    class Run:
+        """One partition of the step over the ranks (`collect`) and one set of views, with its
+        framebuffers and collective slots: validate() and timed() as the bench contract says."""
+
+        def __init__(self, collect, kind):
+            self.collect, self.kind = collect, kind
+            b12, s3, steps_deg = view_set(kind)
+            self.owner = world > 1 and collect == "frames"              # unsplit frames: no collective
+            self.exchange = world > 1 and collect in ("exchange", "frames")
+            if self.exchange:
+                # batch order for the all-to-all: rank q owns batch frames q*k .. q*k+k-1, which are
+                # orbit frames q, q + N, q + 2N, ... (batch frame 0 = orbit frame 0 = the config view)
+                order = D.exchange_order(F, world)
+                b12, s3, steps_deg = b12[order], s3[order], steps_deg[order]
+            self.row_block = args.row_block if world > 1 and not self.owner else H
+            self.tiling = pkg.Tiling(self.row_block, rank, world) if not self.owner else pkg.Tiling(H, 0, 1)
+            self.job = steps_deg                     # the whole job's views, in batch order
+            self.Fl = F                              # frames this rank's launches render
+            if self.owner:
+                self.gather = D.FrameOwner(W, H, rank, world, frames=F, device=dev, slots=slots)
+                mine = self.gather.owned_frames()
+                self.Fl = len(mine)
+                b12, s3 = b12[mine], s3[mine]
+            elif self.exchange:   # each frame to one owner rank: a rank's ingress is (N-1)/N of its k frames
+                self.gather = D.FrameExchange(W, H, self.row_block, rank, world, frames=F, device=dev, slots=slots)
+            else:                 # every frame -> rank 0
+                self.gather = D.BatchGather(W, H, self.row_block, rank, world, frames=F, device=dev, slots=slots)
+            self.b12, self.s3 = b12, s3
+            self.rows = self.gather.local_rows
+            self.d_px = [None if args.no_float else
+                         torch.empty(self.Fl * 3 * W * max(self.rows, 1), dtype=torch.float32, device=dev)
+                         for _ in range(S)]
+            self.pending = [False] * slots
+            self.chunk_counters = [torch.zeros(8, dtype=torch.int64, device=dev)
+                                   for _ in range((self.Fl + MAXF - 1) // MAXF)]
+            self.counters = torch.zeros(8, dtype=torch.int64, device=dev)
+
+        def render(self, slot, st, with_counters=False):
+            # one launch per (at most) 64 frames of the step; frame f's rows at f * 3 * W * rows
+            px = self.d_px[slot % S]
+            fb = 3 * W * max(self.rows, 1)
+            for c, f0 in enumerate(range(0, self.Fl, MAXF)):
+                f1 = min(self.Fl, f0 + MAXF)
+                scene.render_batch_device(self.b12[f0:f1], self.s3[f0:f1], W, H, mode=mode, tiling=self.tiling,
+                                          d_pixels=0 if px is None else px.data_ptr() + 4 * fb * f0,
+                                          d_rgb8=self.gather.local_ptr(slot) + fb * f0,
+                                          d_counters=self.chunk_counters[c].data_ptr() if with_counters else 0,
+                                          stream=st.cuda_stream)
+            if with_counters:
+                with torch.cuda.stream(st):
+                    cs = torch.stack(self.chunk_counters)
+                    self.counters.copy_(torch.cat([cs[:, :6].sum(0), cs[:, 6:7].max(0).values, cs[:, 7:].sum(0)]))
+
+        def step(self, k):
+            slot = k % slots
+            st = streams[k % S]
             with torch.cuda.stream(st):
-                cs = torch.stack(chunk_counters)
-                counters.copy_(torch.cat([cs[:, :6].sum(0), cs[:, 6:7].max(0).values, cs[:, 7:].sum(0)]))
+                if self.pending[slot]:             # the previous use of this slot (step k - slots)
+                    self.gather.finish(slot)
+                    self.pending[slot] = False
+                self.render(slot, st)
+                self.gather.start(slot)
+                self.pending[slot] = True
+                if S == 1:                         # one stream: complete the previous step's gather now
+                    prev = (k - 1) % slots
+                    if self.pending[prev] and prev != slot:
+                        self.gather.finish(prev)
+                        self.pending[prev] = False
 
-    def step(k):
-        slot = k % slots
-        st = streams[k % S]
-        with torch.cuda.stream(st):
-            if pending[slot]:                  # the previous use of this slot (step k - slots)
-                gather.finish(slot)
-                pending[slot] = False
-            render(slot, st)
-            gather.start(slot)
-            pending[slot] = True
-            if S == 1:                         # one stream: complete the previous step's gather now
-                prev = (k - 1) % slots
-                if pending[prev] and prev != slot:
-                    gather.finish(prev)
-                    pending[prev] = False
+        def drain(self):
+            for k_ in range(slots):
+                if self.pending[k_]:
+                    with torch.cuda.stream(streams[k_ % S]):
+                        self.gather.finish(k_)
+                    self.pending[k_] = False
+            self.gather.wait_assembled()
 
-    def drain():
-        for k_ in range(slots):
-            if pending[k_]:
-                with torch.cuda.stream(streams[k_ % S]):
-                    gather.finish(k_)
-                pending[k_] = False
-        gather.wait_assembled()
-
-    def validate():
-        """Untimed: one counted step of the current views.  Returns (rays, hits, checks) where checks
-        compares every frame this rank assembled with the REFERENCE's PPM of the same view
-        (tests/golden/orbit/<config>.json; sha256 of "P6 W H 255\n" + body, static.cpp:135-147)
-        and the step's rays / hits with the reference's per-view counts (render.hpp:155)."""
-        render(0, stream, with_counters=True)
-        gather.start(0)
-        full = gather.finish(0)
-        gather.wait_assembled()
-        torch.cuda.synchronize(dev)
-        c = counters.clone()
-        if world > 1:
-            dist.all_reduce(c)
-        c = c.cpu().numpy()
-        if c[6]:
-            # ceres_finalize's error word: a traversal stack overflowed (single_ray_traverser.hpp:29
-            # asserts instead), so some frame of the batch is wrong -- never time a wrong render
-            raise SystemExit(f"bench.py: traversal stack overflow in the validation batch (error word {int(c[6]):#x})")
-        mine = (list(zip(gather.owned_frames(), full)) if exchange
-                else ([(f, full[f]) for f in range(F)] if rank == 0 else []))
-        head = b"P6 %d %d 255\n" % (W, H)
-        n = [0, 0, 0]                                            # [checked, matched, unpinned]
-        for f, body in mine:
-            e = None if orbit_fx is None else view_entry(orbit_fx.get(step_key(views["job"][f])), build)
-            if e is None:
-                n[2] += 1
-                continue
-            n[0] += 1
-            n[1] += int(hashlib.sha256(head + body.cpu().numpy().tobytes()).hexdigest() == e["sha256"])
-        stat = torch.tensor(n, dtype=torch.int64, device=dev)
-        if world > 1:
-            dist.all_reduce(stat)
-        stat = stat.cpu().numpy()
-        keys = [None if orbit_fx is None else view_entry(orbit_fx.get(step_key(x)), build) for x in views["job"]]
-        ref_rays = sum(e["rays"] for e in keys) if all(keys) else None
-        ref_hits = sum(e["hits"] for e in keys) if all(keys) else None
-        checks = {"frames": F, "frames_checked": int(stat[0]), "frames_unpinned": int(stat[2]),
-                  "all_frames_match_reference": bool(stat[2] == 0 and stat[1] == stat[0] == F),
-                  "step_rays_match_reference": None if ref_rays is None else int(c[0]) == ref_rays,
-                  "step_hits_match_reference": None if ref_hits is None else int(c[1]) == ref_hits}
-        return int(c[0]), int(c[1]), checks
-
-    def timed(prime):
-        """W warmup steps (after >= --prime-s of untimed steps when `prime`), then exactly K steps
-        between barrier + device synchronise; returns the max-over-ranks wall time."""
-        if prime:
-            # untimed setup before the W warmup steps: steps over every stream and collective slot
-            # for at least --prime-s seconds, so no stream's first launch lands in the timed region
-            # when W < S and the GPU has left its idle clock state (measured: K = 20 after W = 5
-            # from a cold start ran 6 % below the same K after W = 200; after this priming they agree)
-            t_prime = time.perf_counter()
-            for k in range(slots):
-                step(k)
-            drain()
+        def validate(self):
+            """Untimed: one counted step.  Returns (rays, hits, checks) where checks compares every
+            frame this rank assembled with the REFERENCE's PPM of the same view
+            (tests/golden/orbit/<config>.json; sha256 of "P6 W H 255\\n" + body, static.cpp:135-147)
+            and the step's rays / hits with the reference's per-view counts (render.hpp:155)."""
+            self.render(0, stream, with_counters=True)
+            self.gather.start(0)
+            full = self.gather.finish(0)
+            self.gather.wait_assembled()
             torch.cuda.synchronize(dev)
-            per_step = max((time.perf_counter() - t_prime) / slots, 1e-5)
-            # the same number of steps on every rank (each step is a collective)
-            more = torch.tensor([min(20000, max(0, int(args.prime_s / per_step) - slots))], dtype=torch.int64,
-                                device=dev)
+            c = self.counters.clone()
             if world > 1:
-                dist.all_reduce(more, op=dist.ReduceOp.MAX)
-            for k in range(int(more.item())):
-                step(slots + k)
-            drain()
+                dist.all_reduce(c)
+            c = c.cpu().numpy()
+            if c[6]:
+                # ceres_finalize's error word: a traversal stack overflowed (single_ray_traverser.hpp:29
+                # asserts instead), so some frame of the batch is wrong -- never time a wrong render
+                raise SystemExit(f"bench.py: traversal stack overflow in the validation batch (error word {int(c[6]):#x})")
+            mine = (list(zip(self.gather.owned_frames(), full)) if self.exchange
+                    else ([(f, full[f]) for f in range(F)] if rank == 0 else []))
+            head = b"P6 %d %d 255\n" % (W, H)
+            n = [0, 0, 0]                                            # [checked, matched, unpinned]
+            for f, body in mine:
+                e = None if orbit_fx is None else view_entry(orbit_fx.get(step_key(self.job[f])), build)
+                if e is None:
+                    n[2] += 1
+                    continue
+                n[0] += 1
+                n[1] += int(hashlib.sha256(head + body.cpu().numpy().tobytes()).hexdigest() == e["sha256"])
+            stat = torch.tensor(n, dtype=torch.int64, device=dev)
+            if world > 1:
+                dist.all_reduce(stat)
+            stat = stat.cpu().numpy()
+            keys = [None if orbit_fx is None else view_entry(orbit_fx.get(step_key(x)), build) for x in self.job]
+            ref_rays = sum(e["rays"] for e in keys) if all(keys) else None
+            ref_hits = sum(e["hits"] for e in keys) if all(keys) else None
+            checks = {"frames": F, "frames_checked": int(stat[0]), "frames_unpinned": int(stat[2]),
+                      "all_frames_match_reference": bool(stat[2] == 0 and stat[1] == stat[0] == F),
+                      "step_rays_match_reference": None if ref_rays is None else int(c[0]) == ref_rays,
+                      "step_hits_match_reference": None if ref_hits is None else int(c[1]) == ref_hits}
+            return int(c[0]), int(c[1]), checks
+
+        def timed(self, prime):
+            """W warmup steps (after >= --prime-s of untimed steps when `prime`), then exactly K steps
+            between barrier + device synchronise; returns the max-over-ranks wall time."""
+            if prime:
+                # untimed setup before the W warmup steps: steps over every stream and collective slot
+                # for at least --prime-s seconds, so no stream's first launch lands in the timed region
+                # when W < S and the GPU has left its idle clock state (measured: K = 20 after W = 5
+                # from a cold start ran 6 % below the same K after W = 200; after this priming they agree)
+                t_prime = time.perf_counter()
+                for k in range(slots):
+                    self.step(k)
+                self.drain()
+                torch.cuda.synchronize(dev)
+                per_step = max((time.perf_counter() - t_prime) / slots, 1e-5)
+                # the same number of steps on every rank (each step is a collective)
+                more = torch.tensor([min(20000, max(0, int(args.prime_s / per_step) - slots))], dtype=torch.int64,
+                                    device=dev)
+                if world > 1:
+                    dist.all_reduce(more, op=dist.ReduceOp.MAX)
+                for k in range(int(more.item())):
+                    self.step(slots + k)
+                self.drain()
+                torch.cuda.synchronize(dev)
+            for k in range(args.warmup):
+                self.step(k)
+            self.drain()
             torch.cuda.synchronize(dev)
-        for k in range(args.warmup):
-            step(k)
-        drain()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            step(k)
-        drain()
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        if world > 1:
-            dist.barrier()
-        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        return float(elapsed.item())
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for k in range(args.steps):
+                self.step(k)
+            self.drain()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            if world > 1:
+                dist.barrier()
+            elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+            return float(elapsed.item())
+
+        def close(self):
+            self.d_px = self.gather = None
 
     def step_bytes(steps):
         """Algorithmic bytes of one step's frames (whole job), from every view's pinned reference
@@ -542,55 +626,77 @@ def main():
             return None
         return int(sum(algorithmic_bytes(e["stats"]) for e in es))
 
-    # validation step of the orbit views (not timed): exact counts + every frame vs the reference
-    rays_step, hits_step, orbit_checks = validate()
+    primary_step = F * W * H
+
+    def loop_block(run, rays, hits, checks, T):
+        return {"value": round(rays * args.steps / T / 1e6, 3), "unit": "Mrays/s",
+                "ms_per_step": round(T / args.steps * 1e3, 5), "rays_per_step": rays, "hits_per_step": hits,
+                "shadow_ray_frac": round((rays - primary_step) / rays, 4) if full_mode else 0.0,
+                "roofline_step": roofline_step_block(step_bytes(run.job), T / args.steps * 1e3, world),
+                "parity": checks}
+
+    collect = choose_collect(args.collect, cfg, world, F)
+    main_run = Run(collect, views_kind)
+    # validation step (not timed): exact counts + every frame vs the reference
+    rays_step, hits_step, step_checks = main_run.validate()
     parity = None
     if rank == 0 and meta is not None:
-        parity = {}
-        # frame 0's ray / hit counts (render.hpp:155) from a counted whole-frame render
+        # frame 0's ray / hit counts (render.hpp:155) from a counted whole-frame render of the config view
         c0 = torch.zeros(8, dtype=torch.int64, device=dev)
         rgb0 = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
-        scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=pkg.Tiling(H, 0, 1), d_rgb8=rgb0.data_ptr(),
+        scene.render_device(ob12[0], os3[0], W, H, mode=mode, tiling=pkg.Tiling(H, 0, 1), d_rgb8=rgb0.data_ptr(),
                             d_counters=c0.data_ptr(), stream=sh)
         torch.cuda.synchronize(dev)
         c0 = c0.cpu().numpy()
         body = b"P6 %d %d 255\n" % (W, H) + rgb0.view(H, 3 * W).cpu().numpy().tobytes()
-        parity.update(reference_build="reference CMake flags (-O3 -mavx2 -mfma, GCC FMA contraction)" if build == "ref"
-                      else "reference with -ffp-contract=off",
-                      frame0_ppm_sha256_matches_reference=hashlib.sha256(body).hexdigest() == meta["ppm_sha256"][build],
-                      rays_match=int(c0[0]) == meta[build]["rays"], hits_match=int(c0[1]) == meta[build]["hits"])
-    if parity is not None:
-        parity.update(orbit_checks)
+        parity = {"reference_build": "reference CMake flags (-O3 -mavx2 -mfma, GCC FMA contraction)" if build == "ref"
+                  else "reference with -ffp-contract=off",
+                  "frame0_ppm_sha256_matches_reference": hashlib.sha256(body).hexdigest() == meta["ppm_sha256"][build],
+                  "rays_match": int(c0[0]) == meta[build]["rays"], "hits_match": int(c0[1]) == meta[build]["hits"]}
+        parity.update(step_checks)
 
-    T = timed(prime=True)
-    value = rays_step * args.steps / T / 1e6
-    bytes_step = step_bytes(views["job"])
-    primary_step = F * W * H
-    view0 = None
-    if not args.no_view0_only and not view0_step:
-        # the same loop with every frame = frame 0's view (C3 itself for dragon_1080): the orbit mix
-        # has fewer shadow rays per frame than C3, so report both
-        v0b, v0s, v0d = (b12_all[:1], s3_all[:1], job_steps[:1]) if owner else (b12[:1], s3[:1], steps_deg[:1])
-        views.update(b12=np.repeat(v0b, Fl, 0), s3=np.repeat(v0s, Fl, 0), steps=np.repeat(v0d, Fl),
-                     job=np.repeat(v0d, F))
-        rays0, hits0, checks0 = validate()
-        T0 = timed(prime=False)
-        b0 = step_bytes(views["job"])
-        view0 = {"value": round(rays0 * args.steps / T0 / 1e6, 3), "unit": "Mrays/s",
-                 "roofline_step": roofline_step_block(b0, T0 / args.steps * 1e3, world),
-                 "ms_per_step": round(T0 / args.steps * 1e3, 5), "rays_per_step": rays0, "hits_per_step": hits0,
-                 "shadow_ray_frac": round((rays0 - primary_step) / rays0, 4) if full_mode else 0.0,
-                 "parity": checks0}
+    T = main_run.timed(prime=True)
+    bytes_step = step_bytes(main_run.job)
+    main_run.close()
+    del main_run
+    torch.cuda.empty_cache()
+
+    alt = None
+    if world > 1 and not args.no_alt:
+        # the other partition of the same step, same views (frames <-> exchange)
+        acol = choose_collect(alt_collect(collect), cfg, world, F)
+        if acol != collect:
+            run = Run(acol, views_kind)
+            r_, h_, ch_ = run.validate()
+            Ta = run.timed(prime=True)
+            alt = dict(collect=acol, **loop_block(run, r_, h_, ch_, Ta))
+            run.close()
+            del run
+            torch.cuda.empty_cache()
+
+    orbit = None
+    if views_kind == "config" and not args.no_orbit and not cfg.get("bench_view0"):
+        # the same loop over the anim.cpp orbit views (frame f turned f x 360/F degrees about z): lighter
+        # than the config view on dragon (fewer shadow rays per frame), reported beside it
+        run = Run(collect, "orbit")
+        r_, h_, ch_ = run.validate()
+        To = run.timed(prime=False)
+        orbit = loop_block(run, r_, h_, ch_, To)
+        run.close()
+        del run
+        torch.cuda.empty_cache()
 
     roofline = roofline_solo = None
     cpu = None
     if rank == 0 and not args.no_roofline and meta is not None:
-        # the step's kernel: one 16-frame launch of the step's first 16 orbit views (whole frames),
-        # n_b launches back to back on ONE stream between two HIP events -- no other stream's work
-        # overlaps, so the mean is a per-launch duration (and agrees with a single-stream trace)
+        # the step's kernel: one 16-frame launch of the step's views (whole frames; views_kind
+        # "config": 16 copies of the config view), n_b launches back to back on ONE stream between two
+        # HIP events -- no other stream's work overlaps, so the mean is a per-launch duration (and
+        # agrees with a single-stream trace of tools/batch_launch.py)
         nb_f = min(16, F)
-        vb12, vs3, vsteps = b12[np.argsort(steps_deg)][:nb_f], s3[np.argsort(steps_deg)][:nb_f], \
-            np.sort(steps_deg)[:nb_f]
+        vb12, vs3, vsteps = view_set(views_kind)
+        order = np.argsort(vsteps, kind="stable")[:nb_f]
+        vb12, vs3, vsteps = vb12[order], vs3[order], vsteps[order]
         bat_rgb = torch.empty(nb_f * 3 * W * H, dtype=torch.uint8, device=dev)
         bat_px = None if args.no_float else torch.empty(nb_f * 3 * W * H, dtype=torch.float32, device=dev)
         whole = pkg.Tiling(H, 0, 1)
@@ -612,26 +718,30 @@ def main():
         bb = step_bytes(vsteps)
         kname = "ceres_fused" if full_mode else "ceres_primary"
         if bb is not None:
+            pmc_views = "" if views_kind == "config" else "_orbit"
             roofline = roofline_block(kname, bb, batch_ms,
-                                      pmc_entry(args.config, f"{kname}_batch{nb_f}_{args.arith}"),
+                                      pmc_entry(args.config, f"{kname}_batch{nb_f}{pmc_views}_{args.arith}"),
                                       scene.info()["device_bytes"])
-            roofline.update(launch=f"ceres_render_batch_device, {nb_f} orbit views (steps {vsteps[0]:g}..{vsteps[-1]:g} "
-                                   f"deg), whole {W}x{H} frames, {n_b} launches back to back on one stream",
-                            frames_per_launch=nb_f)
-        # dominant kernel, timed live with HIP events on the launch stream (one full frame, this GPU)
+            what = (f"{nb_f} copies of the config view" if views_kind == "config" else
+                    f"{nb_f} orbit views (steps {vsteps[0]:g}..{vsteps[-1]:g} deg)")
+            roofline.update(launch=f"ceres_render_batch_device, {what}, whole {W}x{H} frames, {n_b} launches "
+                                   f"back to back on one stream", frames_per_launch=nb_f, views=views_kind)
+        del bat_rgb, bat_px
+        # one full frame per launch (the render() call's regime), timed live with HIP events on the
+        # launch stream
         solo = pkg.Tiling(H, 0, 1)
         solo_rgb = torch.empty(3 * W * H, dtype=torch.uint8, device=dev)
         solo_px = torch.empty(3 * W * H, dtype=torch.float32, device=dev)
         n_t = max(10, min(args.steps, 200))
         for _ in range(3):                            # the solo frame's tile order, warm
-            scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
+            scene.render_device(ob12[0], os3[0], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
                                 d_rgb8=solo_rgb.data_ptr(), stream=sh)
         # n_t back-to-back launches between two HIP events on their stream: mean launch duration
         # (per-launch event pairs would add each launch's dispatch latency, ~13 us here)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record(stream)
         for _ in range(n_t):
-            scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
+            scene.render_device(ob12[0], os3[0], W, H, mode=mode, tiling=solo, d_pixels=solo_px.data_ptr(),
                                 d_rgb8=solo_rgb.data_ptr(), stream=sh)
         ev1.record(stream)
         torch.cuda.synchronize(dev)
@@ -647,50 +757,15 @@ def main():
         if roofline is None:
             roofline = roofline_solo
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.config, cfg, rays_step if F == 1 else meta[build]["rays"], build=build)
+        cpu = cpu_baseline(args.config, cfg, meta[build]["rays"] if meta else rays_step // F, build=build)
 
     if rank == 0:
-        line = {
-            "metric": "Mrays/sec (primary+shadow) on dragon.obj 1920x1080; 1/2/4/8-GPU scaling"
-            if args.config == "dragon_1080" else f"Mrays/sec ({args.config})",
-            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(T / args.steps * 1e3, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "arith": args.arith,
-            "data": ("real mesh from the reference repo (data/%s)" % cfg["obj"] if cfg["obj"] else
-                     "procedural %dx%d-vertex heightfield generated in-process (SURVEY.md §8(d) C5 definition)"
-                     % (cfg["proc"], cfg["proc"]))
-                    + ("; every frame = the config camera" if view0_step else
-                       "; frame 0 = the config camera, frames 1.. = the anim.cpp-style orbit about z"),
-            "config": {"workload": f"{args.config}: {cfg['obj'] or 'proc'} {W}x{H} "
-                                   f"{'primary+shadow' if full_mode else 'primary only'}, "
-                                   + (f"{F} copies of the config view per step" if view0_step
-                                      else f"{F} orbit frame(s) per step"),
-                       "W": W, "H": H, "frames_per_step": F, "rays_per_step": rays_step, "hits_per_step": hits_step,
-                       "shadow_ray_frac": round((rays_step - primary_step) / rays_step, 4)
-                       if full_mode else 0.0,
-                       "row_block": row_block,
-                       "parallelism": (f"unsplit frames x{world}: rank q renders orbit frames q, q+{world}, ... whole, "
-                                       "no collective" if owner else
-                                       f"row-interleaved frames x{world}"
-                                       + ((" + one RCCL all-to-all per step: frame f gathered to rank f (pipelined)"
-                                           if exchange else " + one RCCL gather per step to rank 0 (pipelined)")
-                                          if world > 1 else "")),
-                       "collect": collect if world > 1 else None,
-                       "float_framebuffer": d_px[0] is not None, "streams": S},
-            # the step's one collective against the xGMI budget (DESIGN.md "Multi-GPU"): bytes one rank
-            # receives per step, 1/N of them from each peer over that peer's direct link (one link per
-            # peer in a fully connected 8-GPU node) at 76.8 GB/s per link and direction
-            "collective": None if world == 1 or owner else {
-                "kind": "all_to_all" if exchange else "gather",
-                "recv_bytes_per_rank_step": (world - 1) * (F // world if exchange else F) * H * 3 * W // world,
-                "xgmi_link_ms_est": round((F // world if exchange else F) * H * 3 * W / world / 76.8e6, 4),
-                "ms_per_step": round(T / args.steps * 1e3, 5)},
-            "roofline": roofline, "roofline_step": roofline_step_block(bytes_step, T / args.steps * 1e3, world),
-            "roofline_solo": roofline_solo, "cpu_baseline": cpu, "parity": parity,
-        }
-        if view0 is not None:
-            line["c3_only_value" if args.config == "dragon_1080" else "view0_only_value"] = view0["value"]
-            line["view0_only"] = view0
+        line = result_line(config_name=args.config, cfg=cfg, world=world, backend=backend, collect=collect,
+                           views_kind=views_kind, F=F, steps=args.steps, warmup=args.warmup, T=T,
+                           rays_step=rays_step, hits_step=hits_step, full_mode=full_mode, row_block=args.row_block,
+                           streams=S, float_fb=not args.no_float, arith=args.arith, roofline=roofline,
+                           roofline_step=roofline_step_block(bytes_step, T / args.steps * 1e3, world),
+                           roofline_solo=roofline_solo, cpu=cpu, parity=parity, alt=alt, orbit=orbit)
         print(json.dumps(line), flush=True)
     scene.close()
     if world > 1:

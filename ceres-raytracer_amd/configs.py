@@ -71,6 +71,9 @@ CONFIGS = {
     # step_deg about the axis (the bench's weak-scaling frames are this orbit about z)
     "dragon_orbit3_333x217": _cfg(_DRAGON, W=333, H=217, orbit=((0.0, 0.0, 1.0), 45.0, 3)),
     "bunny_orbit7_160x120": _cfg(_BUNNY, W=160, H=120, orbit=((0.0, 1.0, 0.0), 6.0, 7)),
+    # rotate_triangles<2> (render.hpp:24-44 about z): the z axis's contraction sites --
+    # the bunny turned in the image plane
+    "bunny_rotz_160x120": _cfg(_BUNNY, W=160, H=120, rotate=("z", 37.0)),
     # RobustNodeIntersector traversal (node_intersectors.hpp:54-79): odd sizes
     # give exactly axis-aligned view rays (inverse +-inf), the sun on the y axis axis-aligned
     # shadow rays; reference = the harness's render loop with the library's robust intersector

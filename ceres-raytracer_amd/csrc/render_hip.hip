@@ -51,9 +51,6 @@
 #ifndef CERES_FRAME_MAJOR_PIXELS
 #define CERES_FRAME_MAJOR_PIXELS (1u << 22)    // batches of frames of >= this many pixels: frame after frame (0: never)
 #endif
-#ifndef CERES_SHADOW_NEAREST_BATCH
-#define CERES_SHADOW_NEAREST_BATCH 0           // batch any-hit BVH4 steps: 1 = descend into the nearest passing child,
-#endif                                        // 0 = into the first (A/B: C3 batches -1.6 %, dragon 4096^2 -1.4 %)
 #ifndef CERES_SPLIT_UNIFORM
 #define CERES_SPLIT_UNIFORM 1                  // wave-uniform triangle / BVH4 fetches get their own copy of the test
 #endif
@@ -83,33 +80,9 @@
 #define CERES_RCP_UNIFORM 2                    // rcp_exact's IEEE-division fallback behind a wave-uniform branch
 #endif                                         // (ballot) instead of a divergent one: 0 nowhere, 1 in every
                                                // kernel, 2 in the single-frame kernel only
-#ifndef CERES_TRI_CHAIN
-#define CERES_TRI_CHAIN 0                      // tri_test's predicate as a chain of selects (tmin > -1)
-#endif
-#ifndef CERES_UNIFORM_LOOP
-#define CERES_UNIFORM_LOOP 0                   // trace(): batch-kernel traversal as one wave-uniform loop
-#endif
-#ifndef CERES_TILE_PACKED
-#define CERES_TILE_PACKED 0                    // tile-order entries as bit fields; one-rank row shortcut
-#endif
-#ifndef CERES_FAST_PIXQUOT
-#define CERES_FAST_PIXQUOT 0                   // primary_dir: exact fast quotients (pix_quot, rcp_exact)
-#endif
-#ifndef CERES_PACKET_LEAN
-#define CERES_PACKET_LEAN 0                    // packet leaf loop: do-while, hit masks from ballots
-#endif
 #ifndef CERES_LOAD_ALWAYS
 #define CERES_LOAD_ALWAYS 1                    // trace(): finished lanes load a (cached) record too -- no branch
                                                // (batch kernel; A/B profiles/r04/s4 "ldall": batches -0.7..-1.5 %)
-#endif
-#ifndef CERES_RCP_UNIFORM_TRACE
-#define CERES_RCP_UNIFORM_TRACE 0              // ... and in every primary (closest-hit) traversal
-#endif
-#ifndef CERES_RCP_UNIFORM_PACKET
-#define CERES_RCP_UNIFORM_PACKET 0             // ... and in the shadow packets' triangle tests
-#endif
-#ifndef CERES_STRIP_ORDER
-#define CERES_STRIP_ORDER 0                    // batches: a wavefront's tiles = one horizontal strip (ensure_tile_order)
 #endif
 #ifndef CERES_DEFER_MISS_STORE
 #define CERES_DEFER_MISS_STORE 1               // missed pixels stored at the end of the tile (fused kernel)
@@ -276,15 +249,13 @@ __device__ __forceinline__ bool tri_test(const TriV& tr, F3 o, F3 d, float tmin,
         // (u, v, w) pass, and the comparisons (false on NaN) are combined with bitwise ands
         const float t = dotA<kG>(tr.n, c) * inv_det;
         t_out = t; u_out = u; v_out = v;
-        if (CERES_TRI_CHAIN) {
-            // the conjunction as selects (VALU) instead of and-ed lane masks (SALU): each stage passes
-            // its operand on only while the earlier comparisons held; -1 fails every later one (tmin > -1)
-            const float x1 = u >= 0 ? v : -1.0f;
-            const float x2 = x1 >= 0 ? w : -1.0f;
-            const float x3 = x2 >= 0 ? t : -1.0f;
-            return (x3 >= tmin) & (x3 <= tmax);
-        }
-        return (u >= 0) & (v >= 0) & (w >= 0) & (t >= tmin) & (t <= tmax);
+        // the conjunction as selects (VALU) instead of and-ed lane masks (SALU): each stage passes
+        // its operand on only while the earlier comparisons held; -1 fails every later one (tmin > -1;
+        // round 5 A/B: batches -0.2..-0.4 %)
+        const float x1 = u >= 0 ? v : -1.0f;
+        const float x2 = x1 >= 0 ? w : -1.0f;
+        const float x3 = x2 >= 0 ? t : -1.0f;
+        return (x3 >= tmin) & (x3 <= tmax);
     }
     if (u >= 0 && v >= 0 && w >= 0) {
         const float t = dotA<kG>(tr.n, c) * inv_det;
@@ -432,7 +403,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     float tmax = FLT_MAX;                                           // ray.hpp:17-21
     bool have = false;
     // kOct -2 = the single-frame kernel's generic loop
-    constexpr bool kU = CERES_RCP_UNIFORM == 1 || (CERES_RCP_UNIFORM == 2 && kOct == -2) || CERES_RCP_UNIFORM_TRACE;
+    constexpr bool kU = CERES_RCP_UNIFORM == 1 || (CERES_RCP_UNIFORM == 2 && kOct == -2);
     if (P.root_leaf_count) {                                          // root is a leaf, :72-73
         if (kStats) n_tests += P.root_leaf_count;
         for (uint32_t k = P.root_leaf_first; k < P.root_leaf_first + P.root_leaf_count; ++k) {
@@ -470,47 +441,6 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     const float4* q = reinterpret_cast<const float4*>(P.pairs);       // pair of the root's children (:81)
     float4 A = q[0], B = q[1], C = q[2];
     uint4 L = reinterpret_cast<const uint4*>(q)[3];
-    constexpr bool kUL = CERES_UNIFORM_LOOP && !kAnyHit && !kStats && CERES_TRUST_STACK_BOUND && CERES_TRI_SELECT &&
-                         kOct != -2;
-    if constexpr (kUL) {
-        // The same steps in ONE wave-uniform loop: a lane that has finished keeps stepping without
-        // effect -- its boxes count as missed (no leaf test, no push; sp stays 0, so it stays done)
-        // and it loads the root's pair -- until every lane has finished.  The exit is one ballot
-        // instead of a per-lane exit mask merged into exec every step.
-        bool fin = false;
-        while (true) {
-            const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];
-            float le, lx, re, rx;
-            slab_box<kRobust, kOct>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
-            slab_box<kRobust, kOct>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
-            const bool hit_l = le <= lx && !fin, hit_r = re <= rx && !fin;
-            const bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
-            const bool both = go_l && go_r, none = !go_l && !go_r;
-            const bool swap = le > re;
-            const bool done = none && sp == 0;                        // :118-121
-            const uint32_t near = both ? (swap ? L.w : L.y) : (go_l ? L.y : L.w);
-            const uint32_t nxt = done ? 0u : none ? top : near;
-            stk[sp * kS] = swap ? L.y : L.w;                          // a finished lane: slot 0 of its own stack
-            sp = sp + (both ? 1u : 0u) - ((none && sp != 0) ? 1u : 0u);
-            const uint32_t nl = hit_l ? L.x : 0u, nr = hit_r ? L.z : 0u;
-            const uint32_t n_leaf = nl + nr, k2 = L.w - nl;
-            const float4* nq = reinterpret_cast<const float4*>(P.pairs + nxt);
-            const float4 nA = nq[0], nB = nq[1], nC = nq[2];
-            const uint4 nL = reinterpret_cast<const uint4*>(nq)[3];
-            for (uint32_t j = 0; j < n_leaf; ++j) {
-                const uint32_t idx = (j < nl ? L.y : k2) + j;
-                float t, u, v;
-                const bool h = tri_test_u<kG, kU>(P.tris, idx, o, d, tmin, tmax, t, u, v);
-                best.slot = h ? idx : best.slot; best.t = h ? t : best.t;
-                best.u = h ? u : best.u; best.v = h ? v : best.v;
-                tmax = h ? t : tmax;
-            }
-            fin = done;
-            if (__ballot(!done) == 0) break;
-            A = nA; B = nB; C = nC; L = nL;
-        }
-        return best.slot != kNoSlot;
-    }
     while (true) {                                                    // :82-123
         if (kStats) ++n_pairs;
         const uint32_t top = stk[(sp ? sp - 1 : 0) * kS];             // popped if this step descends nowhere
@@ -583,7 +513,7 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
 // Any-hit traversal of the shadow BVH4 (build_shadow_bvh4): result-identical to trace<true>
 // (see the equivalence argument there).  Per step: one 128-B record, four slab tests with the
 // same fma/min/max restatement as trace(), the triangles of every passing leaf, then descend
-// into one passing inner child (the first, CERES_SHADOW_NEAREST_BATCH) and push the others.  The
+// into one passing inner child (the first) and push the others.  The
 // order only changes how soon an occluder is found, never whether one is.
 struct N4 { float4 lx, hx, ly, hy, lz, hz; uint4 ch; };   // ch: packed child words (Node4::child)
 __device__ __forceinline__ N4 load_n4(const Node4* n) {
@@ -651,11 +581,6 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
             return r;
     }
     uint32_t sp = 0, cur = 0;
-    // kUA: the same steps in one wave-uniform loop (as trace()'s kUL): a lane that has finished --
-    // occluded, or its stack empty -- keeps stepping over the root record with its masks cleared
-    // until every lane has finished; the exit is one ballot instead of per-lane exit masks
-    constexpr bool kUA = CERES_UNIFORM_LOOP && !kStats;
-    bool fin = false, occluded = false;
     while (true) {
         if (kStats) ++n_pairs;
         float e[4];
@@ -693,10 +618,6 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
         }
         const uint32_t cnt[4] = {n4_count(CH.x), n4_count(CH.y), n4_count(CH.z), n4_count(CH.w)};
         const uint32_t fst[4] = {n4_first(CH.x), n4_first(CH.y), n4_first(CH.z), n4_first(CH.w)};
-        if (kUA) {
-            leaf_mask = fin ? 0u : leaf_mask;
-            inner_mask = fin ? 0u : inner_mask;
-        }
         // triangles of every passing leaf child, as one flattened loop (wave-coherent trip count)
         uint32_t k = 0, k_end = 0;
         while (true) {
@@ -709,49 +630,14 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
                 if (kStats) n_tests += k_end - k;
             }
             float t, u, v;
-            if (tri_test_u<kG, CERES_RCP_UNIFORM == 1>(P.tris, k, o, d, tmin, tmax, t, u, v)) {
-                if (!kUA) return true;
-                occluded = true;
-                break;
-            }
+            if (tri_test_u<kG, CERES_RCP_UNIFORM == 1>(P.tris, k, o, d, tmin, tmax, t, u, v)) return true;
             ++k;
-        }
-        if (kUA) {
-            if (occluded) inner_mask = 0;
-            if (inner_mask) {
-                uint32_t best = __builtin_ctz(inner_mask);
-                uint32_t rest = inner_mask & ~(1u << best);
-                if (sp + __builtin_popcount(rest) > P.shadow_stack_entries) { overflow = true; rest = 0; fin = true; }
-                while (rest) {
-                    const uint32_t c = __builtin_ctz(rest);
-                    rest &= rest - 1;
-                    stk[sp * kS] = c == 0 ? fst[0] : c == 1 ? fst[1] : c == 2 ? fst[2] : fst[3];
-                    ++sp;
-                }
-                cur = best == 0 ? fst[0] : best == 1 ? fst[1] : best == 2 ? fst[2] : fst[3];
-            } else if (sp == 0 || occluded) {
-                fin = true;
-            } else {
-                --sp;
-                cur = stk[sp * kS];
-            }
-            fin = fin || occluded;
-            cur = fin ? 0u : cur;
-            if (__ballot(!fin) == 0) break;
-            continue;
         }
         if (inner_mask) {
             // one passing inner child next; the others go on the stack
             // (any order gives the same answer; the nearest-first choice costs its selects in every
             // step and the batch regime is issue-bound, so batches take the first passing child)
-            uint32_t best = __builtin_ctz(inner_mask);
-            if (CERES_SHADOW_NEAREST_BATCH) {
-                float be = e[0];
-                be = best == 1 ? e[1] : best == 2 ? e[2] : best == 3 ? e[3] : be;
-#pragma unroll
-                for (int c = 1; c < 4; ++c)
-                    if ((inner_mask >> c & 1u) && e[c] < be) { be = e[c]; best = c; }
-            }
+            const uint32_t best = __builtin_ctz(inner_mask);
             uint32_t rest = inner_mask & ~(1u << best);
             if (sp + __builtin_popcount(rest) > P.shadow_stack_entries) { overflow = true; return false; }
             while (rest) {
@@ -767,7 +653,7 @@ __device__ __forceinline__ bool trace_any4(const KParams& P, F3 o, F3 d, StkT st
             cur = stk[sp * kS];
         }
     }
-    return kUA && occluded;
+    return false;
 }
 
 // Any-hit of a whole wavefront's shadow rays as ONE masked packet over the shadow BVH4 (batch
@@ -813,32 +699,20 @@ __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<fal
             const uint32_t n = n4_count(chw[c]);
             uint64_t lm = cm[c] & ~occ;
             if (!n || !lm) continue;
-            if (CERES_PACKET_LEAN) {
-                // do-while (n > 0 and lm != 0 on entry), the hit mask straight from the compares
-                const Tri48* tp = P.tris + n4_first(chw[c]);
-                uint32_t left = n;
-                while (true) {                                          // two plain exits: no combined predicate
-                    const float4 a = sload_f4(tp, 0), b = sload_f4(tp, 1), g = sload_f4(tp, 2);
-                    __asm__ volatile("" ::"s"(a.x), "s"(b.x), "s"(g.x));
-                    const TriV tr{{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, g.x}, {g.y, g.z, g.w}};
-                    occ |= tri_mask<kG, CERES_RCP_UNIFORM == 1 || CERES_RCP_UNIFORM_PACKET>(tr, o, d, tmin, tmax) & lm;
-                    lm &= ~occ;
-                    if (!lm) break;
-                    if (--left == 0) break;
-                    ++tp;
-                }
-                continue;
-            }
-            for (uint32_t k = n4_first(chw[c]), ke = k + n; k < ke && lm; ++k) {
-                float t, u, v;
-                const Tri48* tp = P.tris + k;
+            // do-while (n > 0 and lm != 0 on entry), the hit mask straight from the compares: two plain
+            // exits, no combined predicate (round 5 A/B: batches -0.3..-1.2 %)
+            const Tri48* tp = P.tris + n4_first(chw[c]);
+            uint32_t left = n;
+            while (true) {
                 const float4 a = sload_f4(tp, 0), b = sload_f4(tp, 1), g = sload_f4(tp, 2);
                 // all 48 B in flight before the first use (one scalar-load wait per triangle, not two)
                 __asm__ volatile("" ::"s"(a.x), "s"(b.x), "s"(g.x));
                 const TriV tr{{a.x, a.y, a.z}, {a.w, b.x, b.y}, {b.z, b.w, g.x}, {g.y, g.z, g.w}};
-                const bool h = tri_test<kG, CERES_RCP_UNIFORM == 1 || CERES_RCP_UNIFORM_PACKET>(tr, o, d, tmin, tmax, t, u, v);
-                occ |= __ballot(h) & lm;
+                occ |= tri_mask<kG, CERES_RCP_UNIFORM == 1>(tr, o, d, tmin, tmax) & lm;
                 lm &= ~occ;
+                if (!lm) break;
+                if (--left == 0) break;
+                ++tp;
             }
         }
         // one passing inner child next (the first), the others onto the stack with their masks
@@ -896,36 +770,21 @@ __device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32
 }
 
 __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t lr) {
-    if (CERES_TILE_PACKED && P.world == 1) return lr;                 // one rank: local rows are the frame's rows
+    if (P.world == 1) return lr;                                      // one rank: local rows are the frame's rows
     return ((lr / P.row_block) * P.world + P.rank) * P.row_block + lr % P.row_block;
-}
-
-// render.hpp:109-110's 2 * (i + 0.5) / n.  CERES_FAST_PIXQUOT (off until measured): for image
-// sizes n <= 65536 the quotient a / n as fma(fma(-n, q0, a), r0, q0), q0 = a * r0,
-// r0 = v_rcp_f32(n) -- the correctly rounded quotient for every i < n <= 65536 and every r0 within
-// one ulp of 1/n, i.e. whatever the hardware estimate returns (proved by exhaustion on the CPU:
-// tests/test_pixquot_proof.py, 6.4e9 cases; tools/probes/pixquot_exhaustive.hip re-checks it on
-// gfx950); larger n take the division (n is wave-uniform: no divergence)
-__device__ __forceinline__ float pix_quot(uint32_t i, uint32_t n) {
-    const float a = 2 * (float(i) + 0.5f), fn = float(n);
-    if (!CERES_FAST_PIXQUOT || n > 65536u) return a / fn;
-    const float r0 = __builtin_amdgcn_rcpf(fn);
-    const float q0 = a * r0;
-    return __builtin_fmaf(__builtin_fmaf(-fn, q0, a), r0, q0);
 }
 
 // Primary ray direction of pixel (i, j) of frame f, render.hpp:109-111 (GCC: dir + fma(iv, v, iu u)).
 template <bool kG = false>
 __device__ __forceinline__ F3 primary_dir(const KParams& P, uint32_t f, uint32_t i, uint32_t j) {
-    const float u = pix_quot(i, P.W) - 1.0f;
-    const float v = pix_quot(j, P.H) - 1.0f;
+    const float u = 2 * (float(i) + 0.5f) / float(P.W) - 1.0f;       // render.hpp:109-110 (IEEE division)
+    const float v = 2 * (float(j) + 0.5f) / float(P.H) - 1.0f;
     const FrameCam& c = P.cam[f];
     F3 a;
     if constexpr (kG)
         a = F3{c.dir[0] + __builtin_fmaf(c.iv[0], v, c.iu[0] * u), c.dir[1] + __builtin_fmaf(c.iv[1], v, c.iu[1] * u),
                c.dir[2] + __builtin_fmaf(c.iv[2], v, c.iu[2] * u)};
     else a = f3(c.iu) * u + f3(c.iv) * v + f3(c.dir);
-    if (CERES_FAST_PIXQUOT) return a * rcp_exact<true>(sqrtf(dotA<kG>(a, a)));   // normalize, the quotient via rcp_exact
     return kG ? normalizeG<kG>(a) : normalize(a);
 }
 
@@ -1328,7 +1187,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     const uint32_t qq = q & 3;
     const uint32_t t = kTPW == 1 ? tiles4.x : qq == 0 ? tq.x : qq == 1 ? tq.y : qq == 2 ? tq.z : tq.w;
     uint32_t f, by, bx;
-    if (CERES_TILE_PACKED && P.tile_packed) {                        // bit fields (pack_tile), wave-uniform
+    if (P.tile_packed) {                        // bit fields (pack_tile), wave-uniform
         bx = t & ((1u << kTileXBits) - 1u);
         by = (t >> kTileXBits) & ((1u << kTileYBits) - 1u);
         f = t >> (kTileXBits + kTileYBits);
@@ -1673,48 +1532,6 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
         }
         return upload_tile_order(s, W, H, t, frames, tile, order, stream, out, packed, bx, by);
     }
-    const uint32_t tpw_b = uint32_t(CERES_TILES_PER_WAVE);
-    if (CERES_STRIP_ORDER && frames > 1 && tpw_b > 1 && bx >= tpw_b) {
-        // Strips: a wavefront's tpw consecutive order entries are tpw horizontally adjacent tiles
-        // of one row of tiles (a 32x8-pixel strip for 4 tiles per wave), strips centre-first and
-        // shuffled in windows of 64 tiles like single tiles.  A strip's float rows are 384-B runs
-        // (three whole 128-B lines when the row pitch is a multiple of 128 B) written by one
-        // wavefront, instead of 96-B pieces of lines that other wavefronts complete much later in
-        // a batch (each written back twice); its tiles also share BVH paths.  Tiles of a partial
-        // strip (bx not a multiple of tpw) follow all full strips.
-        const uint32_t sx = bx / tpw_b;
-        std::vector<std::pair<double, uint32_t>> sk;
-        sk.reserve(size_t(sx) * by * frames);
-        for (uint32_t f = 0; f < frames; ++f)
-            for (uint32_t y = 0; y < by; ++y) {
-                const size_t lr = std::min<size_t>(size_t(y) * tile + tile / 2, rows - 1);
-                const size_t j = ((lr / t.row_block) * t.world + t.rank) * t.row_block + lr % t.row_block;
-                for (uint32_t x = 0; x < sx; ++x) {
-                    const double dx = (double(x) * tpw_b + 0.5 * tpw_b) * tile - cx, dy = double(j) - cy;
-                    sk.push_back({dx * dx + dy * dy, (f * by + y) * sx + x});
-                }
-            }
-        std::stable_sort(sk.begin(), sk.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-        uint64_t st = 0x9e3779b97f4a7c15ull;
-        const size_t win = std::max<size_t>(1, dev::kTileShuffleWindow / tpw_b);
-        for (size_t b0 = 0; b0 < sk.size(); b0 += win) {
-            const size_t len = std::min<size_t>(win, sk.size() - b0);
-            for (size_t q = len - 1; q > 0; --q) {
-                st = st * 6364136223846793005ull + 1442695040888963407ull;
-                std::swap(sk[b0 + q], sk[b0 + size_t((st >> 33) % (q + 1))]);
-            }
-        }
-        size_t p = 0;
-        for (const auto& e : sk) {
-            const uint32_t fy = e.second / sx, x = e.second - fy * sx;
-            for (uint32_t i = 0; i < tpw_b; ++i) order[p++] = fy * bx + x * tpw_b + i;
-        }
-        for (size_t q = 0; q < n; ++q) {                               // partial strips, centre-first
-            const uint32_t id = k[q].second, x = id % bx;
-            if (x >= sx * tpw_b) order[p++] = id;
-        }
-        return upload_tile_order(s, W, H, t, frames, tile, order, stream, out, packed, bx, by);
-    }
     uint64_t st = 0x9e3779b97f4a7c15ull;
     for (size_t b0 = 0; b0 < n; b0 += dev::kTileShuffleWindow) {
         const size_t len = std::min<size_t>(dev::kTileShuffleWindow, n - b0);
@@ -1870,7 +1687,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     constexpr uint32_t ftile = 8;                                    // fused kernel: 8x8 tiles
     const uint32_t fbx = uint32_t((W + ftile - 1) / ftile), fby = uint32_t((rows + ftile - 1) / ftile);
     const uint32_t* tile_order = nullptr;
-    const bool packed = CERES_TILE_PACKED && frames <= (1u << (32 - kTileXBits - kTileYBits)) &&
+    const bool packed = frames <= (1u << (32 - kTileXBits - kTileYBits)) &&
                         fbx <= (1u << kTileXBits) && fby <= (1u << kTileYBits);
     if (full && rows)
         if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order, packed)) return rc;

@@ -86,6 +86,25 @@ int main() {
     assert r.returncode == 0, r.stderr
 
 
+@pytest.mark.parametrize("flags,warns", [(["-O2", "-mfma"], "CERES_ARITH_FMA"), (["-O0", "-mfma"], "CERES_ARITH_EXACT"),
+                                         (["-O2"], None),
+                                         (["-O2", "-mfma", "-DCERES_DROPIN_ARITH=CERES_ARITH_EXACT"], None),
+                                         (["-O2", "-mfma", "-DCERES_DROPIN_QUIET"], None)])
+def test_dropin_auto_arith_warns(tmp_path, flags, warns):
+    """the header cannot see -ffp-contract, so an automatic arithmetic choice with FMA
+    enabled is announced with a #warning naming the choice; an explicit CERES_DROPIN_ARITH (or
+    CERES_DROPIN_QUIET) silences it, and without FMA there is nothing to guess."""
+    src = tmp_path / "w.cpp"
+    src.write_text('#include "ceres/render.hpp"\nint main() { return CERES_DROPIN_ARITH; }\n')
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", *flags, "-I" + os.path.join(REPO, "include"), str(src)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    if warns is None:
+        assert "#warning" not in r.stderr and "warning" not in r.stderr, r.stderr
+    else:
+        assert "auto-selected " + warns in r.stderr, r.stderr
+
+
 @pytest.mark.skipif(not os.path.isdir("/root/reference/lib/bvh"), reason="reference sources only in the build container")
 def test_dropin_header_compiles_with_reference_types(tmp_path):
     """Drop-in proof: the reference's own static.cpp call pattern compiles against ceres/render.hpp

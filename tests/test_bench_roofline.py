@@ -48,7 +48,8 @@ def test_bound_follows_counters(bench):
 def _bench_lines():
     out = []
     for p in sorted(glob.glob(os.path.join(REPO, "profiles", "r03_end", "sweep", "bench_*.log")) +
-                    glob.glob(os.path.join(REPO, "profiles", "r04", "**", "bench_*.log"), recursive=True)):
+                    glob.glob(os.path.join(REPO, "profiles", "r04", "**", "bench_*.log"), recursive=True) +
+                    glob.glob(os.path.join(REPO, "profiles", "r05", "**", "bench_*.log"), recursive=True)):
         with open(p) as f:
             lines = [ln for ln in f if ln.startswith("{") and '"roofline"' in ln]
         if lines:
@@ -61,7 +62,10 @@ def _pmc_key(line, rf, which):
     if "arith" not in line:                               # round-3 lines: the solo launch, no suffix
         return rf["kernel"]
     if which == "roofline" and "frames_per_launch" in rf:
-        return f"{rf['kernel']}_batch{rf['frames_per_launch']}_{line['arith']}"
+        # round 5: the batch launch is 16 copies of the config view ("views": "config"); orbit
+        # batches carry an "_orbit" key (round-4 lines: orbit batches without the suffix)
+        orbit = "_orbit" if rf.get("views") == "orbit" else ""
+        return f"{rf['kernel']}_batch{rf['frames_per_launch']}{orbit}_{line['arith']}"
     return f"{rf['kernel']}_solo_{line['arith']}"
 
 
@@ -88,6 +92,24 @@ def test_committed_sweep_roofline_recomputes(bench, name, line):
         assert abs(again["achieved"] - rf["achieved"]) <= 1e-3 * rf["achieved"] + 0.2
         assert again["frac"] <= 1.0, (name, which, again["frac"])
     assert line["parity"]["all_frames_match_reference"] is True
+    if line.get("roofline") and "arith" in line and line.get("world_size", 1) == 1:
+        _check_trace_agreement(name, line)
+
+
+def _check_trace_agreement(name, line):
+    """Round 5: a bench line kept next to a single-stream rocprofv3 trace of the
+    same launch (`<dir>/trace_<cfg>_kernel_stats.csv`, tools/batch_launch.py) must agree with it on
+    the mean launch duration within 3 %."""
+    import csv
+    rf = line["roofline"]
+    cfg = line["config"]["workload"].split(":")[0]
+    for p in glob.glob(os.path.join(REPO, "profiles", "r05", "**", f"trace_batch_{cfg}_{line['arith']}_kernel_stats.csv"),
+                       recursive=True):
+        with open(p) as f:
+            rows = [r for r in csv.DictReader(f) if r["Name"].startswith(rf["kernel"])]
+        assert rows, p
+        avg_ms = float(rows[0]["AverageNs"]) / 1e6
+        assert abs(avg_ms - rf["mean_launch_ms"]) <= 0.03 * avg_ms, (name, p, avg_ms, rf["mean_launch_ms"])
 
 
 @pytest.mark.parametrize("name,line", [x for x in _bench_lines() if "roofline_step" in x[1]])
@@ -105,7 +127,9 @@ def test_committed_roofline_step_recomputes(bench, name, line):
     fx = bench.load_orbit_fixture(cfg)
     build = "ref" if line["arith"] == "fma" else "exact"
     F = line["config"]["frames_per_step"]
-    steps = [configs.orbit_step(f, F) for f in range(F)]
+    # round 5: "views": "config" = every frame is the config view (orbit step 0)
+    views = line["config"].get("views", "orbit")
+    steps = [configs.orbit_step(f, F) if views == "orbit" else 0.0 for f in range(F)]
     nbytes = sum(bench.algorithmic_bytes(bench.view_entry(fx[bench.step_key(np.float32(x))], build)["stats"])
                  for x in steps)
     assert nbytes == rs["algorithmic_bytes_per_step"]

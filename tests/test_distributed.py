@@ -343,18 +343,19 @@ def test_frame_owner_gloo_step(world, k):
 
 
 def test_bench_partition_choice():
-    """bench.py --collect auto: C3 (and every untiled config) renders whole frames per rank at every
-    N; the tiled C4 / C5 deal rows and exchange them at N >= 4 but not at N = 2 (DESIGN.md
-    "Multi-GPU": one link would carry the split frames); explicit choices are kept; a frame count
-    that is not a multiple of N falls back to the gather."""
+    """bench.py --collect auto: the framebuffer partition (rows dealt over the ranks, one RCCL
+    all-to-all per step) at every N > 1, except the tiled 4096^2 / 4K configs (C4, C5) at N = 2,
+    where one xGMI link would carry 16 split frames' rows per step (DESIGN.md "Multi-GPU") and each
+    rank renders its frames whole; explicit choices are kept; a frame count that is not a multiple
+    of N falls back to the gather.  The other partition is reported beside it (`alt_collect`)."""
     import sys
     sys.path.insert(0, REPO)
     import bench
     import configs
     C = configs.CONFIGS
-    for n in (1, 2, 4, 8):
-        assert bench.choose_collect("auto", C["dragon_1080"], n, 16 * n) == "frames"
-        assert bench.choose_collect("auto", C["bunny_1080"], n, 16 * n) == "frames"
+    for n in (2, 4, 8):
+        assert bench.choose_collect("auto", C["dragon_1080"], n, 16 * n) == "exchange"
+        assert bench.choose_collect("auto", C["bunny_1080"], n, 16 * n) == "exchange"
     for name in ("dragon_4096", "proc_c5"):
         assert bench.choose_collect("auto", C[name], 2, 32) == "frames"
         assert bench.choose_collect("auto", C[name], 4, 64) == "exchange"
@@ -362,3 +363,105 @@ def test_bench_partition_choice():
     assert bench.choose_collect("exchange", C["dragon_1080"], 4, 64) == "exchange"
     assert bench.choose_collect("gather", C["dragon_1080"], 4, 64) == "gather"
     assert bench.choose_collect("frames", C["dragon_1080"], 3, 16) == "gather"
+    assert bench.alt_collect("exchange") == "frames" and bench.alt_collect("frames") == "exchange"
+
+
+def _line_worker(rank, world, port, q):
+    """Both partitions of a bench step through the slot protocol on gloo, then bench.py's result
+    line built on rank 0 from the ranks' max wall time (as bench.py does at N > 1)."""
+    import sys
+    import time
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    sys.path.insert(0, REPO)
+    from conftest import import_package as ip
+    ip()
+    import hashlib
+    import bench
+    import configs
+    import ceres_raytracer_amd.distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = dict(configs.CONFIGS["dragon_1080"], W=17, H=23)      # the C3 config at a tiny size
+        W, H, k, rb = cfg["W"], cfg["H"], 3, 4
+        F = k * world
+        order = D.exchange_order(F, world)
+        collect = bench.choose_collect("auto", cfg, world, F)
+        res = {}
+        for col in (collect, bench.alt_collect(collect)):
+            g = (D.FrameOwner(W, H, rank, world, frames=F, device="cpu", slots=2) if col == "frames" else
+                 D.FrameExchange(W, H, rb, rank, world, frames=F, device="cpu", slots=2))
+            rows = D.row_map(H, rb, world)[rank] if col == "exchange" else np.arange(H)
+
+            def body(orbit_f, step):
+                rng = np.random.default_rng(1000 * step + orbit_f)
+                return rng.integers(0, 256, size=(H, 3 * W), dtype=np.uint8)
+
+            ok = True
+            t0 = time.perf_counter()
+            for step in range(4):
+                slot = step % 2
+                if col == "frames":
+                    for m, f in enumerate(g.owned_frames()):
+                        g.bufs[slot][m * H:(m + 1) * H] = torch.from_numpy(body(int(order[f]), step))
+                else:                                    # this rank's rows of every frame, ceres_tiling layout
+                    n = len(rows)
+                    for f in range(F):
+                        b = body(int(order[f]), step)
+                        for kk, j in enumerate(rows):
+                            g.bufs[slot][f * n + n - 1 - kk] = torch.from_numpy(b[H - 1 - j].copy())
+                g.start(slot)
+                full = g.finish(slot)
+                g.wait_assembled()
+                got = torch.zeros(F, dtype=torch.int64)
+                for m, f in enumerate(g.owned_frames()):
+                    h = hashlib.sha256(full[m].numpy().tobytes()).hexdigest()
+                    got[int(order[f])] += int(h == hashlib.sha256(body(int(order[f]), step).tobytes()).hexdigest())
+                dist.all_reduce(got)
+                ok &= bool((got == 1).all())
+            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            res[col] = (ok, float(el.item()))
+        if rank == 0:
+            rays = F * W * H + 100
+            alt_c = bench.alt_collect(collect)
+            alt = {"collect": alt_c, "value": round(rays * 4 / res[alt_c][1] / 1e6, 3)}
+            line = bench.result_line(config_name="dragon_1080", cfg=cfg, world=dist.get_world_size(),
+                                     backend=dist.get_backend(), collect=collect, views_kind="config", F=F, steps=4,
+                                     warmup=0, T=res[collect][1], rays_step=rays, hits_step=50, full_mode=True,
+                                     row_block=rb, streams=2, float_fb=False, arith="fma", roofline=None,
+                                     roofline_step=None, roofline_solo=None, cpu=None, parity=None, alt=alt)
+            q.put((all(v[0] for v in res.values()), json_dumps(line)))
+    finally:
+        dist.destroy_process_group()
+
+
+def json_dumps(x):
+    import json
+    return json.dumps(x)
+
+
+def test_bench_line_world2_gloo():
+    """bench.py's N > 1 path on two gloo ranks: the headline partition for C3 is the framebuffer
+    exchange (rows over the ranks + one all-to-all), the collective-free `frames` partition is run
+    as `partition_alt`, every frame of both is produced exactly once, and the line names the world
+    size and backend the collectives ran with."""
+    import json
+    import_package()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_line_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    ok, line = q.get(timeout=10)
+    line = json.loads(line)
+    assert ok
+    assert line["n_gpus"] == line["world_size"] == 2 and line["backend"] == "gloo"
+    assert line["config"]["collect"] == "exchange" and line["collective"]["kind"] == "all_to_all"
+    assert line["config"]["views"] == "config" and "copies of the config view" in line["config"]["workload"]
+    assert line["partition_alt"]["collect"] == "frames" and line["partition_alt"]["value"] > 0
+    assert line["scaling"] == "weak" and line["value"] > 0

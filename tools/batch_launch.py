@@ -3,13 +3,14 @@
 one --pmc counter group per run): `n` launches back to back on ONE stream of
 
   frames = 1:  one whole frame of the config's own view (bench.py `roofline_solo`), or
-  frames = F:  one ceres_render_batch_device launch of the first F orbit views of the bench step
-               (pkg.bench_views, whole frames; bench.py `roofline`),
+  frames = F:  one ceres_render_batch_device launch of F frames, whole: F copies of the config's
+               view (views = config, bench.py's default step and `roofline` launch) or the first F
+               orbit views of the step (views = orbit, pkg.bench_views),
 
 in the chosen arithmetic (fma = the reference CMake build's, exact = -ffp-contract=off), with the
 float + RGB8 framebuffers bench.py writes.  Prints the mean launch duration from HIP events.
 
-usage: python tools/batch_launch.py [config] [fma|exact] [frames] [n]
+usage: python tools/batch_launch.py [config] [fma|exact] [frames] [n] [config|orbit]
 """
 import os
 import sys
@@ -27,6 +28,7 @@ def main():
     arith_s = sys.argv[2] if len(sys.argv) > 2 else "fma"
     frames = int(sys.argv[3]) if len(sys.argv) > 3 else 16
     n = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+    views = sys.argv[5] if len(sys.argv) > 5 else "config"
     pkg = bench.import_package()
     cfg = pkg.configs.CONFIGS[name]
     meta = bench.load_golden(name)
@@ -38,6 +40,8 @@ def main():
     mode = pkg.cfg_mode(cfg, arith)
     b12, s3, _ = pkg.bench_views(cam, cfg["sun"], W, H, max(frames, 1),
                                  basis0=bench.pinned_basis(meta, cfg, cam, build))
+    if views == "config" or cfg.get("bench_view0"):
+        b12, s3 = np.repeat(b12[:1], len(b12), 0), np.repeat(s3[:1], len(s3), 0)
     rgb = torch.empty(frames * 3 * W * H, dtype=torch.uint8, device="cuda")
     px = torch.empty(frames * 3 * W * H, dtype=torch.float32, device="cuda")
     st = torch.cuda.current_stream()
@@ -59,7 +63,7 @@ def main():
     e1.record(st)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / n
-    print(f"{name} {arith_s} frames={frames} launches={n} mean_launch_ms={ms:.5f}", flush=True)
+    print(f"{name} {arith_s} frames={frames} views={views} launches={n} mean_launch_ms={ms:.5f}", flush=True)
     scene.close()
     return 0
 
