@@ -103,7 +103,9 @@ struct alignas(128) Shard {
 };
 static_assert(sizeof(Shard) == 128, "Shard");
 
-constexpr int kMaxFrames = 64;  // frames per batch launch (KParams, cameras inline, stays inside the 4 KB kernarg limit)
+constexpr int kMaxFrames = 64;        // frames per batch call (ceres_render_batch_device)
+constexpr int kFramesPerLaunch = 56;  // frames per kernel launch (KParams: cameras + cull rects inline, inside the 4 KB
+                                      // kernarg limit); a larger batch is two launches on the same stream
 struct FrameCam {              // one frame of a batch: eye + the render.hpp:91-97 basis + its sun
     float eye[3], dir[3], iu[3], iv[3], sun[3];
 };
@@ -113,9 +115,12 @@ struct FrameCam {              // one frame of a batch: eye + the render.hpp:91-
 constexpr uint32_t kTileXBits = 13, kTileYBits = 13;
 constexpr uint32_t pack_tile(uint32_t f, uint32_t y, uint32_t x) { return (f << (kTileXBits + kTileYBits)) | (y << kTileXBits) | x; }
 
+struct CullRect { uint16_t i0, i1, j0, j1; };   // pixels (column i, global row j) whose rays may reach the root box
+
 struct KParams {
-    FrameCam cam[kMaxFrames];
-    uint32_t frames;                             // frames in this batch (1..kMaxFrames)
+    FrameCam cam[kFramesPerLaunch];
+    CullRect cull_rect[kFramesPerLaunch];        // production kernels: the background cull (tile_misses_root)
+    uint32_t frames;                             // frames in this launch (1..kFramesPerLaunch)
     uint32_t W, H;
     uint32_t row_block, rank, world, local_rows; // this rank's rows of every frame (ceres_tiling)
     uint32_t row_blocks_per_frame;               // 16-row blocks of local rows per frame (primary grid.y)
@@ -123,6 +128,7 @@ struct KParams {
     uint32_t root_leaf_count, root_leaf_first;   // root is a leaf (single_ray_traverser.hpp:72-73)
     float root_box[6];                           // the root node's bounds (bvh.hpp:25-30 order) ...
     uint32_t root_box_ok;                        // ... and whether both root children lie inside it
+    uint32_t cull;                               // production kernels: background tiles culled (tile_misses_root)
     uint32_t shadow_stack_entries;               // BVH4 traversal stack (shadow rays)
     uint32_t packets;                            // batch kernel: wave-wide packets (L2-resident scenes, render_hip.hip)
     uint32_t tiles_x;                            // tile columns per row (fused kernel)

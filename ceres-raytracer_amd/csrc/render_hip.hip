@@ -84,8 +84,8 @@
 #define CERES_LOAD_ALWAYS 1                    // trace(): finished lanes load a (cached) record too -- no branch
                                                // (batch kernel; A/B profiles/r04/s4 "ldall": batches -0.7..-1.5 %)
 #endif
-#ifndef CERES_DEFER_MISS_STORE
-#define CERES_DEFER_MISS_STORE 1               // missed pixels stored at the end of the tile (fused kernel)
+#ifndef CERES_CULL
+#define CERES_CULL 1                           // tiles whose rays provably miss the root box: stored as misses (tile_misses_root)
 #endif
 #ifndef CERES_TRI_SELECT
 #define CERES_TRI_SELECT 1                     // triangle test without control flow (t always computed, one
@@ -788,6 +788,20 @@ __device__ __forceinline__ F3 primary_dir(const KParams& P, uint32_t f, uint32_t
     return kG ? normalizeG<kG>(a) : normalize(a);
 }
 
+// Exact background cull (round 5).  A tile whose every pixel's primary ray provably misses the
+// root box is stored as misses (render.hpp:116-117: RGB 0) without tracing: the root-box pre-test
+// (set_root_box) already shows that such a ray fails both of the root's children in the
+// reference's first step (single_ray_traverser.hpp:81-123), so the pixel, the ray count and the
+// hit count are the reference's.  The host proves per frame which pixels' rays cannot reach the
+// box (cull_rect: the image of the root box, expanded, is inside a pixel rectangle) and passes
+// that rectangle in the kernel arguments; a tile is culled when none of its pixels lies inside.
+// Stats / records kernels never cull (their per-ray counters count the root step).
+__device__ __forceinline__ bool tile_misses_root(const KParams& P, uint32_t f, bool active, uint32_t i, uint32_t j) {
+    const CullRect& r = P.cull_rect[f];
+    const bool out = i < r.i0 || i > r.i1 || j < r.j0 || j > r.j1;
+    return __ballot(active && !out) == 0;
+}
+
 // Hit point + self-intersection offset, render.hpp:127-133 (p1() = p0 - e1, p2() = p0 + e2).
 // GCC: fma(n, scale, fma(w, p2, fma(v, p1, u p0))) per component.
 template <bool kG>
@@ -856,7 +870,10 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     Hit h{0, 0.f, 0.f, 0.f};
     uint32_t n_pairs = 0, n_tests = 0;
     bool overflow = false;
-    if (active) {
+    const bool culled = !kStats && P.cull && tile_misses_root(P, f, active, i, global_row(P, lr));
+    if (culled) {
+        if (active) store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);        // render.hpp:116-117, every pixel a miss
+    } else if (active) {
         const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
         hit = trace<false, kStats, kBlock, uint32_t*, kRobust, -1, kG>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests, overflow);
         if (P.rec_prim) {
@@ -1111,20 +1128,18 @@ __device__ __forceinline__ bool shadow_packet(const KParams& P, bool hit, const 
     return false;
 }
 
-// Shading / store of a lit or occluded pixel (render.hpp:139-150).
+// Colour of a pixel with a primary hit, lit or occluded (render.hpp:139-150).
 template <bool kG>
-__device__ __forceinline__ void finish_pixel(const KParams& P, uint32_t f, uint32_t lr, uint32_t i, uint32_t pix,
-                                             bool blocked, F3 sun_line, uint32_t slot, float hu, float hv,
-                                             uint32_t& occluded) {
+__device__ __forceinline__ void shade_pixel(const KParams& P, uint32_t f, uint32_t lr, uint32_t i, uint32_t pix,
+                                            bool blocked, F3 sun_line, uint32_t slot, float hu, float hv,
+                                            uint32_t& occluded, float c[3]) {
     if (P.rec_shadow) P.rec_shadow[pix] = blocked ? 1 : 0;
+    c[0] = c[1] = c[2] = 0.f;
     if (blocked) {
         ++occluded;
-        store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);
     } else {
         const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
-        float c[3];
         shade<kG>(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
-        store_pixel(P, f, lr, i, c[0], c[1], c[2]);
     }
 }
 
@@ -1209,6 +1224,10 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     RayWork w{};
     uint64_t t_start = 0;
     if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
+    if (!kStats && P.cull && tile_misses_root(P, f, active, i, global_row(P, lr))) {
+        if (active) store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);        // render.hpp:116-117, every pixel a miss
+        continue;
+    }
     if (active) {
         const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
         // kOct -1: the traversal dispatches on a wave-uniform octant; -2: generic loop only
@@ -1224,7 +1243,6 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
         // a missed pixel (render.hpp:116-117) is stored with the tile's lit ones, at the end: a
         // store here would sit in the in-order vector-memory counter ahead of the hit lanes'
         // triangle fetch below, which would then wait for the store's write acknowledgement
-        if (!CERES_DEFER_MISS_STORE && !hit) store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);
         if (hit) {                                                   // render.hpp:127-135
             const TriV tr = load_tri(P.tris + h.slot);
             const F3 normal = normalizeG<kG>(tr.n);
@@ -1251,8 +1269,9 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     else
         L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust, kQ, kPacketsCompiled ? -2 : -1, kG>(
                                     P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
-    if (hit) finish_pixel<kG>(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded);
-    else if (CERES_DEFER_MISS_STORE && active) store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);   // render.hpp:116-117
+    float col[3] = {0.f, 0.f, 0.f};                                    // a miss: render.hpp:116-117
+    if (hit) shade_pixel<kG>(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded, col);
+    if (active) store_pixel(P, f, lr, i, col[0], col[1], col[2]);
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
         // primary hits, wave primary pairs, wave shadow pairs
@@ -1620,14 +1639,64 @@ void set_root_box(ceres_scene* s, const float root[6], const SiblingPair& p0) {
     s->root_box_ok = (!s->root_leaf_count && inside(p0.lb) && inside(p0.rb)) ? 1u : 0u;
 }
 
-// One batch: `frames` cameras (basis12 = frames x {eye, dir, iu, iv}) and suns (frames x 3).
-int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* sun, int mode, size_t W, size_t H,
-           const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream,
-           int32_t* d_rec_prim = nullptr, float* d_rec_tuv = nullptr, int8_t* d_rec_shadow = nullptr) {
+// The background cull's proof for one frame (tile_misses_root).  The primary ray of image
+// coordinates (u, v) is eye + s (iu u + iv v + dir) (render.hpp:109-111), so a point X projects to
+// (p / w, q / w) with (p, q, w) = [iu iv dir]^-1 (X - eye).  Every corner of the root box, EXPANDED
+// by 1e-4 of the scene / eye coordinate scale, must lie in front of the eye (w > 0.01 |X - eye|);
+// then the expanded box's image lies inside the bounding rectangle of the corner images (a convex
+// set in front of the eye projects into the hull of its corners' images), and a pixel whose (u, v)
+// = (2 (i + 0.5) / W - 1, 2 (j + 0.5) / H - 1) lies outside that rectangle widened by m = 2e-3 (1 +
+// max |corner coordinate|) -- two pixels at 1080p -- has a ray that misses the expanded box.  The
+// kernel's float ray (render.hpp:109-113: rounding of ~1e-6 in (u, v) and in the unit direction)
+// and float slab test (~1e-6 relative in the slab distances, node_intersectors.hpp:83-103) stay far
+// inside those margins, so its root-box test fails too.  Computed in double; anything degenerate
+// (a corner behind the eye, NaN, a frame wider than 65,535 pixels) keeps every pixel.
+static CullRect cull_rect(const FrameCam& c, const float root[6], uint32_t W, uint32_t H) {
+    const CullRect keep{0u, 0xffffu, 0u, 0xffffu};
+    if (W > 0xffffu || H > 0xffffu) return keep;
+    double e[3], iu[3], iv[3], d[3];
+    for (int k = 0; k < 3; ++k) { e[k] = c.eye[k]; iu[k] = c.iu[k]; iv[k] = c.iv[k]; d[k] = c.dir[k]; }
+    double sc = 0;
+    for (int k = 0; k < 3; ++k) sc = std::max(sc, std::fabs(e[k]));
+    for (int k = 0; k < 6; ++k) sc = std::max(sc, std::fabs(double(root[k])));
+    const double pad = 1e-4 * sc;
+    auto cr = [](const double* a, const double* b, double* o) {
+        o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0]; };
+    double c0[3], c1[3], c2[3];
+    cr(iv, d, c0); cr(d, iu, c1); cr(iu, iv, c2);
+    const double det = iu[0] * c0[0] + iu[1] * c0[1] + iu[2] * c0[2];
+    double u0 = HUGE_VAL, u1 = -HUGE_VAL, v0 = HUGE_VAL, v1 = -HUGE_VAL;
+    for (int k = 0; k < 8; ++k) {
+        const double X[3] = {(k & 1) ? root[1] + pad : root[0] - pad, (k & 2) ? root[3] + pad : root[2] - pad,
+                             (k & 4) ? root[5] + pad : root[4] - pad};
+        const double r[3] = {X[0] - e[0], X[1] - e[1], X[2] - e[2]};
+        const double pw = r[0] * c0[0] + r[1] * c0[1] + r[2] * c0[2], qw = r[0] * c1[0] + r[1] * c1[1] + r[2] * c1[2];
+        const double ww = r[0] * c2[0] + r[1] * c2[1] + r[2] * c2[2];
+        if (!(ww / det > 0.01 * std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]))) return keep;
+        u0 = std::min(u0, pw / ww); u1 = std::max(u1, pw / ww); v0 = std::min(v0, qw / ww); v1 = std::max(v1, qw / ww);
+    }
+    const double m = 2e-3 * (1 + std::max(std::max(std::fabs(u0), std::fabs(u1)), std::max(std::fabs(v0), std::fabs(v1))));
+    // pixels whose u lies in [u0 - m, u1 + m]: i in [(u0 - m + 1) W / 2 - 0.5, (u1 + m + 1) W / 2 - 0.5], one more each side
+    auto lo = [](double x, uint32_t n) { return x <= 0 ? 0u : x >= n ? n : uint32_t(std::floor(x)); };
+    const double a0 = (u0 - m + 1) * W / 2 - 0.5 - 1, a1 = (u1 + m + 1) * W / 2 - 0.5 + 1;
+    const double b0 = (v0 - m + 1) * H / 2 - 0.5 - 1, b1 = (v1 + m + 1) * H / 2 - 0.5 + 1;
+    if (!(a0 == a0 && a1 == a1 && b0 == b0 && b1 == b1)) return keep;
+    if (a1 < 0 || b1 < 0) return CullRect{1u, 0u, 1u, 0u};            // empty: the whole frame misses
+    return CullRect{uint16_t(lo(a0, W)), uint16_t(std::min<double>(std::ceil(a1), 0xffff)),
+                    uint16_t(lo(b0, H)), uint16_t(std::min<double>(std::ceil(b1), 0xffff))};
+}
+
+// One launch of a batch: `frames` (<= kFramesPerLaunch) cameras (basis12 = frames x {eye, dir, iu,
+// iv}) and suns (frames x 3).  first / last: the first and last launch of a batch call (the counter
+// shards are cleaned before the first and summed after the last, over `batch_frames` frames).
+int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const float* sun, int mode, size_t W, size_t H,
+                 const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream,
+                 int32_t* d_rec_prim, float* d_rec_tuv, int8_t* d_rec_shadow, bool first, bool last,
+                 uint32_t batch_frames) {
     if (!s || !basis12 || !sun) return set_error(CERES_EINVAL, "render: null argument");
     if (s->f64) return set_error(CERES_EINVAL, "scene is double precision: use ceres_render_f64");
-    if (frames == 0 || frames > uint32_t(kMaxFrames))
-        return set_error(CERES_EINVAL, "render: %u frames per batch (1..%d)", frames, kMaxFrames);
+    if (frames == 0 || frames > uint32_t(kFramesPerLaunch))
+        return set_error(CERES_EINVAL, "render: %u frames per launch (1..%d)", frames, kFramesPerLaunch);
     const bool robust = (mode & CERES_MODE_ROBUST) != 0;            // RobustNodeIntersector traversal
     const bool qbvh = (mode & CERES_MODE_QBVH4) != 0;              // compressed shadow BVH4 (not exact)
     const bool gfma = (mode & CERES_MODE_FMA) != 0;                 // the reference CMake build's FMA contraction
@@ -1670,6 +1739,11 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     P.root_leaf_count = s->root_leaf_count; P.root_leaf_first = s->root_leaf_first;
     for (int k = 0; k < 6; ++k) P.root_box[k] = s->root_box[k];
     P.root_box_ok = CERES_ROOT_TEST ? s->root_box_ok : 0u;
+    // the background cull rests on the root-box pre-test's argument (tile_misses_root); stats scenes
+    // and hit records keep every ray's own root step
+    P.cull = (CERES_CULL && P.root_box_ok && !(s->flags & CERES_SCENE_STATS) && !d_rec_prim) ? 1u : 0u;
+    if (P.cull)
+        for (uint32_t f = 0; f < frames; ++f) P.cull_rect[f] = cull_rect(P.cam[f], P.root_box, P.W, P.H);
     P.pairs = s->d_pairs; P.nodes4 = s->d_nodes4; P.tris = s->d_tris; P.orig = s->d_orig; P.norms = s->d_norms;
     P.qnodes4 = s->d_qnodes4;
     P.pixels = d_pixels; P.rgb8 = d_rgb8; P.shards = s->d_shards;
@@ -1695,7 +1769,7 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     // the fused kernel without counters only adds to them, so its steady-state frames skip the
     // memset (ceres_finalize re-zeroes them after every counted render).
     const bool need_clean = d_counters || !full;
-    if (need_clean && s->shards_dirty) HIP_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, stream));
+    if (first && need_clean && s->shards_dirty) HIP_TRY(hipMemsetAsync(s->d_shards, 0, sizeof(Shard) * kShards, stream));
     s->shards_dirty = true;
     if (rows) {                                                      // a rank may own no rows
         if (e0) HIP_TRY(hipEventRecord(e0, stream));
@@ -1775,11 +1849,38 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
         HIP_TRY(hipGetLastError());
         if (e1) HIP_TRY(hipEventRecord(e1, stream));
     }
-    if (d_counters) {
+    if (d_counters && last) {
         hipLaunchKernelGGL(dev::ceres_finalize, dim3(1), dim3(64), 0, stream, s->d_shards,
-                           uint64_t(frames) * W * rows, d_counters);
+                           uint64_t(batch_frames) * W * rows, d_counters);
         HIP_TRY(hipGetLastError());
         s->shards_dirty = false;
+    }
+    return CERES_OK;
+}
+
+// One batch call of 1..kMaxFrames frames: launches of at most kFramesPerLaunch frames on `stream`,
+// frame f's outputs at offset f x W x local rows (pixels x 3) as in one launch.
+int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* sun, int mode, size_t W, size_t H,
+           const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream,
+           int32_t* d_rec_prim = nullptr, float* d_rec_tuv = nullptr, int8_t* d_rec_shadow = nullptr) {
+    if (frames == 0 || frames > uint32_t(kMaxFrames))
+        return set_error(CERES_EINVAL, "render: %u frames per batch (1..%d)", frames, kMaxFrames);
+    if (!basis12 || !sun) return set_error(CERES_EINVAL, "render: null argument");
+    if (frames <= uint32_t(kFramesPerLaunch))
+        return launch_chunk(s, frames, basis12, sun, mode, W, H, tiling, d_pixels, d_rgb8, d_counters, stream, d_rec_prim,
+                            d_rec_tuv, d_rec_shadow, true, true, frames);
+    ceres_tiling t{uint32_t(H), 0, 1};
+    if (tiling) t = *tiling;
+    if (t.world == 0 || t.rank >= t.world || t.row_block == 0) return set_error(CERES_EINVAL, "render: bad tiling");
+    const size_t fp = W * local_rows_of(H, t.row_block, t.rank, t.world);   // pixels per frame on this rank
+    for (uint32_t f0 = 0; f0 < frames; f0 += kFramesPerLaunch) {
+        const uint32_t n = std::min<uint32_t>(kFramesPerLaunch, frames - f0);
+        const size_t o = size_t(f0) * fp;
+        if (int rc = launch_chunk(s, n, basis12 + 12 * size_t(f0), sun + 3 * size_t(f0), mode, W, H, tiling,
+                                  d_pixels ? d_pixels + 3 * o : nullptr, d_rgb8 ? d_rgb8 + 3 * o : nullptr, d_counters,
+                                  stream, d_rec_prim ? d_rec_prim + o : nullptr, d_rec_tuv ? d_rec_tuv + 3 * o : nullptr,
+                                  d_rec_shadow ? d_rec_shadow + o : nullptr, f0 == 0, f0 + n >= frames, frames))
+            return rc;
     }
     return CERES_OK;
 }
