@@ -50,7 +50,9 @@ EXPORTED_SYMBOLS = (
     "ceres_bvh_build_device", "ceres_obj_load_gpu", "ceres_obj_parse_device", "ceres_rotate_triangles_device",
     "ceres_device_free", "ceres_camera_basis", "ceres_obj_load_f64", "ceres_proc_mesh_f64", "ceres_rotate_triangles_f64",
     "ceres_bvh_build_f64", "ceres_camera_basis_f64", "ceres_orbit_cameras_f64", "ceres_scene_create_f64",
-    "ceres_render_f64", "ceres_render_records_f64",
+    "ceres_render_f64", "ceres_render_records_f64", "ceres_obj_load_f64_arith", "ceres_proc_mesh_f64_arith",
+    "ceres_rotate_triangles_f64_arith", "ceres_bvh_build_f64_arith", "ceres_camera_basis_f64_arith",
+    "ceres_orbit_cameras_f64_arith",
     "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_multi_f32", "ceres_device_count", "ceres_assemble_rgb8_packed", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
@@ -133,6 +135,16 @@ def lib():
     L.ceres_camera_basis_f64.argtypes = [_dp, _dp, _dp, ctypes.c_double, _sz, _sz, _dp]
     L.ceres_orbit_cameras_f64.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_double, _sz, _sz, _dp, ctypes.c_double,
                                           ctypes.c_uint32, ctypes.c_int, _dp, _dp, _dp]
+    L.ceres_obj_load_f64_arith.argtypes = [ctypes.c_char_p, ctypes.POINTER(_dp), ctypes.POINTER(_dp), ctypes.POINTER(_sz),
+                                           ctypes.c_int]
+    L.ceres_proc_mesh_f64_arith.argtypes = [ctypes.c_int, ctypes.POINTER(_dp), ctypes.POINTER(_dp), ctypes.POINTER(_sz),
+                                            ctypes.c_int]
+    L.ceres_rotate_triangles_f64_arith.argtypes = [_dp, _sz, ctypes.c_int, ctypes.c_double, ctypes.c_int]
+    L.ceres_bvh_build_f64_arith.argtypes = [_dp, _sz, ctypes.POINTER(_u64p), ctypes.POINTER(_sz), ctypes.POINTER(_u64p),
+                                            ctypes.c_int]
+    L.ceres_camera_basis_f64_arith.argtypes = [_dp, _dp, _dp, ctypes.c_double, _sz, _sz, _dp, ctypes.c_int]
+    L.ceres_orbit_cameras_f64_arith.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_double, _sz, _sz, _dp, ctypes.c_double,
+                                                ctypes.c_uint32, ctypes.c_int, _dp, _dp, _dp, ctypes.c_int]
     L.ceres_scene_create_f64.argtypes = [_dp, _sz, _dp, _vp, _sz, _u64p, ctypes.c_int, ctypes.c_uint32]
     L.ceres_scene_create_f64.restype = _vp
     L.ceres_render_f64.argtypes = [_vp, _dp, _dp, ctypes.c_int, _dp, ctypes.POINTER(ctypes.c_uint8), _sz, _sz,
@@ -218,8 +230,9 @@ class Camera:
         """render.hpp:91-97 on the host (libm stays on the host): {eye, dir, image_u, image_v}."""
         if self.dtype == np.float64:
             out = np.zeros(9, np.float64)
-            _check(lib().ceres_camera_basis_f64(_p(self.eye, ctypes.c_double), _p(self.dir, ctypes.c_double),
-                                                _p(self.up, ctypes.c_double), self.fov, W, H, _p(out, ctypes.c_double)))
+            _check(lib().ceres_camera_basis_f64_arith(_p(self.eye, ctypes.c_double), _p(self.dir, ctypes.c_double),
+                                                      _p(self.up, ctypes.c_double), self.fov, W, H,
+                                                      _p(out, ctypes.c_double), self.arith))
             return np.concatenate([self.eye, out])
         out = np.zeros(9, np.float32)
         _check(lib().ceres_camera_basis_arith(_p(self.eye, ctypes.c_float), _p(self.dir, ctypes.c_float),
@@ -262,17 +275,18 @@ def load_obj(path, arith=ARITH_EXACT):
     return Mesh(_take(t, c * 12, np.float32).reshape(c, 12), _take(n, c * 9, np.float32).reshape(c, 9))
 
 
-def load_obj_f64(path):
+def load_obj_f64(path, arith=ARITH_EXACT):
     """obj::load_from_file<double> (anim.cpp -d): strtof coordinates widened to double."""
     t, n, cnt = _dp(), _dp(), _sz()
-    _check(lib().ceres_obj_load_f64(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt)))
+    _check(lib().ceres_obj_load_f64_arith(os.fsencode(path), ctypes.byref(t), ctypes.byref(n), ctypes.byref(cnt),
+                                          int(arith)))
     c = cnt.value
     return Mesh(_take(t, c * 12, np.float64).reshape(c, 12), _take(n, c * 9, np.float64).reshape(c, 9))
 
 
-def proc_mesh_f64(n):
+def proc_mesh_f64(n, arith=ARITH_EXACT):
     t, nn, cnt = _dp(), _dp(), _sz()
-    _check(lib().ceres_proc_mesh_f64(int(n), ctypes.byref(t), ctypes.byref(nn), ctypes.byref(cnt)))
+    _check(lib().ceres_proc_mesh_f64_arith(int(n), ctypes.byref(t), ctypes.byref(nn), ctypes.byref(cnt), int(arith)))
     c = cnt.value
     return Mesh(_take(t, c * 12, np.float64).reshape(c, 12), _take(nn, c * 9, np.float64).reshape(c, 9))
 
@@ -314,7 +328,8 @@ def proc_mesh(n, arith=ARITH_EXACT):
 def rotate_triangles(mesh, axis, degrees, arith=ARITH_EXACT):
     ax = {"x": 0, "y": 1, "z": 2}[axis] if isinstance(axis, str) else int(axis)
     if mesh.f64:
-        _check(lib().ceres_rotate_triangles_f64(_p(mesh.tri, ctypes.c_double), len(mesh), ax, float(degrees)))
+        _check(lib().ceres_rotate_triangles_f64_arith(_p(mesh.tri, ctypes.c_double), len(mesh), ax, float(degrees),
+                                                      int(arith)))
     else:
         _check(lib().ceres_rotate_triangles_arith(_p(mesh.tri, ctypes.c_float), len(mesh), ax, float(degrees),
                                                   int(arith)))
@@ -324,8 +339,8 @@ def rotate_triangles(mesh, axis, degrees, arith=ARITH_EXACT):
 def build_bvh(mesh, arith=ARITH_EXACT):
     if mesh.f64:
         nodes, prim, m = _u64p(), _u64p(), _sz()
-        _check(lib().ceres_bvh_build_f64(_p(mesh.tri, ctypes.c_double), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
-                                         ctypes.byref(prim)))
+        _check(lib().ceres_bvh_build_f64_arith(_p(mesh.tri, ctypes.c_double), len(mesh), ctypes.byref(nodes),
+                                               ctypes.byref(m), ctypes.byref(prim), int(arith)))
         return Bvh(_take(nodes, m.value * 8, np.uint64).reshape(-1, 8), _take(prim, len(mesh), np.uint64))
     nodes, prim, m = _u32p(), _u64p(), _sz()
     _check(lib().ceres_bvh_build_arith(_p(mesh.tri, ctypes.c_float), len(mesh), ctypes.byref(nodes), ctypes.byref(m),
@@ -536,10 +551,10 @@ def pose(cfg, frame=0, arith=ARITH_EXACT):
     return Camera(b[n, :3], d3[n], cfg["up"], cfg["fov"], arith=arith), s3[n].copy()
 
 
-def pose_f64(cfg):
+def pose_f64(cfg, arith=ARITH_EXACT):
     """(Camera<double>, sun) of a config: its values as double literals (anim.cpp writes its
     camera as double literals), orbited with Transform<double> when the config has "orbit"."""
-    cam = Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"], dtype=np.float64)
+    cam = Camera(cfg["eye"], cfg["dir"], cfg["up"], cfg["fov"], dtype=np.float64, arith=arith)
     sun = np.asarray(cfg["sun"], np.float64)
     if not cfg.get("orbit"):
         return cam, sun
@@ -548,11 +563,12 @@ def pose_f64(cfg):
     s3 = np.zeros((n + 1, 3), np.float64)
     d3 = np.zeros((n + 1, 3), np.float64)
     ax = np.asarray(axis, np.float64)
-    _check(lib().ceres_orbit_cameras_f64(_p(cam.eye, ctypes.c_double), _p(cam.dir, ctypes.c_double),
-                                         _p(cam.up, ctypes.c_double), _p(sun, ctypes.c_double), cam.fov, cfg["W"],
-                                         cfg["H"], _p(ax, ctypes.c_double), float(step), n + 1, 0,
-                                         _p(b, ctypes.c_double), _p(s3, ctypes.c_double), _p(d3, ctypes.c_double)))
-    return Camera(b[n, :3], d3[n], cfg["up"], cfg["fov"], dtype=np.float64), s3[n].copy()
+    _check(lib().ceres_orbit_cameras_f64_arith(_p(cam.eye, ctypes.c_double), _p(cam.dir, ctypes.c_double),
+                                               _p(cam.up, ctypes.c_double), _p(sun, ctypes.c_double), cam.fov, cfg["W"],
+                                               cfg["H"], _p(ax, ctypes.c_double), float(step), n + 1, 0,
+                                               _p(b, ctypes.c_double), _p(s3, ctypes.c_double), _p(d3, ctypes.c_double),
+                                               int(arith)))
+    return Camera(b[n, :3], d3[n], cfg["up"], cfg["fov"], dtype=np.float64, arith=arith), s3[n].copy()
 
 
 def assemble_rgb8(d_gathered, rank_stride, d_out, frames, W, H, row_block, world, stream=0):
@@ -589,12 +605,12 @@ def prepare(cfg, f64=False, arith=ARITH_EXACT):
     pipeline (anim.cpp -d) -- double mesh / BVH, camera at the config's pose in double.
     arith = ARITH_FMA: every step in the reference CMake build's arithmetic (render with MODE_FMA)."""
     if f64:
-        mesh = proc_mesh_f64(cfg["proc"]) if cfg.get("proc") else load_obj_f64(configs.obj_path(cfg))
+        mesh = proc_mesh_f64(cfg["proc"], arith) if cfg.get("proc") else load_obj_f64(configs.obj_path(cfg), arith)
         if len(mesh) == 0:
             raise CeresError("The given scene is empty or cannot be loaded")
         if cfg.get("rotate"):
-            rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1])
-        return mesh, build_bvh(mesh), pose_f64(cfg)[0]
+            rotate_triangles(mesh, cfg["rotate"][0], cfg["rotate"][1], arith)
+        return mesh, build_bvh(mesh, arith), pose_f64(cfg, arith)[0]
     mesh = proc_mesh(cfg["proc"], arith) if cfg.get("proc") else load_obj(configs.obj_path(cfg), arith)
     if len(mesh) == 0:
         raise CeresError("The given scene is empty or cannot be loaded")

@@ -14,6 +14,15 @@
 // used, render.hpp:139), shading, store.  Records are double-width (112-B sibling pairs, 96-B
 // triangles); the stack is u32 in LDS like the float path.  Built without FP contraction;
 // IEEE double division and sqrt are correctly rounded on gfx950.
+//
+// CERES_MODE_FMA (kG = true, round 5): the reference's own CMake build of anim.cpp -d (g++ -O3
+// -mavx2 -mfma, CMakeLists.txt:11) fuses the double hot path at the same sites as the float one
+// -- GCC's widening_mul dump of the double harness lists the same (file, line, column, FMA kind)
+// multiset for render()'s pixel loop, smooth_shading and blinn_phong_spec
+// (oracle/contraction_sites.txt) -- so the kernel carries an explicit fma at each: dotA / dotB,
+// cross with the first product fused, the primary direction dir + fma(iv, v, iu u), the hit point
+// fma(n, -1e-5, fma(w, p2, fma(v, p1, u p0))), lambertian as dotA in double, and the float
+// fmaf(lam, 0.5, amb) / fmaf(base, k, spec) of smooth_shading.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -53,6 +62,20 @@ __device__ __forceinline__ double dot(D3 a, D3 b) { double s = a.x * b.x; s += a
 __device__ __forceinline__ D3 cross(D3 a, D3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 __device__ __forceinline__ D3 normalize(D3 v) { const double inv = 1.0 / sqrt(dot(v, v)); return v * inv; }
 __device__ __forceinline__ D3 d3(const double* p) { return {p[0], p[1], p[2]}; }
+// GCC's contraction of vector.hpp:134-167 in the reference-flag build (kG; oracle/contraction_sites.txt)
+template <bool kG> __device__ __forceinline__ double dotA(D3 a, D3 b) {
+    if constexpr (kG) return fma(a.z, b.z, fma(a.x, b.x, a.y * b.y));
+    else return dot(a, b);
+}
+template <bool kG> __device__ __forceinline__ double dotB(D3 a, D3 b) {
+    if constexpr (kG) return fma(a.z, b.z, fma(a.y, b.y, a.x * b.x));
+    else return dot(a, b);
+}
+template <bool kG> __device__ __forceinline__ D3 crossG(D3 a, D3 b) {
+    if constexpr (kG) return {fma(a.y, b.z, -(a.z * b.y)), fma(a.z, b.x, -(a.x * b.z)), fma(a.x, b.y, -(a.y * b.x))};
+    else return cross(a, b);
+}
+template <bool kG> __device__ __forceinline__ D3 normalizeG(D3 v) { const double inv = 1.0 / sqrt(dotA<kG>(v, v)); return v * inv; }
 
 struct Cam64 { double eye[3], dir[3], iu[3], iv[3], sun[3]; };
 
@@ -82,16 +105,17 @@ __device__ __forceinline__ TriD load_tri(const Tri96* t) {
 }
 
 // Triangle<double>::intersect (triangle.hpp:95-115)
+template <bool kG>
 __device__ __forceinline__ bool tri_test(const TriD& tr, D3 o, D3 d, double tmin, double tmax, double& t_out, double& u_out,
                                          double& v_out) {
     const D3 c = tr.p0 - o;
-    const D3 r = cross(d, c);
-    const double inv_det = 1.0 / dot(tr.n, d);
-    const double u = dot(r, tr.e2) * inv_det;
-    const double v = dot(r, tr.e1) * inv_det;
+    const D3 r = crossG<kG>(d, c);
+    const double inv_det = 1.0 / dotA<kG>(tr.n, d);
+    const double u = dotA<kG>(r, tr.e2) * inv_det;
+    const double v = dotB<kG>(r, tr.e1) * inv_det;
     const double w = 1.0 - u - v;
     if (u >= 0 && v >= 0 && w >= 0) {
-        const double t = dot(tr.n, c) * inv_det;
+        const double t = dotA<kG>(tr.n, c) * inv_det;
         if (t >= tmin && t <= tmax) { t_out = t; u_out = u; v_out = v; return true; }
     }
     return false;
@@ -102,7 +126,7 @@ struct Hit { uint32_t slot; double t, u, v; };
 // single_ray_traverser.hpp:68-126 in double (the float trace() of render_hip.hip: the same
 // visiting order, octant-free monotone slab test, near-first ties left; any-hit returns at the
 // first accepted triangle).
-template <bool kAnyHit>
+template <bool kAnyHit, bool kG>
 __device__ bool trace(const KParams64& P, D3 o, D3 d, uint32_t* stk, Hit& best, bool& overflow) {
     const double tmin = 0.0;
     double tmax = DBL_MAX;                                          // ray.hpp:17-21
@@ -110,7 +134,7 @@ __device__ bool trace(const KParams64& P, D3 o, D3 d, uint32_t* stk, Hit& best, 
     if (P.root_leaf_count) {
         for (uint32_t k = P.root_leaf_first; k < P.root_leaf_first + P.root_leaf_count; ++k) {
             double t, u, v;
-            if (tri_test(load_tri(P.tris + k), o, d, tmin, tmax, t, u, v)) {
+            if (tri_test<kG>(load_tri(P.tris + k), o, d, tmin, tmax, t, u, v)) {
                 best = {k, t, u, v}; have = true;
                 if (kAnyHit) return true;
                 tmax = t;
@@ -143,7 +167,7 @@ __device__ bool trace(const KParams64& P, D3 o, D3 d, uint32_t* stk, Hit& best, 
         while (k < k_end || k2 < k2_end) {
             const uint32_t idx = k < k_end ? k++ : k2++;
             double t, u, v;
-            if (tri_test(load_tri(P.tris + idx), o, d, tmin, tmax, t, u, v)) {
+            if (tri_test<kG>(load_tri(P.tris + idx), o, d, tmin, tmax, t, u, v)) {
                 best = {idx, t, u, v}; have = true;
                 if (kAnyHit) return true;
                 tmax = t;
@@ -181,6 +205,7 @@ __device__ __forceinline__ float pow24_from_double(double x) {
 }
 
 // smooth_shading<double> (render.hpp:46-84): float helpers, double weights, float accumulators
+template <bool kG>
 __device__ __forceinline__ void shade(D3 sun_line, const double* nrm, D3 view, double u, double v, float c[3]) {
     c[0] = c[1] = c[2] = 0.0f;
     const float amb = 0.2;
@@ -189,14 +214,14 @@ __device__ __forceinline__ void shade(D3 sun_line, const double* nrm, D3 view, d
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const D3 N{nrm[3 * k], nrm[3 * k + 1], nrm[3 * k + 2]};
-        const float lam = float(fabs(sun_line.x * N.x + sun_line.y * N.y + sun_line.z * N.z));   // lambertian
-        const float diffuse = 0.5f * lam;
-        const float spec = 0.8f * pow24_from_double(dot(N, normalize(sun_line + vneg)));        // blinn_phong_spec
-        const float base = amb + diffuse;
+        const float lam = float(fabs(kG ? dotA<true>(sun_line, N) : sun_line.x * N.x + sun_line.y * N.y + sun_line.z * N.z));   // lambertian
+        const float spec = 0.8f * pow24_from_double(dotA<kG>(N, normalizeG<kG>(sun_line + vneg)));  // blinn_phong_spec
+        const float base = kG ? __builtin_fmaf(lam, 0.5f, amb) : amb + 0.5f * lam;
         auto clamp01 = [](float x) { return (x < 0.f) ? 0.f : (1.f < x) ? 1.f : x; };          // std::clamp
-        c[0] = float(double(c[0]) + w[k] * double(clamp01(base * 0.5f + spec)));
-        c[1] = float(double(c[1]) + w[k] * double(clamp01(base * 0.0f + spec)));
-        c[2] = float(double(c[2]) + w[k] * double(clamp01(base * 0.8f + spec)));
+        auto ch = [&](float k) { return kG ? __builtin_fmaf(base, k, spec) : base * k + spec; };
+        c[0] = float(double(c[0]) + w[k] * double(clamp01(ch(0.5f))));
+        c[1] = float(double(c[1]) + w[k] * double(clamp01(ch(0.0f))));
+        c[2] = float(double(c[2]) + w[k] * double(clamp01(ch(0.8f))));
     }
 }
 
@@ -216,7 +241,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // 1-D grid over the frame's kTile x kTile tiles in tile_order (as the float path: expensive tiles
 // first, every XCD an unbiased share); each wavefront an 8x8 tile (of its workgroup's 16x16
 // pixels when kBlock = 256)
-template <int kMode>
+template <int kMode, bool kG>
 __global__ __launch_bounds__(kBlock) void ceres_render64(const KParams64 P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -239,32 +264,44 @@ __global__ __launch_bounds__(kBlock) void ceres_render64(const KParams64 P) {
         // render.hpp:109-113
         const double u = 2 * (double(i) + 0.5) / double(P.W) - 1.0;
         const double v = 2 * (double(j) + 0.5) / double(P.H) - 1.0;
-        const D3 view = normalize(d3(c.iu) * u + d3(c.iv) * v + d3(c.dir));
+        D3 a;
+        if constexpr (kG)                                            // GCC: dir + fma(iv, v, iu u)
+            a = D3{c.dir[0] + fma(c.iv[0], v, c.iu[0] * u), c.dir[1] + fma(c.iv[1], v, c.iu[1] * u),
+                   c.dir[2] + fma(c.iv[2], v, c.iu[2] * u)};
+        else a = d3(c.iu) * u + d3(c.iv) * v + d3(c.dir);
+        const D3 view = normalizeG<kG>(a);
         Hit h{};
-        const bool hit = trace<false>(P, d3(c.eye), view, stk, h, overflow);
+        const bool hit = trace<false, kG>(P, d3(c.eye), view, stk, h, overflow);
         double px[3] = {0.0, 0.0, 0.0};
         int8_t shadow_rec = -1;
         if (hit) {
             n_hit = 1;
             const TriD tri = load_tri(P.tris + h.slot);
-            const D3 normal = normalize(tri.n);
+            const D3 normal = normalizeG<kG>(tri.n);
             if (kMode == CERES_MODE_PRIMARY) {                        // render.hpp:123-125
                 px[0] = fabs(normal.x); px[1] = fabs(normal.y); px[2] = fabs(normal.z);
             } else {
                 const D3 p1 = tri.p0 - tri.e1, p2 = tri.p0 + tri.e2;   // p1(), p2()
-                D3 p = h.u * tri.p0 + h.v * p1 + (1 - h.u - h.v) * p2;   // render.hpp:129 (permuted weights)
                 const double scale = -0.00001;
-                p = p + scale * normal;
-                const D3 sun_line = normalize(d3(c.sun) - p);          // render.hpp:135
+                D3 p;
+                if constexpr (kG) {                                  // GCC: fma(n, scale, fma(w, p2, fma(v, p1, u p0)))
+                    const double w = 1 - h.u - h.v;
+                    auto cp = [&](double a0, double q1, double q2, double n) { return fma(n, scale, fma(w, q2, fma(h.v, q1, h.u * a0))); };
+                    p = D3{cp(tri.p0.x, p1.x, p2.x, normal.x), cp(tri.p0.y, p1.y, p2.y, normal.y), cp(tri.p0.z, p1.z, p2.z, normal.z)};
+                } else {
+                    p = h.u * tri.p0 + h.v * p1 + (1 - h.u - h.v) * p2;   // render.hpp:129 (permuted weights)
+                    p = p + scale * normal;
+                }
+                const D3 sun_line = normalizeG<kG>(d3(c.sun) - p);     // render.hpp:135
                 Hit h2;
                 n_shadow = 1;
-                const bool blocked = trace<true>(P, p, sun_line, stk, h2, overflow);
+                const bool blocked = trace<true, kG>(P, p, sun_line, stk, h2, overflow);
                 shadow_rec = blocked ? 1 : 0;
                 if (blocked) {
                     n_occ = 1;
                 } else {
                     float col[3];
-                    shade(sun_line, P.norms + 9 * size_t(P.orig[h.slot]), view, h.u, h.v, col);
+                    shade<kG>(sun_line, P.norms + 9 * size_t(P.orig[h.slot]), view, h.u, h.v, col);
                     px[0] = col[0]; px[1] = col[1]; px[2] = col[2];
                 }
             }
@@ -313,6 +350,8 @@ int render64(ceres_scene* s, const double basis12[12], const double sun[3], int 
              uint8_t* d_rgb, int32_t* d_prim, double* d_tuv, int8_t* d_sh, ceres_stats* st) {
     if (!s || !basis12 || !sun) return set_error(CERES_EINVAL, "ceres_render_f64: null argument");
     if (!s->f64) return set_error(CERES_EINVAL, "scene is single precision: use ceres_render_f32");
+    const bool gfma = (mode & CERES_MODE_FMA) != 0;                 // the reference CMake build's FMA contraction
+    mode &= ~CERES_MODE_FMA;
     if (mode != CERES_MODE_FULL && mode != CERES_MODE_PRIMARY) return set_error(CERES_EINVAL, "bad mode %d", mode);
     if (W == 0 || H == 0 || W > 65535u * kTile || H > 65535u * kTile) return set_error(CERES_EINVAL, "bad frame size %zux%zu", W, H);
     HIP64_TRY(hipSetDevice(s->device));
@@ -339,8 +378,10 @@ int render64(ceres_scene* s, const double basis12[12], const double sun[3], int 
     const dim3 grid(tx * ty), block(kBlock);
     const size_t lds = size_t(s->stack_entries) * kBlock * 4;
     HIP64_TRY(hipEventRecord(e0, s->stream));
-    if (mode == CERES_MODE_PRIMARY) hipLaunchKernelGGL(ceres_render64<CERES_MODE_PRIMARY>, grid, block, lds, s->stream, P);
-    else hipLaunchKernelGGL(ceres_render64<CERES_MODE_FULL>, grid, block, lds, s->stream, P);
+    if (mode == CERES_MODE_PRIMARY && gfma) hipLaunchKernelGGL((ceres_render64<CERES_MODE_PRIMARY, true>), grid, block, lds, s->stream, P);
+    else if (mode == CERES_MODE_PRIMARY) hipLaunchKernelGGL((ceres_render64<CERES_MODE_PRIMARY, false>), grid, block, lds, s->stream, P);
+    else if (gfma) hipLaunchKernelGGL((ceres_render64<CERES_MODE_FULL, true>), grid, block, lds, s->stream, P);
+    else hipLaunchKernelGGL((ceres_render64<CERES_MODE_FULL, false>), grid, block, lds, s->stream, P);
     HIP64_TRY(hipGetLastError());
     HIP64_TRY(hipEventRecord(e1, s->stream));
     std::vector<Shard> sh(kShards);

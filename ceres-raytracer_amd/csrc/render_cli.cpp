@@ -11,7 +11,7 @@
 //                [--orbit ax ay az step_deg count] [--frames N] [--gpu-bvh] [--double|-d]
 //                [--gpus N] [--row-block R] [--robust] [--qbvh] [--exact | --fma]
 //
-// Arithmetic (float pipeline): --fma (the default) computes every step as the reference's own
+// Arithmetic (float and double pipelines): --fma (the default) computes every step as the reference's own
 // CMake build does (CMakeLists.txt:11-13, g++ -O3 -mavx2 -mfma: GCC contracts a*b+c into FMA at
 // the sites listed in oracle/contraction_sites.txt) -- the scene (normals, rotation, SAH costs),
 // the camera basis, the orbit and the kernels (CERES_ARITH_FMA + CERES_MODE_FMA), so the PPM is
@@ -164,19 +164,20 @@ template <> struct Api<float> {
 };
 template <> struct Api<double> {
     using Node = uint64_t;
-    // render<double>: the contraction-free double build (its FMA sites are not modelled)
-    static int load(const char* p, double** t, double** n, size_t* c, int) { return ceres_obj_load_f64(p, t, n, c); }
-    static int proc(int k, double** t, double** n, size_t* c, int) { return ceres_proc_mesh_f64(k, t, n, c); }
-    static int rotate(double* t, size_t c, int ax, double deg, int) { return ceres_rotate_triangles_f64(t, c, ax, deg); }
-    static int bvh(const double* t, size_t c, Node** nodes, size_t* m, uint64_t** prim, bool gpu, int, int) {
+    // render<double> in either arithmetic (--fma: anim.cpp -d as the reference's CMake build compiles it)
+    static int load(const char* p, double** t, double** n, size_t* c, int ar) { return ceres_obj_load_f64_arith(p, t, n, c, ar); }
+    static int proc(int k, double** t, double** n, size_t* c, int ar) { return ceres_proc_mesh_f64_arith(k, t, n, c, ar); }
+    static int rotate(double* t, size_t c, int ax, double deg, int ar) { return ceres_rotate_triangles_f64_arith(t, c, ax, deg, ar); }
+    static int bvh(const double* t, size_t c, Node** nodes, size_t* m, uint64_t** prim, bool gpu, int, int ar) {
         if (gpu) { std::fprintf(stderr, "error: --gpu-bvh builds single-precision BVHs only\n"); return CERES_EUNSUPPORTED; }
-        return ceres_bvh_build_f64(t, c, nodes, m, prim);
+        return ceres_bvh_build_f64_arith(t, c, nodes, m, prim, ar);
     }
     static ceres_scene* scene(const double* t, size_t c, const double* n, const Node* nodes, size_t m, const uint64_t* prim, int dev) {
         return ceres_scene_create_f64(t, c, n, nodes, m, prim, dev, 0);
     }
-    static int orbit(const Num<double>& v, size_t W, size_t H, uint32_t k, double* b, double* s, int) {
-        return ceres_orbit_cameras_f64(v.eye, v.dir, v.up, v.sun, v.fov, W, H, v.orbit_axis, v.orbit_step, k, 0, b, s, nullptr);
+    static int orbit(const Num<double>& v, size_t W, size_t H, uint32_t k, double* b, double* s, int ar) {
+        return ceres_orbit_cameras_f64_arith(v.eye, v.dir, v.up, v.sun, v.fov, W, H, v.orbit_axis, v.orbit_step, k, 0, b, s,
+                                             nullptr, ar);
     }
     static int render(ceres_scene* sc, const double* b, const double* s, int mode, uint8_t* rgb, size_t W, size_t H, ceres_stats* st) {
         return ceres_render_f64(sc, b, s, mode, nullptr, rgb, W, H, st);
@@ -299,7 +300,6 @@ int run(const Opts& o, const Num<S>& v) {
 int main(int argc, char** argv) {
     Opts o;
     if (!parse(argc, argv, o)) return usage();
-    if (o.f64) o.arith = CERES_ARITH_EXACT;                      // render<double>: contraction-free only
     if (o.arith == CERES_ARITH_FMA) o.mode |= CERES_MODE_FMA;
     return o.f64 ? run<double>(o, o.d) : run<float>(o, o.f);
 }

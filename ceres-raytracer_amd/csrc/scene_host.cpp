@@ -804,4 +804,78 @@ int ceres_orbit_cameras_arith(const float eye[3], const float dir[3], const floa
                                                rotate_first, basis12, sun3, dir3);
 }
 
+// render<double> in the reference CMake build's arithmetic (anim.cpp -d compiled with -mfma,
+// CMakeLists.txt:11): GCC fuses the double host steps at the same sites as the float ones
+// (oracle/contraction_sites.txt; the double dump's FMA sites -- triangle normals, rotation, vertex
+// normals, SAH costs -- carry the same expressions), so the G = true templates serve both scalars.
+int ceres_obj_load_f64_arith(const char* path, double** tri96, double** norm72, size_t* n_tri, int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? obj_load<double, true>(path, tri96, norm72, n_tri) : obj_load<double, false>(path, tri96, norm72, n_tri);
+}
+int ceres_proc_mesh_f64_arith(int n, double** tri96, double** norm72, size_t* n_tri, int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? proc_mesh<double, true>(n, tri96, norm72, n_tri) : proc_mesh<double, false>(n, tri96, norm72, n_tri);
+}
+int ceres_rotate_triangles_f64_arith(double* tri96, size_t n_tri, int axis, double degrees, int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? rotate_triangles<double, true>(tri96, n_tri, axis, degrees)
+                 : rotate_triangles<double, false>(tri96, n_tri, axis, degrees);
+}
+int ceres_bvh_build_f64_arith(const double* tri96, size_t n_tri, uint64_t** nodes64, size_t* n_nodes, uint64_t** prim64,
+                              int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    if (!nodes64) return set_error(CERES_EINVAL, "ceres_bvh_build_f64: null argument");
+    NodeT<double>* nodes = nullptr;
+    const int rc = arith ? bvh_build<double, true>(tri96, n_tri, &nodes, n_nodes, prim64)
+                         : bvh_build<double, false>(tri96, n_tri, &nodes, n_nodes, prim64);
+    *nodes64 = reinterpret_cast<uint64_t*>(nodes);
+    return rc;
+}
+int ceres_camera_basis_f64_arith(const double eye[3], const double dir[3], const double up[3], double fov_deg,
+                                 size_t width, size_t height, double out9[9], int arith) {
+    (void)eye;
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? camera_basis<double, true>(dir, up, fov_deg, width, height, out9)
+                 : camera_basis<double, false>(dir, up, fov_deg, width, height, out9);
+}
+int ceres_orbit_cameras_f64_arith(const double eye[3], const double dir[3], const double up[3], const double sun[3],
+                                  double fov_deg, size_t width, size_t height, const double axis[3], double step_deg,
+                                  uint32_t n_frames, int rotate_first, double* basis12, double* sun3, double* dir3,
+                                  int arith) {
+    if (int rc = bad_arith(arith)) return rc;
+    return arith ? orbit_cameras<double, true>(eye, dir, up, sun, fov_deg, width, height, axis, step_deg, n_frames,
+                                               rotate_first, basis12, sun3, dir3)
+                 : orbit_cameras<double, false>(eye, dir, up, sun, fov_deg, width, height, axis, step_deg, n_frames,
+                                                rotate_first, basis12, sun3, dir3);
+}
+
 }  // extern "C"
+
+// ---------------------------------------------------------------- compacted float readback
+// render.hpp:86-89 writes every pixel of the caller's float framebuffer; ceres_render_f32 sends
+// only the lit pixels over the host link (a C3 frame: ~7 % of them) and writes the rest here as
+// zeros -- the bits the reference stores for a miss or a shadowed hit (render.hpp:116-117,147-150).
+// The fill runs on the caller's cores while the kernel runs.
+namespace ceres {
+static int host_threads() {
+    const int t = omp_get_max_threads();
+    return t < 1 ? 1 : t > 16 ? 16 : t;
+}
+void host_fill_zero(float* dst, size_t n) {
+    const size_t chunk = size_t(1) << 16;                            // 256 KB per task
+    const long long nc = (long long)((n + chunk - 1) / chunk);
+    #pragma omp parallel for schedule(static) num_threads(host_threads())
+    for (long long c = 0; c < nc; ++c) {
+        const size_t a = size_t(c) * chunk, b = std::min(n, a + chunk);
+        std::memset(dst + a, 0, (b - a) * sizeof(float));
+    }
+}
+void host_scatter_lit(float* dst, const uint32_t* lit4, size_t n) {    // records {pixel, r, g, b} (bits)
+    #pragma omp parallel for schedule(static) num_threads(host_threads()) if (n > 16384)
+    for (long long k = 0; k < (long long)n; ++k) {
+        const uint32_t* r = lit4 + 4 * size_t(k);
+        uint32_t* q = reinterpret_cast<uint32_t*>(dst + 3 * size_t(r[0]));
+        q[0] = r[1]; q[1] = r[2]; q[2] = r[3];
+    }
+}
+}  // namespace ceres

@@ -58,6 +58,17 @@ struct ceres_scene {
     hipStream_t copy_stream = nullptr;
     uint64_t* d_band_counters = nullptr;
     std::vector<hipEvent_t> band_events;
+    // host float framebuffers (ceres_render_f32): the lit pixels -- those with any non-zero bit --
+    // compacted on the device into {index, r, g, b} records, copied, and scattered over a host
+    // zero fill that overlaps the kernel (host_fill_zero / host_scatter_lit, scene_host.cpp)
+    uint4* d_lit = nullptr;
+    uint32_t* d_lit_count = nullptr;
+    size_t lit_cap = 0;
+    uint32_t* h_small = nullptr;       // pinned: lit count + 8 counters
+    std::vector<uint4> h_lit;
+    double last_lit_frac = 0.0;        // the previous call's lit fraction (dense frames take the full copy)
+    uint32_t dense_calls = 0;
+    hipEvent_t ev_count = nullptr;
     int num_cus = 256;
     unsigned long long* d_wave_log = nullptr;   // stats scenes: per-wave diagnostic records
     size_t wave_log_waves = 0, last_grid_waves = 0;
@@ -73,6 +84,9 @@ struct ceres_scene {
 };
 
 namespace ceres {
+// host side of the compacted float readback (scene_host.cpp, OpenMP over the caller's cores)
+void host_fill_zero(float* dst, size_t n);
+void host_scatter_lit(float* dst, const uint32_t* lit4, size_t n);   // records {pixel, r, g, b}
 void scene_release(ceres_scene* s);          // frees every device buffer and the stream (render_hip.hip)
 // centre-first, XCD-balanced order of one whole frame's tile x tile tiles (render_hip.hip)
 int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out);

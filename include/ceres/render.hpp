@@ -137,13 +137,14 @@ struct Camera {                                                      // render.h
 
 // render.hpp:24-44 -- rotation about one axis, in place, rebuilding each triangle from p0,
 // p1() = p0 - e1, p2() = p0 + e2 (bit-identical to the reference in CERES_DROPIN_ARITH's
-// arithmetic; float scenes -- the double build's contraction is not modelled; runs on the host).
+// arithmetic, float and double scenes; runs on the host).
 template <size_t Axis, typename Scalar, typename Tri>
 static void rotate_triangles(Scalar degrees, Tri* triangles, size_t triangle_count) {
     static_assert((std::is_same<Scalar, float>::value && sizeof(Tri) == 48) ||
                   (std::is_same<Scalar, double>::value && sizeof(Tri) == 96), "ceres: bvh::Triangle<float|double> only");
     const int rc = std::is_same<Scalar, double>::value
-        ? ceres_rotate_triangles_f64(reinterpret_cast<double*>(triangles), triangle_count, int(Axis), double(degrees))
+        ? ceres_rotate_triangles_f64_arith(reinterpret_cast<double*>(triangles), triangle_count, int(Axis), double(degrees),
+                                           CERES_DROPIN_ARITH)
         : ceres_rotate_triangles_arith(reinterpret_cast<float*>(triangles), triangle_count, int(Axis), float(degrees),
                                        CERES_DROPIN_ARITH);
     if (rc != CERES_OK) ceres::detail::fail("rotate_triangles");
@@ -214,8 +215,10 @@ std::pair<int, int> render(const Camera<Scalar>& camera, const Vec& sun_position
     ceres_stats st{};
     int rc;
     if constexpr (kF64) {
-        if (ceres_camera_basis_f64(eye, dir, up, camera.fov, width, height, basis + 3) != CERES_OK) ceres::detail::fail("camera basis");
-        rc = ceres_render_f64(c.scene, basis, sun, CERES_MODE_FULL, pixels, nullptr, width, height, &st);
+        if (ceres_camera_basis_f64_arith(eye, dir, up, camera.fov, width, height, basis + 3, CERES_DROPIN_ARITH) != CERES_OK)
+            ceres::detail::fail("camera basis");
+        const int mode = CERES_MODE_FULL | (CERES_DROPIN_ARITH == CERES_ARITH_FMA ? CERES_MODE_FMA : 0);
+        rc = ceres_render_f64(c.scene, basis, sun, mode, pixels, nullptr, width, height, &st);
     } else {
         if (ceres_camera_basis_arith(eye, dir, up, camera.fov, width, height, basis + 3, CERES_DROPIN_ARITH) != CERES_OK)
             ceres::detail::fail("camera basis");

@@ -184,6 +184,19 @@ int ceres_camera_basis_f64(const double eye[3], const double dir[3], const doubl
 int ceres_orbit_cameras_f64(const double eye[3], const double dir[3], const double up[3], const double sun[3],
                             double fov_deg, size_t width, size_t height, const double axis[3], double step_deg,
                             uint32_t n_frames, int rotate_first, double* basis12, double* sun3, double* dir3);
+/* The same double steps in a chosen arithmetic (CERES_ARITH_FMA: anim.cpp -d as the reference's
+ * CMake build compiles it, -O3 -mavx2 -mfma; pair with CERES_MODE_FMA renders). */
+int ceres_obj_load_f64_arith(const char* path, double** tri96, double** norm72, size_t* n_tri, int arith);
+int ceres_proc_mesh_f64_arith(int n, double** tri96, double** norm72, size_t* n_tri, int arith);
+int ceres_rotate_triangles_f64_arith(double* tri96, size_t n_tri, int axis, double degrees, int arith);
+int ceres_bvh_build_f64_arith(const double* tri96, size_t n_tri, uint64_t** nodes64, size_t* n_nodes,
+                              uint64_t** prim64, int arith);
+int ceres_camera_basis_f64_arith(const double eye[3], const double dir[3], const double up[3], double fov_deg,
+                                 size_t width, size_t height, double out9[9], int arith);
+int ceres_orbit_cameras_f64_arith(const double eye[3], const double dir[3], const double up[3], const double sun[3],
+                                  double fov_deg, size_t width, size_t height, const double axis[3], double step_deg,
+                                  uint32_t n_frames, int rotate_first, double* basis12, double* sun3, double* dir3,
+                                  int arith);
 
 /* ---- device scene ---- */
 

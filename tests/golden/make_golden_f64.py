@@ -10,6 +10,8 @@ oracle/ref_harness.cpp compiled with Scalar = double from the unmodified headers
   <cfg>.exact.ppm.gz   PPM of the contraction-free build (small configs)
   <cfg>.records.npz    per-pixel {pixel, prim, t, u, v, shadow, rgb} (float64) of the
                        contraction-free build, every pixel for small configs, else a sample
+  <cfg>.ref.records.npz  the same pixels in the reference-flag build (round 5), whose scene
+                       hashes, camera basis, pose and statistics are the "ref*" keys of the JSON
 
 Command-line numbers reach the harness as decimal strings parsed with strtod, i.e. the
 configs' values are double literals (as anim.cpp writes its camera).
@@ -82,7 +84,9 @@ def make(name):
     p_ex = os.path.join(SCRATCH, name + ".exact.ppm")
     p_rec = os.path.join(SCRATCH, name + ".records.bin")
     p_dump = os.path.join(SCRATCH, name)
-    j_ref = run(REF, cfg, ["--out", p_ref])
+    p_rrec = os.path.join(SCRATCH, name + ".ref.records.bin")
+    p_rdump = os.path.join(SCRATCH, name + ".ref")
+    j_ref = run(REF, cfg, ["--out", p_ref, "--stats", "--records", p_rrec, "--dump", p_rdump])
     j_ex = run(REF_EXACT, cfg, ["--out", p_ex, "--stats", "--records", p_rec, "--dump", p_dump])
     ppm_ref = open(p_ref, "rb").read()
     ppm_ex = open(p_ex, "rb").read()
@@ -93,7 +97,13 @@ def make(name):
         "n_tri": j_ex["n_tri"], "n_nodes": j_ex["n_nodes"],
         "exact": {k: j_ex[k] for k in ("rays", "hits", "primary_pairs", "primary_tests", "shadow_rays",
                                        "shadow_pairs", "shadow_tests", "loop_vs_render_mismatch")},
-        "ref": {k: j_ref[k] for k in ("rays", "hits")},
+        "ref": {k: j_ref[k] for k in ("rays", "hits", "primary_pairs", "primary_tests", "shadow_rays",
+                                      "shadow_pairs", "shadow_tests", "loop_vs_render_mismatch")},
+        "ref_basis": {"dir": j_ref["basis_dir"], "u": j_ref["basis_u"], "v": j_ref["basis_v"]},
+        "ref_pose": {"eye": j_ref["eye"], "sun": j_ref["sun"]},
+        "ref_scene": {"tri96_sha256": sha(p_rdump + ".tri96"), "norm72_sha256": sha(p_rdump + ".norm72"),
+                      "bvh_canonical_sha256": canonical_bvh64_sha(open(p_rdump + ".nodes64", "rb").read(),
+                                                                  open(p_rdump + ".prim64", "rb").read())},
         "basis": {"dir": j_ex["basis_dir"], "u": j_ex["basis_u"], "v": j_ex["basis_v"]},
         "pose": {"eye": j_ex["eye"], "sun": j_ex["sun"]},
         "ppm_sha256": {"exact": sha(ppm_ex), "ref": sha(ppm_ref)},
@@ -120,13 +130,19 @@ def make(name):
                         prim=r["prim"], t=r["t"], u=r["u"], v=r["v"], shadow=r["shadow"],
                         rgb=np.stack([r["r"], r["g"], r["b"]], axis=1))
     meta["records"] = {"count": int(keep.size), "sampled": not small, "seed": SEED}
+    rr = np.fromfile(p_rrec, dtype=REC_DTYPE)[keep]
+    np.savez_compressed(os.path.join(OUT, name + ".ref.records.npz"),
+                        pixel=(rr["j"].astype(np.uint64) * W + rr["i"]).astype(np.uint32),
+                        prim=rr["prim"], t=rr["t"], u=rr["u"], v=rr["v"], shadow=rr["shadow"],
+                        rgb=np.stack([rr["r"], rr["g"], rr["b"]], axis=1))
     if small:
         with open(os.path.join(OUT, name + ".exact.ppm.gz"), "wb") as f:
             f.write(gzip.compress(ppm_ex, mtime=0))
     with open(os.path.join(OUT, name + ".json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
         f.write("\n")
-    for p in (p_ref, p_ex, p_rec, p_dump + ".tri96", p_dump + ".norm72", p_dump + ".nodes64", p_dump + ".prim64"):
+    for p in (p_ref, p_ex, p_rec, p_rrec, p_dump + ".tri96", p_dump + ".norm72", p_dump + ".nodes64", p_dump + ".prim64",
+              p_rdump + ".tri96", p_rdump + ".norm72", p_rdump + ".nodes64", p_rdump + ".prim64"):
         os.remove(p)
     print(name, meta["exact"]["rays"], meta["exact"]["hits"], meta["ppm_bytes_differing_ref_vs_exact"], flush=True)
 

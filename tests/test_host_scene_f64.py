@@ -24,20 +24,35 @@ def hex64(a):
 
 
 @pytest.mark.parametrize("name", NAMES)
-def test_f64_scene_prep_matches_reference(pkg, name):
+@pytest.mark.parametrize("build", ["exact", "ref"])
+def test_f64_scene_prep_matches_reference(pkg, name, build):
+    """build "exact": the -ffp-contract=off double build; "ref": the reference's own CMake build
+    (-O3 -mavx2 -mfma, GCC's FMA contraction; CERES_ARITH_FMA) -- round 5."""
     import make_golden_f64
     meta = json.load(open(os.path.join(F64, name + ".json")))
     cfg = configs.CONFIGS[name]
-    mesh, bvh, cam = pkg.prepare(cfg, f64=True)
+    arith = 1 if build == "ref" else 0
+    want = meta["ref_scene"] if build == "ref" else meta
+    basis, pose = (meta["ref_basis"], meta["ref_pose"]) if build == "ref" else (meta["basis"], meta["pose"])
+    mesh, bvh, cam = pkg.prepare(cfg, f64=True, arith=arith)
     assert mesh.tri.dtype == np.float64 and len(mesh) == meta["n_tri"]
-    assert hashlib.sha256(mesh.tri.tobytes()).hexdigest() == meta["tri96_sha256"]
-    assert hashlib.sha256(mesh.norm.tobytes()).hexdigest() == meta["norm72_sha256"]
-    assert bvh.nodes.shape[0] == meta["n_nodes"]
-    assert make_golden_f64.canonical_bvh64_sha(bvh.nodes.tobytes(), bvh.prim.tobytes()) == meta["bvh_canonical_sha256"]
+    assert hashlib.sha256(mesh.tri.tobytes()).hexdigest() == want["tri96_sha256"]
+    assert hashlib.sha256(mesh.norm.tobytes()).hexdigest() == want["norm72_sha256"]
+    assert make_golden_f64.canonical_bvh64_sha(bvh.nodes.tobytes(), bvh.prim.tobytes()) == want["bvh_canonical_sha256"]
+    if build == "exact":
+        assert bvh.nodes.shape[0] == meta["n_nodes"]
     b = cam.basis(cfg["W"], cfg["H"])
-    assert hex64(b[:3]) == meta["pose"]["eye"]
-    assert hex64(b[3:]) == meta["basis"]["dir"] + meta["basis"]["u"] + meta["basis"]["v"]
-    assert hex64(pkg.pose_f64(cfg)[1]) == meta["pose"]["sun"]
+    assert hex64(b[:3]) == pose["eye"]
+    assert hex64(b[3:]) == basis["dir"] + basis["u"] + basis["v"]
+    assert hex64(pkg.pose_f64(cfg, arith)[1]) == pose["sun"]
+
+
+def test_f64_builds_differ_in_the_scene():
+    """The two double builds do prepare different scenes (FMA contraction of the normals and the
+    rotation), so the "ref" cases above pin something the "exact" ones do not."""
+    differ = [n for n in NAMES if json.load(open(os.path.join(F64, n + ".json")))["ref_scene"]["tri96_sha256"] !=
+              json.load(open(os.path.join(F64, n + ".json")))["tri96_sha256"]]
+    assert len(differ) >= 6, differ
 
 
 def test_f64_fixtures_cover_the_paths():

@@ -2,7 +2,7 @@
 # static.cpp-style tools/probes/dropin_bench through include/ceres/render.hpp (host float
 # framebuffer) and ./render --bench (RGB8 to the host), dragon 1080p (C3) and 4096^2.
 # BANDS="1 2 4 8" sweeps ceres_render_f32's row bands (CERES_HOST_BANDS).  Outputs under gpurun_out/e2e/.
-set -u; cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; OUT=gpurun_out/e2e; mkdir -p $OUT
+set -u; cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; OUT=gpurun_out/${TAG:-e2e}; mkdir -p $OUT
 A="data/dragon.obj --eye 0.0 -15.0 2.0 --dir 0.0 1.0 0.0 --up 0.0 0.0 1.0 --sun -50.0 -20.0 0.0 --rotate x 90.0"
 for bands in ${BANDS:-4}; do
 export CERES_HOST_BANDS=$bands
