@@ -53,7 +53,7 @@ def _bench_lines():
         with open(p) as f:
             lines = [ln for ln in f if ln.startswith("{") and '"roofline"' in ln]
         if lines:
-            out.append((os.path.basename(p), json.loads(lines[-1])))
+            out.append((os.path.relpath(p, os.path.join(REPO, "profiles")), json.loads(lines[-1])))
     return out
 
 
@@ -98,15 +98,17 @@ def test_committed_sweep_roofline_recomputes(bench, name, line):
 
 def _check_trace_agreement(name, line):
     """Round 5: a bench line kept next to a single-stream rocprofv3 trace of the
-    same launch (`<dir>/trace_<cfg>_kernel_stats.csv`, tools/batch_launch.py) must agree with it on
-    the mean launch duration within 3 %."""
+    same launch (`<dir>/trace_batch_<cfg>_<arith>_kernel_stats.csv`, tools/batch_launch.py under
+    rocprofv3 --kernel-trace --stats, same session) must agree with it on the mean launch duration
+    within 3 %."""
     import csv
     rf = line["roofline"]
     cfg = line["config"]["workload"].split(":")[0]
-    for p in glob.glob(os.path.join(REPO, "profiles", "r05", "**", f"trace_batch_{cfg}_{line['arith']}_kernel_stats.csv"),
-                       recursive=True):
+    # the trace kept in the same directory as the bench line (one session, one build)
+    for p in glob.glob(os.path.join(REPO, "profiles", os.path.dirname(name),
+                                    f"trace_batch_{cfg}_{line['arith']}_kernel_stats.csv")):
         with open(p) as f:
-            rows = [r for r in csv.DictReader(f) if r["Name"].startswith(rf["kernel"])]
+            rows = [r for r in csv.DictReader(f) if rf["kernel"] + "<" in r["Name"]]
         assert rows, p
         avg_ms = float(rows[0]["AverageNs"]) / 1e6
         assert abs(avg_ms - rf["mean_launch_ms"]) <= 0.03 * avg_ms, (name, p, avg_ms, rf["mean_launch_ms"])
@@ -137,3 +139,11 @@ def test_committed_roofline_step_recomputes(bench, name, line):
     for k in ("achieved_job", "achieved_per_gpu", "frac_l2", "frac_hbm"):
         assert abs(again[k] - rs[k]) <= 1e-3 * abs(rs[k]) + 1e-3, k
     assert again["frac_l2"] <= 1.0
+
+
+def test_headline_trace_pairing_is_kept():
+    """The final build's headline launch has its bench line and single-stream trace side by side
+    (the check above is not vacuous): at least one profiles/r05 directory holds both."""
+    pairs = [p for p in glob.glob(os.path.join(REPO, "profiles", "r05", "**", "trace_batch_dragon_1080_fma_kernel_stats.csv"),
+                                  recursive=True) if os.path.exists(os.path.join(os.path.dirname(p), "bench_dragon_1080.log"))]
+    assert pairs
