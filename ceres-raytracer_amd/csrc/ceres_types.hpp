@@ -62,7 +62,11 @@ static_assert(sizeof(SiblingPair64) == 112, "SiblingPair64");
 // boxes as SoA float4 rows, then one packed word per child: first << 5 | count (count 0: inner,
 // first = Node4 index; 1..31: leaf of `count` triangles from leaf slot `first`), kNode4Empty for
 // an unused slot.  One word per child keeps a traversal step at 7 vector loads instead of 8 (the
-// kernel pays per load instruction).  128 B = one L2 line; the last 16 B are unused.
+// kernel pays per load instruction).  128 B = one L2 line.  Children are stored leaves
+// first, then inner children, then empty slots (each group in build order: node4_leaves_first),
+// and nleaf counts the leaf children -- the packet walk's per-child leaf / inner split is one
+// compare against it.  An empty slot holds the inverted infinite box (lo +inf, hi -inf), which
+// every slab test fails.
 constexpr uint32_t kNode4Empty = 0xffffffffu;
 constexpr uint32_t kNode4CountBits = 5;
 constexpr uint32_t kNode4MaxCount = (1u << kNode4CountBits) - 1;             // 31
@@ -70,13 +74,39 @@ constexpr uint32_t kNode4MaxFirst = (1u << (32 - kNode4CountBits)) - 2;      // 
 struct alignas(128) Node4 {
     float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
     uint32_t child[4];
-    uint32_t unused[4];
+    uint32_t nleaf;
+    uint32_t unused[3];
 };
 static_assert(sizeof(Node4) == 128, "Node4");
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
 inline uint32_t node4_child(uint32_t count, uint32_t first) { return first << kNode4CountBits | count; }
+
+// Reorders a filled record's children: leaves, inner children, empty slots (stable within each
+// group, so the walk still meets inner children in build order), sets nleaf, zeroes the rest.
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline void node4_leaves_first(Node4& r) {
+    Node4 t;
+    uint32_t k = 0, nl = 0;
+    for (int pass = 0; pass < 3; ++pass)
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t w = r.child[c];
+            const int group = w == kNode4Empty ? 2 : (w & kNode4MaxCount) ? 0 : 1;
+            if (group != pass) continue;
+            t.lo_x[k] = r.lo_x[c]; t.hi_x[k] = r.hi_x[c];
+            t.lo_y[k] = r.lo_y[c]; t.hi_y[k] = r.hi_y[c];
+            t.lo_z[k] = r.lo_z[c]; t.hi_z[k] = r.hi_z[c];
+            t.child[k] = w;
+            nl += group == 0;
+            ++k;
+        }
+    t.nleaf = nl;
+    t.unused[0] = t.unused[1] = t.unused[2] = 0;
+    r = t;
+}
 
 // Compressed shadow BVH4 record (CERES_MODE_QBVH4; quantize_nodes4 in render_hip.hip): the node's
 // box origin and a power-of-two scale per axis, each child bound as one byte (4 children's lo_x

@@ -47,7 +47,8 @@
 
 #ifndef CERES_TILES_PER_WAVE
 #define CERES_TILES_PER_WAVE 4                // fused kernel, batches: consecutive tile-order entries (1, 2, 4 or 8) per
-#endif                                        // wavefront (A/B, 16-frame batches x 8 streams: 4 beats 2 by 2 %, 8 = 4)
+#endif                                        // wavefront (A/B, 16-frame batches x 8 streams: 4 beats 2 by 2 %; round 5
+                                              // profiles/r05/s8-s9: 8 vs 4 within +-1 %, no consistent sign)
 #ifndef CERES_FRAME_MAJOR_PIXELS
 #define CERES_FRAME_MAJOR_PIXELS (1u << 22)    // batches of frames of >= this many pixels: frame after frame (0: never)
 #endif
@@ -686,19 +687,24 @@ __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<fal
         const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
         const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
         const uint32_t chw[4] = {CH.x, CH.y, CH.z, CH.w};
-        uint64_t cm[4];
+        const uint32_t nleaf = sload_u32(&q->nleaf);
+        // per child the lanes whose ray passes its box; children 0..nleaf-1 are leaves, the rest
+        // inner or empty (node4_leaves_first).  An empty slot holds the inverted infinite box, which
+        // the octant-selected slab test always fails (entry +inf, exit -inf), so no empty-slot test.
+        uint64_t hm[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             float e, x;
             slab_box<false, kOct>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e, x);
-            cm[c] = chw[c] != kNode4Empty ? (__ballot(e <= x) & m) : 0;
+            hm[c] = __ballot(e <= x) & m;
         }
         // triangles of every passing leaf child, for the lanes that reach it and are not yet occluded
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
+            if (uint32_t(c) >= nleaf) break;
+            uint64_t lm = hm[c] & ~occ;
+            if (!lm) continue;
             const uint32_t n = n4_count(chw[c]);
-            uint64_t lm = cm[c] & ~occ;
-            if (!n || !lm) continue;
             // do-while (n > 0 and lm != 0 on entry), the hit mask straight from the compares: two plain
             // exits, no combined predicate (round 5 A/B: batches -0.3..-1.2 %)
             const Tri48* tp = P.tris + n4_first(chw[c]);
@@ -721,7 +727,8 @@ __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<fal
         uint64_t nm = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const uint64_t mm = n4_count(chw[c]) ? 0 : cm[c] & ~occ;
+            if (uint32_t(c) < nleaf) continue;
+            const uint64_t mm = hm[c] & ~occ;
             if (!mm) continue;
             if (nxt < 0) { nxt = c; nm = mm; continue; }
             const bool mine = lane == sp;                              // a write into lane sp

@@ -160,7 +160,8 @@ __global__ void __launch_bounds__(256) k_nodes4(const RefNode* __restrict__ node
     Node4 r;
     for (int q = 0; q < 4; ++q) {
         if (q >= n) {
-            r.lo_x[q] = r.hi_x[q] = r.lo_y[q] = r.hi_y[q] = r.lo_z[q] = r.hi_z[q] = 0.f;
+            r.lo_x[q] = r.lo_y[q] = r.lo_z[q] = INFINITY;             // the inverted infinite box (build_shadow_bvh4)
+            r.hi_x[q] = r.hi_y[q] = r.hi_z[q] = -INFINITY;
             r.child[q] = kNode4Empty;
             continue;
         }
@@ -172,7 +173,7 @@ __global__ void __launch_bounds__(256) k_nodes4(const RefNode* __restrict__ node
         if (e.primitive_count > kNode4MaxCount || first > kNode4MaxFirst) atomicOr(err, uint32_t(kErrNode4));
         r.child[q] = node4_child(e.primitive_count, first);
     }
-    for (int q = 0; q < 4; ++q) r.unused[q] = 0;
+    node4_leaves_first(r);
     out[node4_of[x]] = r;
 }
 

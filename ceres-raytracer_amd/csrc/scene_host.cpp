@@ -593,6 +593,13 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
     auto set_box = [](Node4& rec, int c, const float* b) {
         rec.lo_x[c] = b[0]; rec.hi_x[c] = b[1]; rec.lo_y[c] = b[2]; rec.hi_y[c] = b[3]; rec.lo_z[c] = b[4]; rec.hi_z[c] = b[5];
     };
+    // an empty slot: kNode4Empty and the inverted infinite box (lo +inf, hi -inf), which every
+    // octant-selected slab test fails (render_hip.hip packet_any4 tests no child word)
+    auto set_empty = [](Node4& rec, int c) {
+        rec.lo_x[c] = rec.lo_y[c] = rec.lo_z[c] = INFINITY;
+        rec.hi_x[c] = rec.hi_y[c] = rec.hi_z[c] = -INFINITY;
+        rec.child[c] = kNode4Empty;
+    };
     // child word of a leaf of `count` triangles from slot `first` reached with `acc` stack entries
     // held above it; oversized leaves are split into piece nodes (recursively, 4 ways)
     std::function<int(const float*, uint32_t, uint32_t, uint32_t, uint32_t&)> leaf_word =
@@ -610,12 +617,13 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
         Node4 rec{};
         for (uint32_t c = 0; c < 4; ++c) {
             const uint32_t lo = c * per, n = c < parts && lo < count ? std::min(per, count - lo) : 0;
-            if (!n) { rec.child[c] = kNode4Empty; continue; }
+            if (!n) { set_empty(rec, int(c)); continue; }
             set_box(rec, int(c), box);
             uint32_t w = 0;
             if (int rc = leaf_word(box, n, first + lo, acc2, w)) return rc;
             rec.child[c] = w;
         }
+        node4_leaves_first(rec);
         out[idx] = rec;
         word = node4_child(0, idx);
         return CERES_OK;
@@ -649,7 +657,7 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
         stack_bound = std::max(stack_bound, acc);
         Node4 rec{};
         for (int c = 0; c < 4; ++c) {
-            if (c >= n) { rec.child[c] = kNode4Empty; continue; }
+            if (c >= n) { set_empty(rec, c); continue; }
             set_box(rec, c, ents[c].box);
             if (ents[c].count) {
                 uint32_t w = 0;
@@ -666,6 +674,7 @@ int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>&
                 st.push_back({ents[c].first, idx, acc});
             }
         }
+        node4_leaves_first(rec);
         out[it.node4] = rec;
     }
     return CERES_OK;

@@ -16,3 +16,13 @@ for sz in "1920 1080" "4096 4096"; do
   rm -f $OUT/cli_$t.ppm
 done
 done
+# C5=1: the 10M-triangle scene through the drop-in (3840x2160, host float framebuffer), with the
+# per-call content hash (dropin_bench) and without it (dropin_bench_trust, CERES_DROPIN_TRUST_UNCHANGED)
+if [ -n "${C5:-}" ]; then
+  P="--proc 2237 --size 3840 2160 --eye 0.5 -0.4 0.6 --dir 0.0 0.9 -0.55 --up 0.0 0.0 1.0 --sun -50.0 -20.0 100.0"
+  for b in dropin_bench dropin_bench_trust; do
+    timeout -k 10 300 tools/probes/$b $P --reps ${C5_REPS:-10} --out $OUT/${b}_c5.ppm > $OUT/${b}_c5.json 2> $OUT/${b}_c5.err || { cat $OUT/${b}_c5.err; exit 3; }
+    echo "$b c5 $(cat $OUT/${b}_c5.json) sha=$(sha256sum $OUT/${b}_c5.ppm | cut -c1-64)"
+    rm -f $OUT/${b}_c5.ppm
+  done
+fi

@@ -6,7 +6,11 @@
 // it), and reports the wall time per call (e2e) beside the kernel's own device time
 // (ceres_render_f32 stats.ms) and the PPM sha-independent checks the test harness needs.
 //
-// usage: dropin_bench <obj> [--size W H] [--rotate x|y|z deg] [--eye x y z] [--dir x y z]
+// hash_ms: the per-call content hash of the caller's arrays alone (render.hpp's scene check,
+// ceres_content_hash over nodes, primitive_indices, triangles and tri_norms); the
+// dropin_bench_trust build defines CERES_DROPIN_TRUST_UNCHANGED and skips it.
+//
+// usage: dropin_bench <obj> | --proc N  [--size W H] [--rotate x|y|z deg] [--eye x y z] [--dir x y z]
 //                     [--up x y z] [--sun x y z] [--reps N] [--out f.ppm]
 #include <algorithm>
 #include <chrono>
@@ -21,7 +25,7 @@
 int main(int argc, char** argv) {
     std::string obj;
     size_t W = 1920, H = 1080;
-    int rot_axis = -1, reps = 50;
+    int rot_axis = -1, reps = 50, proc = 0;
     float rot_deg = 0.f;
     float eye[3] = {0.f, -15.f, 2.f}, dir[3] = {0.f, 1.f, 0.f}, up[3] = {0.f, 0.f, 1.f}, sun[3] = {-50.f, -20.f, 0.f};
     std::string out;
@@ -35,13 +39,15 @@ int main(int argc, char** argv) {
         else if (a == "--up") v3(up);
         else if (a == "--sun") v3(sun);
         else if (a == "--reps") reps = std::atoi(argv[++i]);
+        else if (a == "--proc") proc = std::atoi(argv[++i]);
         else if (a == "--out") out = argv[++i];
         else obj = a;
     }
     float *tri = nullptr, *norm = nullptr;
     size_t n_tri = 0;
-    if (ceres_obj_load(obj.c_str(), &tri, &norm, &n_tri) != CERES_OK || n_tri == 0) {
-        std::fprintf(stderr, "cannot load %s: %s\n", obj.c_str(), ceres_last_error());
+    const int lrc = proc ? ceres_proc_mesh(proc, &tri, &norm, &n_tri) : ceres_obj_load(obj.c_str(), &tri, &norm, &n_tri);
+    if (lrc != CERES_OK || n_tri == 0) {
+        std::fprintf(stderr, "cannot load %s: %s\n", proc ? "the procedural mesh" : obj.c_str(), ceres_last_error());
         return 1;
     }
     std::vector<ceres::HostTriangle> triangles(n_tri);
@@ -111,12 +117,27 @@ int main(int argc, char** argv) {
             }
         std::fclose(f);
     }
+    std::vector<double> hash;
+    for (int r = 0; r < 5; ++r) {
+        auto a = clk::now();
+        uint64_t h = ceres_content_hash(bvh.nodes.get(), n_nodes * 32) ^ ceres_content_hash(bvh.primitive_indices.get(), n_tri * 8);
+        h ^= ceres_content_hash(triangles.data(), n_tri * 48) ^ ceres_content_hash(tri_norms.data(), n_tri * 36);
+        hash.push_back(std::chrono::duration<double, std::milli>(clk::now() - a).count());
+        volatile uint64_t sink = h;
+        (void)sink;
+    }
     auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
     auto mn = [](const std::vector<double>& v) { return v.empty() ? 0.0 : *std::min_element(v.begin(), v.end()); };
     std::printf("{\"W\": %zu, \"H\": %zu, \"rays\": %d, \"hits\": %d, \"reps\": %d, \"first_call_ms\": %.3f, "
                 "\"e2e_ms_median\": %.4f, \"e2e_ms_min\": %.4f, \"device_ms_median\": %.4f, \"float_bytes\": %zu, "
-                "\"e2e_mrays_per_s\": %.2f}\n",
-                W, H, rays, hits, reps, first_ms, med(e2e), mn(e2e), med(dev), 3 * W * H * sizeof(float),
+                "\"hash_ms_median\": %.3f, \"hashed_bytes\": %zu, \"trust_unchanged\": %d, \"e2e_mrays_per_s\": %.2f}\n",
+                W, H, rays, hits, reps, first_ms, med(e2e), mn(e2e), med(dev), 3 * W * H * sizeof(float), med(hash),
+                n_nodes * 32 + n_tri * (8 + 48 + 36),
+#ifdef CERES_DROPIN_TRUST_UNCHANGED
+                1,
+#else
+                0,
+#endif
                 med(e2e) > 0 ? rays / (med(e2e) * 1e3) : 0.0);
     return 0;
 }
