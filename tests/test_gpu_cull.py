@@ -67,15 +67,17 @@ def test_cull_changes_nothing_single_frames(gpu, name, arith):
     ref.close()
 
 
-def test_cull_changes_nothing_in_a_batch(gpu):
+@pytest.mark.parametrize("W,H", [(333, 217), (480, 272), (484, 270)])
+def test_cull_changes_nothing_in_a_batch(gpu, W, H):
     """16 random views in one ceres_render_batch_device launch (the batch kernel: 4 tiles per wave,
-    tiles of different frames in one wavefront) against the stats scene's single frames."""
+    tiles of different frames in one wavefront, XCD row runs) against the stats scene's single
+    frames.  Sizes: odd width (RGB8 byte stores), whole tiles with 4-byte rows (the dword RGB8 rows
+    of store_tile), and 4-byte rows with ragged right and bottom tiles (both paths in one frame)."""
     import torch
     pkg = gpu
     cfg = configs.CONFIGS["dragon_1080"]
     mesh, bvh, _ = pkg.prepare(cfg, arith=1)
     prod, ref = pkg.Scene(mesh, bvh), pkg.Scene(mesh, bvh, stats=True)
-    W, H = 333, 217
     cams = [(b, s) for b, s, _, _ in _cameras(pkg, mesh, 16, 99, 1, size=(W, H))]
     b12 = np.stack([c[0] for c in cams]).astype(np.float32)
     s3 = np.stack([c[1] for c in cams]).astype(np.float32)

@@ -11,6 +11,7 @@ in the chosen arithmetic (fma = the reference CMake build's, exact = -ffp-contra
 float + RGB8 framebuffers bench.py writes.  Prints the mean launch duration from HIP events.
 
 usage: python tools/batch_launch.py [config] [fma|exact] [frames] [n] [config|orbit]
+BL_BUFFERS=float|rgb8 writes only that framebuffer (the write-amplification split), default both.
 """
 import os
 import sys
@@ -44,16 +45,19 @@ def main():
         b12, s3 = np.repeat(b12[:1], len(b12), 0), np.repeat(s3[:1], len(s3), 0)
     rgb = torch.empty(frames * 3 * W * H, dtype=torch.uint8, device="cuda")
     px = torch.empty(frames * 3 * W * H, dtype=torch.float32, device="cuda")
+    bufs = os.environ.get("BL_BUFFERS", "both")
+    d_px = px.data_ptr() if bufs in ("both", "float") else 0
+    d_rgb = rgb.data_ptr() if bufs in ("both", "rgb8") else 0
     st = torch.cuda.current_stream()
     whole = pkg.Tiling(H, 0, 1)
 
     def launch():
         if frames == 1:
-            scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=whole, d_pixels=px.data_ptr(),
-                                d_rgb8=rgb.data_ptr(), stream=st.cuda_stream)
+            scene.render_device(b12[0], s3[0], W, H, mode=mode, tiling=whole, d_pixels=d_px,
+                                d_rgb8=d_rgb, stream=st.cuda_stream)
         else:
-            scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=whole, d_pixels=px.data_ptr(),
-                                      d_rgb8=rgb.data_ptr(), stream=st.cuda_stream)
+            scene.render_batch_device(b12, s3, W, H, mode=mode, tiling=whole, d_pixels=d_px,
+                                      d_rgb8=d_rgb, stream=st.cuda_stream)
     for _ in range(3):
         launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -63,7 +67,7 @@ def main():
     e1.record(st)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / n
-    print(f"{name} {arith_s} frames={frames} views={views} launches={n} mean_launch_ms={ms:.5f}", flush=True)
+    print(f"{name} {arith_s} frames={frames} views={views} buffers={bufs} launches={n} mean_launch_ms={ms:.5f}", flush=True)
     scene.close()
     return 0
 
