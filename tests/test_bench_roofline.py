@@ -2,8 +2,9 @@
 hard-coded, and no field named as the bound exceeds its peak.
 
 Checked two ways: synthetic counter summaries through `bench.roofline_block`, and every committed
-bench line (`profiles/r03_end/sweep/bench_*.log`, `profiles/r04/**/bench_*.log`) recomputed from its
-own algorithmic bytes, mean launch time and `profiles/pmc_summary.json` entry; round-4 lines also
+bench line (`profiles/r03_end/sweep/bench_*.log`, `profiles/r0[45]/**/bench_*.log`) recomputed from its
+own algorithmic bytes, mean launch time and `profiles/pmc_summary.json` entry (round 5: the
+session's own `pmc_summary_*.json` beside the log when it has the entry); round-4 lines also
 carry `roofline_step` (the timed regime), whose bytes are recomputed from the per-view reference
 statistics of tests/golden/orbit/<cfg>.json."""
 import glob
@@ -69,6 +70,18 @@ def _pmc_key(line, rf, which):
     return f"{rf['kernel']}_solo_{line['arith']}"
 
 
+def _session_pmc(name, cfg, key):
+    """The counters a round-5 session priced its bench line with: that session's own summary
+    (`pmc_summary_*.json` beside the bench log, merged into profiles/pmc_summary.json on the box
+    before the bench ran), which a later session's merge may have replaced globally."""
+    for p in glob.glob(os.path.join(REPO, "profiles", os.path.dirname(name), "pmc_summary_*.json")):
+        with open(p) as f:
+            e = json.load(f).get(cfg, {}).get(key)
+        if e is not None:
+            return e
+    return None
+
+
 @pytest.mark.parametrize("name,line", _bench_lines())
 def test_committed_sweep_roofline_recomputes(bench, name, line):
     cfg = line["config"]["workload"].split(":")[0]
@@ -76,7 +89,8 @@ def test_committed_sweep_roofline_recomputes(bench, name, line):
         rf = line.get(which)
         if rf is None:
             continue
-        pmc = bench.pmc_entry(cfg, _pmc_key(line, rf, which))   # None: the line must say "unmeasured"
+        key = _pmc_key(line, rf, which)
+        pmc = _session_pmc(name, cfg, key) or bench.pmc_entry(cfg, key)   # None: the line must say "unmeasured"
         if which == "roofline_solo" and line.get("arith") == "exact" and rf["traffic"] is not None and \
                 (pmc or {}).get("hbm_bytes_per_launch") != rf["traffic"]:
             pmc = bench.pmc_entry(cfg, rf["kernel"])          # bench.py's fallback for the exact solo launch

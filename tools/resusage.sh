@@ -13,7 +13,7 @@ for blk in t.split("Function Name: ")[1:]:
     name = blk.split()[0]
     if "fused" not in name: continue
     g = lambda k: (re.search(k + r": (\d+)", blk) or [0, 0])[1]
-    print(name[22:60], "V", g("VGPRs"), "S", g("TotalSGPRs"), "scr", g(r"ScratchSize \[bytes/lane\]"),
+    print(name[22:90], "V", g("VGPRs"), "S", g("TotalSGPRs"), "scr", g(r"ScratchSize \[bytes/lane\]"),
           "sspill", g("SGPRs Spill"), "vspill", g("VGPRs Spill"), "occ", g(r"Occupancy \[waves/SIMD\]"))
 PY
 rm -f "$out"
