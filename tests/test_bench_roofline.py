@@ -152,7 +152,9 @@ def test_committed_roofline_step_recomputes(bench, name, line):
     again = bench.roofline_step_block(nbytes, line["ms_per_step"], line["n_gpus"])
     for k in ("achieved_job", "achieved_per_gpu", "frac_l2", "frac_hbm"):
         assert abs(again[k] - rs[k]) <= 1e-3 * abs(rs[k]) + 1e-3, k
-    assert again["frac_l2"] <= 1.0
+    # per-ray bytes may exceed the L2 rate (packets: one scalar-cache read per wavefront for ~60
+    # rays; L1 hits); bench.py says so in the block
+    assert again["frac_l2"] <= 1.0 or rs.get("above_l2_note"), (name, again["frac_l2"])
 
 
 def test_headline_trace_pairing_is_kept():
