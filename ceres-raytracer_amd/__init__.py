@@ -44,6 +44,7 @@ def cfg_mode(cfg, arith=ARITH_EXACT):
     return ((MODE_PRIMARY if cfg["mode"] == "primary" else MODE_FULL) | (MODE_ROBUST if cfg.get("robust") else 0)
             | (MODE_FMA if arith else 0))
 SCENE_STATS = 1
+SCENE_FIRST_ORDER = 2
 
 EXPORTED_SYMBOLS = (
     "ceres_obj_load", "ceres_proc_mesh", "ceres_rotate_triangles", "ceres_bvh_build", "ceres_bvh_build_gpu",
@@ -53,7 +54,7 @@ EXPORTED_SYMBOLS = (
     "ceres_render_f64", "ceres_render_records_f64", "ceres_obj_load_f64_arith", "ceres_proc_mesh_f64_arith",
     "ceres_rotate_triangles_f64_arith", "ceres_bvh_build_f64_arith", "ceres_camera_basis_f64_arith",
     "ceres_orbit_cameras_f64_arith",
-    "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_render_f32",
+    "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_scene_shadow_stacks", "ceres_render_f32",
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_multi_f32", "ceres_device_count", "ceres_assemble_rgb8_packed", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
@@ -162,6 +163,7 @@ def lib():
     L.ceres_scene_destroy.argtypes = [_vp]
     L.ceres_scene_destroy.restype = None
     L.ceres_scene_info.argtypes = [_vp, _u32p, _u32p, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]
+    L.ceres_scene_shadow_stacks.argtypes = [_vp, _u32p, _u32p]
     L.ceres_render_f32.argtypes = [_vp, _fp, _fp, ctypes.c_int, _fp, ctypes.POINTER(ctypes.c_uint8), _sz, _sz,
                                    ctypes.POINTER(_Stats)]
     L.ceres_render_device.argtypes = [_vp, _fp, _fp, ctypes.c_int, _sz, _sz, ctypes.POINTER(Tiling), _vp, _vp, _vp, _vp]
@@ -367,21 +369,22 @@ def build_bvh_device(d_tri48, n_tri, d_nodes32, d_prim32, stream=0, arith=ARITH_
 class Scene:
     """A scene resident in HBM of one device (ceres_scene_create)."""
 
-    def __init__(self, mesh, bvh, device=0, stats=False, _handle=None):
+    def __init__(self, mesh, bvh, device=0, stats=False, first_order=False, _handle=None):
         L = lib()
         if _handle is not None:                      # Scene.from_device
             self._h, self.device, self.n_tri = _handle
             self.f64 = False
             return
         self.f64 = mesh.f64
+        flags = (SCENE_STATS if stats else 0) | (SCENE_FIRST_ORDER if first_order else 0)
         if self.f64:
             self._h = L.ceres_scene_create_f64(_p(mesh.tri, ctypes.c_double), len(mesh), _p(mesh.norm, ctypes.c_double),
                                                bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0],
-                                               _p(bvh.prim, ctypes.c_uint64), int(device), SCENE_STATS if stats else 0)
+                                               _p(bvh.prim, ctypes.c_uint64), int(device), flags)
         else:
             self._h = L.ceres_scene_create(_p(mesh.tri, ctypes.c_float), len(mesh), _p(mesh.norm, ctypes.c_float),
                                            bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0],
-                                           _p(bvh.prim, ctypes.c_uint64), int(device), SCENE_STATS if stats else 0)
+                                           _p(bvh.prim, ctypes.c_uint64), int(device), flags)
         if not self._h:
             raise CeresError("ceres_scene_create: " + L.ceres_last_error().decode())
         self.device = device
@@ -400,7 +403,10 @@ class Scene:
     def info(self):
         d, s, n, b = ctypes.c_uint32(), ctypes.c_uint32(), _sz(), _sz()
         _check(lib().ceres_scene_info(self._h, ctypes.byref(d), ctypes.byref(s), ctypes.byref(n), ctypes.byref(b)))
-        return dict(depth=d.value, stack_entries=s.value, n_pairs=n.value, device_bytes=b.value)
+        near, first = ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().ceres_scene_shadow_stacks(self._h, ctypes.byref(near), ctypes.byref(first)))
+        return dict(depth=d.value, stack_entries=s.value, n_pairs=n.value, device_bytes=b.value,
+                    shadow_stack_nearest=near.value, shadow_stack_first=first.value)
 
     def close(self):
         if getattr(self, "_h", None):

@@ -160,6 +160,7 @@ struct KParams {
     uint32_t root_box_ok;                        // ... and whether both root children lie inside it
     uint32_t cull;                               // production kernels: background tiles culled (tile_misses_root)
     uint32_t shadow_stack_entries;               // BVH4 traversal stack (shadow rays)
+    uint32_t steal_first;                        // work-stealing shadow loop: first passing child, not nearest
     uint32_t packets;                            // batch kernel: wave-wide packets (L2-resident scenes, render_hip.hip)
     uint32_t tiles_x;                            // tile columns per row (fused kernel)
     uint32_t lds_entries;                        // fused kernel: LDS stack slots per lane (24-bit planes)
@@ -204,6 +205,7 @@ int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, siz
                  uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first);
 int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>& out, uint32_t& stack_bound,
                       uint32_t& not_collapsed);
+int order_shadow_bvh4(std::vector<Node4>& nodes, uint32_t& first_bound);
 int relayout_bvh64(const RefNode64* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri96* tris,
                    std::vector<SiblingPair64>& pairs, std::vector<Tri96>& leaf_tris, std::vector<uint32_t>& orig,
                    uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first);

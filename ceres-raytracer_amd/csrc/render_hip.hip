@@ -1031,12 +1031,16 @@ __device__ __forceinline__ void steal_traverse(const KParams& P, bool has_job, R
                 L.blocked[owner] = 1u;
                 active = false;
             } else if (inner_mask) {
-                // nearest first here: with work stealing it pays (first-child order: bunny solo +20 %)
+                // nearest first here: with work stealing it pays (first-child order: bunny solo +20 %);
+                // the first passing child when the scene's LDS budget asks for the smaller stack
+                // bound of that order (P.steal_first, order_shadow_bvh4)
                 uint32_t best = __builtin_ctz(inner_mask);
-                float be = best == 0 ? e[0] : best == 1 ? e[1] : best == 2 ? e[2] : e[3];
+                if (!P.steal_first) {
+                    float be = best == 0 ? e[0] : best == 1 ? e[1] : best == 2 ? e[2] : e[3];
 #pragma unroll
-                for (int c = 1; c < 4; ++c)
-                    if ((inner_mask >> c & 1u) && e[c] < be) { be = e[c]; best = c; }
+                    for (int c = 1; c < 4; ++c)
+                        if ((inner_mask >> c & 1u) && e[c] < be) { be = e[c]; best = c; }
+                }
                 uint32_t rest = inner_mask & ~(1u << best);
                 if (cnt + __builtin_popcount(rest) > cap) { overflow = true; rest = 0; }
                 while (rest) {
@@ -1160,6 +1164,7 @@ __device__ __forceinline__ void shade_pixel(const KParams& P, uint32_t f, uint32
 // whose pixel missed help the others), then shades.  No shadow-ray queue in HBM, no second
 // launch: the shadow work of early tiles overlaps the primary work of later ones.
 constexpr int kFusedB = 64;      // single-wavefront workgroups (LDS is released per workgroup)
+constexpr size_t kLdsPerCu = 160 * 1024;   // LDS per CU (MI355X_MICROARCH.md)
 template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ, bool kG>
 __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     constexpr int kB = kFusedB;
@@ -1759,6 +1764,18 @@ static CullRect cull_rect(const FrameCam& c, const float root[6], uint32_t W, ui
 // One launch of a batch: `frames` (<= kFramesPerLaunch) cameras (basis12 = frames x {eye, dir, iu,
 // iv}) and suns (frames x 3).  first / last: the first and last launch of a batch call (the counter
 // shards are cleaned before the first and summed after the last, over `batch_frames` frames).
+// LDS stack entry width of a scene's fused kernels: the narrowest every pair / BVH4 index fits
+static int stack_width(size_t n_pairs, size_t n_nodes4) {
+    const size_t nmax = std::max(n_pairs, n_nodes4);
+    return CERES_STACK16 && nmax < (1u << 16) ? 2 : CERES_STACK24 && nmax < (1u << 24) ? 3 : 4;
+}
+// LDS of one fused-kernel wavefront for `entries` stack slots, and whether that costs waves: above
+// kLdsPerCu / 28 a CU holds fewer than 7 waves per SIMD (the kernels' VGPR budget)
+static size_t fused_lds_bytes(uint32_t entries, int stw) {
+    return size_t(entries) * dev::kFusedB * stw + sizeof(dev::StealLdsT<dev::kFusedB>);
+}
+static bool lds_limits_waves(uint32_t entries, int stw) { return fused_lds_bytes(entries, stw) > dev::kLdsPerCu / 28; }
+
 int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const float* sun, int mode, size_t W, size_t H,
                  const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream,
                  int32_t* d_rec_prim, float* d_rec_tuv, int8_t* d_rec_shadow, bool first, bool last,
@@ -1845,17 +1862,27 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
         if (e0) HIP_TRY(hipEventRecord(e0, stream));
         if (full) {
             // one kernel: primary + shadow + shading per 8x8 tile
-            const size_t nmax = std::max(s->n_pairs, s->n_nodes4);
-            const int stw = CERES_STACK16 && nmax < (1u << 16) ? 2 : CERES_STACK24 && nmax < (1u << 24) ? 3 : 4;
+            const int stw = stack_width(s->n_pairs, s->n_nodes4);
             const bool st16 = stw == 2;
-            P.lds_entries = uint32_t(std::max(s->stack_entries + 1, s->shadow_stack_entries));
+            // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
+            const bool steal = frames == 1;
+            // BVH4 stack: the batch kernels' walks descend into the first passing child and need
+            // only shadow_stack_first entries (order_shadow_bvh4); the stealing loop descends into
+            // the nearest child (bunny solo -20 % against first-child order) and needs the
+            // nearest-first bound -- unless that bound's LDS costs waves (C5: 37 entries x 3 B x
+            // 64 lanes + the stealing mailboxes = 7.9 KB, 5 waves per SIMD; the first-child bound,
+            // 27, fits the primary stack's 28: 6.1 KB), and there the loop takes the first
+            // passing child too (scene creation ordered those scenes' records for it)
+            P.steal_first = steal && !stats && ((s->flags & CERES_SCENE_FIRST_ORDER) ||
+                                                lds_limits_waves(std::max(s->stack_entries + 1, s->shadow_stack_entries), stw))
+                                ? 1u : 0u;
+            P.shadow_stack_entries = (!steal || P.steal_first) ? s->shadow_stack_first : s->shadow_stack_entries;
+            P.lds_entries = uint32_t(std::max(s->stack_entries + 1, P.shadow_stack_entries));
             const size_t flds = size_t(P.lds_entries) * dev::kFusedB * stw;
             P.tile_order = tile_order;
             P.tile_packed = packed ? 1u : 0u;
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
-            // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
-            const bool steal = frames == 1;
             const uint32_t tpw = (!stats && !steal) ? CERES_TILES_PER_WAVE : 1;   // = kTPW
             const uint32_t n_tiles = fbx * fby * frames;
             const dim3 fgrid((n_tiles + tpw - 1) / tpw), fblock(dev::kFusedB);
@@ -2007,11 +2034,21 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     std::vector<Node4> nodes4;
     uint32_t stack4 = 0, not_collapsed = 0;
     if (!rlc && build_shadow_bvh4(pairs, nodes4, stack4, not_collapsed)) return nullptr;
+    // scenes whose nearest-first BVH4 stack costs waves (lds_limits_waves) get their inner
+    // children ordered for the first-passing-child bound (order_shadow_bvh4; their single-frame
+    // launches then walk in that order); the others keep the build order, which the nearest-first
+    // stealing loop prefers (reordered: C3 solo +4 %, bunny +2 %, profiles/r05/s19)
+    uint32_t stack4_first = stack4;
+    if (!rlc && ((flags & CERES_SCENE_FIRST_ORDER) ||
+                 lds_limits_waves(std::max(depth + 1, stack4), stack_width(pairs.size(), nodes4.size()))) &&
+        order_shadow_bvh4(nodes4, stack4_first))
+        return nullptr;
     if (nodes4.empty()) nodes4.emplace_back();
     auto* s = new (std::nothrow) ceres_scene;
     if (!s) { set_error(CERES_ENOMEM, "out of host memory"); return nullptr; }
     s->n_nodes4 = nodes4.size();
     s->shadow_stack_entries = std::max<uint32_t>(1, stack4);
+    s->shadow_stack_first = std::max<uint32_t>(1, std::min(stack4, stack4_first));
     s->device = device; s->flags = flags; s->n_tri = n_tri; s->n_pairs = pairs.size();
     s->depth = depth; s->root_leaf_count = rlc; s->root_leaf_first = rlf;
     s->stack_entries = std::max<uint32_t>(1, depth);                 // stack <= depth - 1 entries
@@ -2088,6 +2125,7 @@ ceres_scene* ceres_scene_create_device(const float* d_tri48, size_t n_tri, const
         s->depth = L.depth; s->root_leaf_count = L.root_leaf_count; s->root_leaf_first = L.root_leaf_first;
         s->stack_entries = std::max<uint32_t>(1, L.depth);           // stack <= depth - 1 entries
         s->shadow_stack_entries = std::max<uint32_t>(1, L.stack4);
+        s->shadow_stack_first = s->shadow_stack_entries;              // device records keep build order
         if (!L.root_leaf_count) {
             SiblingPair p0;
             HIP_TRY(hipMemcpyAsync(&p0, L.pairs, sizeof p0, hipMemcpyDeviceToHost, st));
@@ -2119,6 +2157,13 @@ int ceres_scene_info(const ceres_scene* s, uint32_t* depth, uint32_t* stack_entr
     if (n_pairs) *n_pairs = s->n_pairs;
     if (device_bytes)
         *device_bytes = s->n_pairs * sizeof(SiblingPair) + s->n_nodes4 * sizeof(Node4) + s->n_tri * (sizeof(Tri48) + 4 + 36);
+    return CERES_OK;
+}
+
+int ceres_scene_shadow_stacks(const ceres_scene* s, uint32_t* nearest_first, uint32_t* first_passing) {
+    if (!s) return set_error(CERES_EINVAL, "null scene");
+    if (nearest_first) *nearest_first = s->shadow_stack_entries;
+    if (first_passing) *first_passing = s->shadow_stack_first;
     return CERES_OK;
 }
 

@@ -19,7 +19,8 @@ struct ceres_scene {
     uint32_t depth = 0, stack_entries = 1, root_leaf_count = 0, root_leaf_first = 0;
     float root_box[6] = {0, 0, 0, 0, 0, 0};   // root node bounds; root_box_ok: both children inside it
     uint32_t root_box_ok = 0;
-    uint32_t shadow_stack_entries = 1;
+    uint32_t shadow_stack_entries = 1;     // BVH4 stack bound of the nearest-first walk (any child order)
+    uint32_t shadow_stack_first = 1;       // ... of first-passing-child walks (order_shadow_bvh4; <= the above)
     size_t n_nodes4 = 0;
     SiblingPair* d_pairs = nullptr;
     Node4* d_nodes4 = nullptr;

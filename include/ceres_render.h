@@ -201,6 +201,9 @@ int ceres_orbit_cameras_f64_arith(const double eye[3], const double dir[3], cons
 /* ---- device scene ---- */
 
 #define CERES_SCENE_STATS 1u   /* flag: build the kernels' traversal-statistics variant */
+#define CERES_SCENE_FIRST_ORDER 2u  /* flag: order the shadow BVH4's inner children for walks that take the
+                                     * first passing child, and walk single frames in that order (automatic
+                                     * for scenes whose nearest-first stack would cost waves, e.g. C5) */
 
 /* Upload a scene to HIP device `device` (re-laid for the GPU: sibling-pair 64-B node records,
  * triangles permuted into leaf order).  The caller keeps ownership of its host arrays; they
@@ -231,6 +234,9 @@ void ceres_scene_destroy(ceres_scene* scene);
 /* depth of the BVH (levels below the root) and the traversal-stack entries the kernels use */
 int ceres_scene_info(const ceres_scene* scene, uint32_t* depth, uint32_t* stack_entries,
                      size_t* n_pairs, size_t* device_bytes);
+/* shadow-BVH4 traversal-stack bounds: nearest-first walks (any child order) and walks that take
+ * the first passing child (after the host's inner-child ordering; device-built scenes: equal) */
+int ceres_scene_shadow_stacks(const ceres_scene* scene, uint32_t* nearest_first, uint32_t* first_passing);
 
 /* ---- the hot path ---- */
 
