@@ -27,8 +27,8 @@
 // anim.cpp:82-125 upload once and a caller that edits any of them in place gets the edited scene.
 // Define CERES_DROPIN_TRUST_UNCHANGED to skip the hash (the caller promises never to edit the
 // arrays behind the same pointers).  The hash reads every byte: for the 10M-triangle C5 scene
-// (1.26 GB of arrays) it is the larger part of a call -- 11.0 ms per 3840x2160 render<float>()
-// against 5.4 ms with the define, kernel 2.4 ms (tools/probes/dropin_bench).
+// (1.26 GB of arrays) it is the larger part of a call -- 9.7 ms per 3840x2160 render<float>()
+// against 5.2 ms with the define, kernel 2.1 ms (tools/probes/dropin_bench).
 //
 // Arithmetic: the reference's CMake build (g++ -O3 -mavx2 -mfma) contracts a*b+c into FMA, so a
 // caller compiling its scene code (obj_norms / lib/bvh / rotate_triangles) that way holds the
