@@ -50,7 +50,8 @@
 #endif                                        // wavefront (A/B, 16-frame batches x 8 streams: 4 beats 2 by 2 %; round 5
                                               // profiles/r05/s8-s9: 8 vs 4 within +-1 %, no consistent sign)
 #ifndef CERES_FRAME_MAJOR_PIXELS
-#define CERES_FRAME_MAJOR_PIXELS (1u << 22)    // batches of frames of >= this many pixels: frame after frame (0: never)
+#define CERES_FRAME_MAJOR_PIXELS (1u << 20)    // batches of frames of >= this many pixels: frame after frame, XCD-local
+                                               // Morton order (0: never; round 5: 1 Mpixel, was 4)
 #endif
 #ifndef CERES_SPLIT_UNIFORM
 #define CERES_SPLIT_UNIFORM 1                  // wave-uniform triangle / BVH4 fetches get their own copy of the test
@@ -1560,7 +1561,11 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     // Large views go one frame after another (each centre-first): the waves in flight then share
     // one view's BVH nodes and triangles in L2 instead of F views' (8 x 16-frame batches: dragon
     // 4096^2 -18 %, C5 -4 %; also for a rank's interleaved rows of such a view).  Smaller views
-    // stay interleaved so every frame's expensive centre starts early (C3: frame-major +0..6 %).
+    // stay interleaved so every frame's expensive centre starts early (round 3, C3: frame-major
+    // +0..6 %).  Round 5 moved the threshold from 4 to 1 Mpixel: with the current kernel the
+    // frame-major batches' XCD-local Morton order below wins for 1080p views (16-frame batches x 8
+    // streams: C3 orbit -8.3 %, C3 copies -5.8 %, bunny 1080p copies -3.5 %; 256 Kpixel: bunny 640
+    // +5 %, so 1 Mpixel; profiles/r05/s27-s28).
     const uint64_t fm_pixels = CERES_FRAME_MAJOR_PIXELS;
     const bool frame_major = fm_pixels != 0 && uint64_t(W) * H >= fm_pixels;
     for (uint32_t f = 0; f < frames; ++f)

@@ -321,7 +321,7 @@ def test_batch_of_64_frames_matches_single_frames(gpu):
 
 
 def test_large_frame_batch_matches_single_frames(gpu):
-    """Frames of >= 4 Mpixel are dealt frame after frame in a batch (CERES_FRAME_MAJOR_PIXELS)
+    """Frames of >= 1 Mpixel are dealt frame after frame in a batch (CERES_FRAME_MAJOR_PIXELS)
     instead of interleaved: every frame's PPM body == a one-frame render, whole frames and one
     rank of a 3-way row split."""
     import torch
