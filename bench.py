@@ -22,10 +22,11 @@ At N > 1 (--collect, default auto):
             ceres_render_batch_device launch, into its own HBM -- no collective (frames are
             independent: render.hpp:104-153);
   gather    rows interleaved, all F frames to rank 0.
-  auto = exchange, except for the tiled 4096^2 / 4K configs (C4, C5) at N = 2, where the single
-  xGMI link would carry 16 split frames' rows per step and outlast the render (DESIGN.md
-  "Multi-GPU"): frames there, reported as untiled.  The other partition of the same step is timed
-  too and reported as `partition_alt`; the line carries the world size and backend RCCL ran with.
+  auto = frames (the step's frames are independent units: no data-path collective), except for
+  the configs BASELINE.json defines as one framebuffer tiled across the GPUs (C4, C5) at N >= 4:
+  exchange (at N = 2 the single xGMI link would carry 16 split frames' rows per step and outlast
+  the render, DESIGN.md "Multi-GPU").  The other partition of the same step is timed too and
+  reported as `partition_alt`; the line carries the world size and backend RCCL ran with.
 RGB8 + float framebuffers in HBM.  Steps rotate over --streams HIP streams (own buffers each):
 the collective/assembly of step k and the tail of its render overlap later steps; the timed
 region ends when every step's frames are assembled.
@@ -284,16 +285,20 @@ def roofline_step_block(nbytes, ms_step, world):
 
 
 def choose_collect(requested, cfg, world, frames):
-    """The N > 1 partition of a step (DESIGN.md "Multi-GPU"): "auto" = "exchange" -- every frame's
-    rows dealt over the ranks and gathered with ONE RCCL all-to-all per step, the framebuffer
-    partition BASELINE.json's north star names -- at every N, except for a config defined as a
-    4096^2 / 4K framebuffer (configs.py "tiled": C4, C5) at N = 2, where the single xGMI link would
-    carry 16 split frames' rows per step and outlast the render (C4 1.23x); there each
-    rank renders its frames whole ("frames", no collective, reported as untiled).  Partitions that
-    deal whole frames need F to be a multiple of N, else every frame goes to rank 0 ("gather")."""
+    """The N > 1 partition of a step (DESIGN.md "Multi-GPU").  "auto": the step's frames are the
+    units -- each rank renders its 16 frames whole with no data-path collective ("frames"; render.hpp
+    :104-153 touches one frame, pixels are independent) -- except for the configs BASELINE.json
+    defines as ONE framebuffer tiled across the GPUs (configs.py "tiled": C4, C5) at N >= 4, whose
+    frames' rows are dealt over the ranks and gathered to their owners with one RCCL all-to-all per
+    step ("exchange", the north star's framebuffer partition).  At N = 2 those take "frames" too:
+    the single xGMI link would carry 16 split frames' rows per step and outlast the render (C4
+    1.23x).  The other partition is timed in the same run and reported beside it (alt_collect):
+    round 5's one-GPU rehearsal predicts C3 at N = 8 at 0.995 weak efficiency with frames and 0.71-0.86
+    with the exchange (tools/scaling_rehearsal.py, profiles/r05/s36).  Partitions that deal whole
+    frames need F to be a multiple of N, else every frame goes to rank 0 ("gather")."""
     collect = requested
     if collect == "auto":
-        collect = "frames" if cfg.get("tiled") and world == 2 else "exchange"
+        collect = "exchange" if cfg.get("tiled") and world >= 4 else "frames"
     if collect in ("frames", "exchange") and frames % world:
         collect = "gather"
     return collect

@@ -1567,7 +1567,8 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     // streams: C3 orbit -8.3 %, C3 copies -5.8 %, bunny 1080p copies -3.5 %; 256 Kpixel: bunny 640
     // +5 %, so 1 Mpixel; profiles/r05/s27-s28).
     const uint64_t fm_pixels = CERES_FRAME_MAJOR_PIXELS;
-    const bool frame_major = fm_pixels != 0 && uint64_t(W) * H >= fm_pixels;
+    // (the pixels of a frame this launch renders: a rank's rows of a row-split frame count alone)
+    const bool frame_major = fm_pixels != 0 && uint64_t(W) * rows >= fm_pixels;
     for (uint32_t f = 0; f < frames; ++f)
         for (uint32_t y = 0; y < by; ++y) {
             const size_t lr = std::min<size_t>(size_t(y) * tile + tile / 2, rows - 1);
@@ -1975,14 +1976,17 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     if (tiling) t = *tiling;
     if (t.world == 0 || t.rank >= t.world || t.row_block == 0) return set_error(CERES_EINVAL, "render: bad tiling");
     const size_t fp = W * local_rows_of(H, t.row_block, t.rank, t.world);   // pixels per frame on this rank
-    for (uint32_t f0 = 0; f0 < frames; f0 += kFramesPerLaunch) {
-        const uint32_t n = std::min<uint32_t>(kFramesPerLaunch, frames - f0);
+    // equal chunks (64 frames: 32 + 32, not 56 + 8 -- a small last launch is all tail)
+    const uint32_t n_launch = (frames + kFramesPerLaunch - 1) / kFramesPerLaunch;
+    for (uint32_t c = 0, f0 = 0; c < n_launch; ++c) {
+        const uint32_t n = frames / n_launch + (c < frames % n_launch ? 1u : 0u);
         const size_t o = size_t(f0) * fp;
         if (int rc = launch_chunk(s, n, basis12 + 12 * size_t(f0), sun + 3 * size_t(f0), mode, W, H, tiling,
                                   d_pixels ? d_pixels + 3 * o : nullptr, d_rgb8 ? d_rgb8 + 3 * o : nullptr, d_counters,
                                   stream, d_rec_prim ? d_rec_prim + o : nullptr, d_rec_tuv ? d_rec_tuv + 3 * o : nullptr,
                                   d_rec_shadow ? d_rec_shadow + o : nullptr, f0 == 0, f0 + n >= frames, frames))
             return rc;
+        f0 += n;
     }
     return CERES_OK;
 }

@@ -343,19 +343,20 @@ def test_frame_owner_gloo_step(world, k):
 
 
 def test_bench_partition_choice():
-    """bench.py --collect auto: the framebuffer partition (rows dealt over the ranks, one RCCL
-    all-to-all per step) at every N > 1, except the tiled 4096^2 / 4K configs (C4, C5) at N = 2,
-    where one xGMI link would carry 16 split frames' rows per step (DESIGN.md "Multi-GPU") and each
-    rank renders its frames whole; explicit choices are kept; a frame count that is not a multiple
-    of N falls back to the gather.  The other partition is reported beside it (`alt_collect`)."""
+    """bench.py --collect auto: whole frames per rank with no data-path collective for the
+    frame-unit configs (C3, bunny) at every N > 1; the tiled 4096^2 / 4K configs (C4, C5) deal their
+    frames' rows over the ranks and gather them with one RCCL all-to-all per step at N >= 4, and
+    render whole frames at N = 2 (one xGMI link, DESIGN.md "Multi-GPU"); explicit choices are kept;
+    a frame count that is not a multiple of N falls back to the gather.  The other partition is
+    reported beside it (`alt_collect`)."""
     import sys
     sys.path.insert(0, REPO)
     import bench
     import configs
     C = configs.CONFIGS
     for n in (2, 4, 8):
-        assert bench.choose_collect("auto", C["dragon_1080"], n, 16 * n) == "exchange"
-        assert bench.choose_collect("auto", C["bunny_1080"], n, 16 * n) == "exchange"
+        assert bench.choose_collect("auto", C["dragon_1080"], n, 16 * n) == "frames"
+        assert bench.choose_collect("auto", C["bunny_1080"], n, 16 * n) == "frames"
     for name in ("dragon_4096", "proc_c5"):
         assert bench.choose_collect("auto", C[name], 2, 32) == "frames"
         assert bench.choose_collect("auto", C[name], 4, 64) == "exchange"
@@ -442,10 +443,10 @@ def json_dumps(x):
 
 
 def test_bench_line_world2_gloo():
-    """bench.py's N > 1 path on two gloo ranks: the headline partition for C3 is the framebuffer
-    exchange (rows over the ranks + one all-to-all), the collective-free `frames` partition is run
-    as `partition_alt`, every frame of both is produced exactly once, and the line names the world
-    size and backend the collectives ran with."""
+    """bench.py's N > 1 path on two gloo ranks: the headline partition for C3 is the collective-free
+    `frames` partition (each rank's frames whole), the framebuffer exchange (rows over the ranks +
+    one all-to-all) is run as `partition_alt`, every frame of both is produced exactly once, and the
+    line names the world size and backend the collectives ran with."""
     import json
     import_package()
     ctx = mp.get_context("spawn")
@@ -461,7 +462,7 @@ def test_bench_line_world2_gloo():
     line = json.loads(line)
     assert ok
     assert line["n_gpus"] == line["world_size"] == 2 and line["backend"] == "gloo"
-    assert line["config"]["collect"] == "exchange" and line["collective"]["kind"] == "all_to_all"
+    assert line["config"]["collect"] == "frames"
     assert line["config"]["views"] == "config" and "copies of the config view" in line["config"]["workload"]
-    assert line["partition_alt"]["collect"] == "frames" and line["partition_alt"]["value"] > 0
+    assert line["partition_alt"]["collect"] == "exchange" and line["partition_alt"]["value"] > 0
     assert line["scaling"] == "weak" and line["value"] > 0
