@@ -49,6 +49,9 @@
 #define CERES_TILES_PER_WAVE 4                // fused kernel, batches: consecutive tile-order entries (1, 2, 4 or 8) per
 #endif                                        // wavefront (A/B, 16-frame batches x 8 streams: 4 beats 2 by 2 %; round 5
                                               // profiles/r05/s8-s9: 8 vs 4 within +-1 %, no consistent sign)
+#ifndef CERES_TPW_BY_SIZE
+#define CERES_TPW_BY_SIZE 1                    // batches of 16-bit-stack 1080p-class frames: 2 tiles per wave (batch_tiles_per_wave)
+#endif
 #ifndef CERES_FRAME_MAJOR_PIXELS
 #define CERES_FRAME_MAJOR_PIXELS (1u << 20)    // batches of frames of >= this many pixels: frame after frame, XCD-local
                                                // Morton order (0: never; round 5: 1 Mpixel, was 4)
@@ -1166,7 +1169,7 @@ __device__ __forceinline__ void shade_pixel(const KParams& P, uint32_t f, uint32
 // launch: the shadow work of early tiles overlaps the primary work of later ones.
 constexpr int kFusedB = 64;      // single-wavefront workgroups (LDS is released per workgroup)
 constexpr size_t kLdsPerCu = 160 * 1024;   // LDS per CU (MI355X_MICROARCH.md)
-template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ, bool kG>
+template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ, bool kG, int kTPWo = 0>
 __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     constexpr int kB = kFusedB;
     // kernels that trace shadow packets keep only the generic per-lane any-hit loop as fallback
@@ -1190,7 +1193,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     // wavefronts -- the background tiles' short waves are mostly launch and first-fetch latency);
     // one per wavefront for single frames (latency: their longest tiles set the frame time) and
     // in stats builds (the wave log is per tile)
-    constexpr uint32_t kTPW = (kStats || kSteal) ? 1 : CERES_TILES_PER_WAVE;
+    constexpr uint32_t kTPW = (kStats || kSteal) ? 1 : kTPWo ? uint32_t(kTPWo) : uint32_t(CERES_TILES_PER_WAVE);
     const uint32_t per_frame = P.tiles_x * P.row_blocks_per_frame;
     const uint32_t n_tiles = per_frame * P.frames;
     uint32_t n_shadow = 0, occluded = 0, n_pairs = 0, n_tests = 0;
@@ -1547,10 +1550,12 @@ static void xcd_group_rows(std::vector<uint32_t>& order, uint32_t bx, uint32_t p
 // orders; the least recently used one is retired (freed later, see ceres_scene::retired), so
 // eviction neither rewrites an order a launch in flight reads nor stalls the streams.
 int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t, size_t rows, uint32_t frames,
-                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out, bool packed) {
+                      uint32_t bx, uint32_t by, uint32_t tile, hipStream_t stream, const uint32_t** out, bool packed,
+                      uint32_t tpw) {
+    const uint32_t tile_key = tile | tpw << 16;                    // the order depends on the tiles per wave
     for (auto& o : s->orders)
         if (o.W == W && o.H == H && o.row_block == t.row_block && o.rank == t.rank && o.world == t.world &&
-            o.frames == frames && o.tile == tile && o.packed == packed) {
+            o.frames == frames && o.tile == tile_key && o.packed == packed) {
             o.used = ++s->order_clock;
             *out = o.d;
             return CERES_OK;
@@ -1618,7 +1623,6 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
             mk[id] = {(uint64_t(f) << 40) | morton(x, y), id};
         }
         std::sort(mk.begin(), mk.end());
-        const uint32_t tpw = frames == 1 ? 1u : uint32_t(CERES_TILES_PER_WAVE);
         const size_t c = std::max<size_t>(tpw, lchunk / tpw * tpw), cw = c / tpw, grp = 8 * c;
         const size_t full = n / grp * grp;
         for (size_t p = 0; p < n; ++p) {
@@ -1629,7 +1633,7 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
             }
             order[p] = mk[src].second;
         }
-        return upload_tile_order(s, W, H, t, frames, tile, order, stream, out, packed, bx, by);
+        return upload_tile_order(s, W, H, t, frames, tile_key, order, stream, out, packed, bx, by);
     }
     uint64_t st = 0x9e3779b97f4a7c15ull;
     for (size_t b0 = 0; b0 < n; b0 += dev::kTileShuffleWindow) {
@@ -1639,8 +1643,8 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
             std::swap(order[b0 + q], order[b0 + size_t((st >> 33) % (q + 1))]);
         }
     }
-    if (CERES_XCD_GROUP_TILES && frames > 1) xcd_group_rows(order, bx, per_frame, uint32_t(CERES_TILES_PER_WAVE));
-    return upload_tile_order(s, W, H, t, frames, tile, order, stream, out, packed, bx, by);
+    if (CERES_XCD_GROUP_TILES && frames > 1) xcd_group_rows(order, bx, per_frame, tpw);
+    return upload_tile_order(s, W, H, t, frames, tile_key, order, stream, out, packed, bx, by);
 }
 
 // CERES_MODE_QBVH4: the exact shadow BVH4 (Node4) -> compressed QNode4 records.  Per node and
@@ -1775,6 +1779,16 @@ static int stack_width(size_t n_pairs, size_t n_nodes4) {
     const size_t nmax = std::max(n_pairs, n_nodes4);
     return CERES_STACK16 && nmax < (1u << 16) ? 2 : CERES_STACK24 && nmax < (1u << 24) ? 3 : 4;
 }
+// Tiles per wavefront of the batch kernel: consecutive tile-order entries a wave takes.  16-bit-stack
+// scenes (dragon, bunny) with frames of 1-4 Mpixel (1080p) take 2, everything else
+// CERES_TILES_PER_WAVE (A/B, 16-frame batches x 8 streams: C3 -2.1 %, bunny +-1 %, a C3 batch
+// launch alone -11 %; 8 for 4096^2 measured +-0.6 %; profiles/r05/s38, s39).  The kernel
+// instantiation for 2 exists for these scenes only.
+static uint32_t batch_tiles_per_wave(size_t frame_pixels, int stw, bool qbvh) {
+    if (!CERES_TPW_BY_SIZE || stw != 2 || qbvh) return CERES_TILES_PER_WAVE;
+    return frame_pixels >= (size_t(1) << 20) && frame_pixels < (size_t(1) << 22) ? 2u : uint32_t(CERES_TILES_PER_WAVE);
+}
+
 // LDS of one fused-kernel wavefront for `entries` stack slots, and whether that costs waves: above
 // kLdsPerCu / 28 a CU holds fewer than 7 waves per SIMD (the kernels' VGPR budget)
 static size_t fused_lds_bytes(uint32_t entries, int stw) {
@@ -1856,8 +1870,12 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
     const uint32_t* tile_order = nullptr;
     const bool packed = frames <= (1u << (32 - kTileXBits - kTileYBits)) &&
                         fbx <= (1u << kTileXBits) && fby <= (1u << kTileYBits);
+    // tiles per wavefront of the fused kernel: 1 for the stealing single-frame and the stats
+    // kernels; batch_tiles_per_wave for batches (the kernel instantiation must match the order)
+    const uint32_t tpw = (!stats && frames > 1) ? batch_tiles_per_wave(size_t(W) * rows, stack_width(s->n_pairs, s->n_nodes4), qbvh)
+                                                : 1u;
     if (full && rows)
-        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order, packed)) return rc;
+        if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order, packed, tpw)) return rc;
     // The shards must start at zero when they are read back (counters) or count primary-only hits;
     // the fused kernel without counters only adds to them, so its steady-state frames skip the
     // memset (ceres_finalize re-zeroes them after every counted render).
@@ -1889,7 +1907,6 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
             P.tile_packed = packed ? 1u : 0u;
             P.tiles_x = fbx;
             P.row_blocks_per_frame = fby;
-            const uint32_t tpw = (!stats && !steal) ? CERES_TILES_PER_WAVE : 1;   // = kTPW
             const uint32_t n_tiles = fbx * fby * frames;
             const dim3 fgrid((n_tiles + tpw - 1) / tpw), fblock(dev::kFusedB);
             if (stats) {                                             // per-wave diagnostic timeline
@@ -1920,7 +1937,12 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
                 if (stats && st16) hipLaunchKernelGGL((dev::ceres_fused<true, uint16_t*, 1, R, T, false, G>), fgrid, fblock, flds, stream, P);
                 else if (stats && stw == 3) hipLaunchKernelGGL((dev::ceres_fused<true, dev::Stk24, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
                 else if (stats) hipLaunchKernelGGL((dev::ceres_fused<true, uint32_t*, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
-                else if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, R, T, false, G>), fgrid, fblock, flds, stream, P);
+                else if (st16) {
+                    if constexpr (!T) {                              // batches: tiles per wave by frame size
+                        if (tpw == 2) { hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, R, T, false, G, 2>), fgrid, fblock, flds, stream, P); return; }
+                    }
+                    hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, R, T, false, G>), fgrid, fblock, flds, stream, P);
+                }
                 else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
                 else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
             };
@@ -2003,7 +2025,7 @@ namespace ceres {
 int frame_tile_order(ceres_scene* s, size_t W, size_t H, uint32_t tile, hipStream_t stream, const uint32_t** out) {
     const ceres_tiling t{uint32_t(H), 0, 1};
     return ensure_tile_order(s, W, H, t, H, 1, uint32_t((W + tile - 1) / tile), uint32_t((H + tile - 1) / tile), tile,
-                             stream, out, false);
+                             stream, out, false, 1u);
 }
 }  // namespace ceres
 
