@@ -78,6 +78,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(REPO, "ceres-raytracer_amd")
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md §L2: aggregate over the 8 XCD L2s, ~34.5 TB/s
+N_CU = 256                     # MI355X_MICROARCH.md chip table
+CLOCK_GHZ = 2.4                # max clock (chip table); the issue ceilings below use it, so they are upper bounds
+VALU_PER_CU_CYCLE = 2.0        # 4 SIMD-32 per CU, a wave64 VALU instruction every 2 cycles per SIMD (MI355X_MICROARCH.md:54)
+SALU_PER_CU_CYCLE = 1.0        # one scalar unit per CU shared by its 4 SIMDs
+L2_REQ_BYTES = 128             # one TCC request = at most one 128-B L2 line (an upper bound on its bytes)
 
 
 def import_package():
@@ -150,7 +155,17 @@ def cpu_baseline(cfg_name, cfg, rays_per_frame, budget_s=3.0, build="ref"):
     """Reference CPU path on this host, bounded sample of the same workload (rank 0, N = 1)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import configs
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    hc = host_cpus()
+    # every core this process may use: the affinity mask, capped by the cgroup quota and by
+    # OMP_NUM_THREADS (the GPU lease's CPU share: 16 on the one-GPU box) when those are set
+    threads = hc["affinity_cpus"] or os.cpu_count()
+    if hc["cgroup_cpu_quota"]:
+        threads = min(threads, max(1, int(hc["cgroup_cpu_quota"])))
+    if hc["omp_num_threads"]:
+        threads = min(threads, int(hc["omp_num_threads"]))
+    note = (f"{threads} threads = the CPUs this process may use (affinity {hc['affinity_cpus']}, cgroup quota "
+            f"{hc['cgroup_cpu_quota']}, OMP_NUM_THREADS {hc['omp_num_threads']}); the node exposes "
+            f"{hc['node_cpus']} CPUs, the rest belong to the other GPUs' leases")
     # the reference binary of the same arithmetic as the GPU run (the CMake-flag build by default)
     ref = os.path.join(REPO, "oracle", "_ref", "ref_render" if build == "ref" else "ref_render_exact")
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
@@ -168,7 +183,7 @@ def cpu_baseline(cfg_name, cfg, rays_per_frame, budget_s=3.0, build="ref"):
                     "sample": f"{cfg_name}: {reps} full frames of reference render() (render.hpp:87, "
                               f"-O3 -mavx2 -mfma -fopenmp{'' if build == 'ref' else ' -ffp-contract=off'}), "
                               f"median {ms:.2f} ms/frame, {out['rays']} rays/frame",
-                    "cpu_model": _cpu_model()}
+                    "cpu_model": _cpu_model(), "host": hc, "cores_note": note}
         except Exception as e:  # noqa: BLE001 -- fall through to the port
             sys.stderr.write(f"reference CPU baseline failed ({e}); timing the oracle port\n")
     import oracle
@@ -183,7 +198,7 @@ def cpu_baseline(cfg_name, cfg, rays_per_frame, budget_s=3.0, build="ref"):
     ms = float(np.median(times)) * 1e3
     return {"value": round(rays_per_frame / (ms * 1e3), 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{cfg_name}: {len(times)} full frames of oracle/liboracle.so, median {ms:.2f} ms/frame",
-            "cpu_model": _cpu_model()}
+            "cpu_model": _cpu_model(), "host": hc, "cores_note": note}
 
 
 def _cpu_model():
@@ -209,8 +224,144 @@ def pmc_entry(cfg_name, kernel):
         return None
 
 
-def roofline_block(name, nbytes, ms, pmc, scene_bytes):
-    """The roofline object for the dominant kernel (one launch = one frame).
+def l1_peak():
+    """The vector-L1 (TCP) ceiling in cache accesses per CU-cycle, calibrated on this chip with
+    tools/probes/l1_peak.hip under rocprofv3 --pmc (profiles/r06/l1_probe/l1_peak.json: the most
+    TCP_TOTAL_CACHE_ACCESSES per CU-cycle any of its load shapes sustained), or None."""
+    p = os.path.join(REPO, "profiles", "r06", "l1_probe", "l1_peak.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f).get("tcp_accesses_per_cu_cycle_peak")
+
+
+def measured_ceilings(pmc, ms, launches=1.0):
+    """Every ceiling the kernel's own counters price (round 6): the counts of
+    `launches` launches (rocprofv3 --pmc of that launch, per dispatch) over `ms` of wall time.
+      valu_issue   SQ_INSTS_VALU / (256 CUs x 2 wave-instructions per CU-cycle x 2.4 GHz)
+      salu_issue   SQ_INSTS_SALU / (256 x 1 x 2.4 GHz)
+      vmem_ta      TA busy cycles / TA cycles (measured in the profiled run itself)
+      vmem_td      TD busy cycles / TD cycles
+      l1           TCP_TOTAL_CACHE_ACCESSES / (256 x the probe's accesses per CU-cycle x 2.4 GHz)
+      l2           TCC_REQ x 128 B / 34.5 TB/s (128 B per request: an upper bound on its bytes)
+      hbm          DRAM bytes (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction) / 8 TB/s
+    Returns {name: {achieved, peak, unit, frac}} (only the ceilings the summary has counters for)."""
+    if not pmc or ms <= 0:
+        return {}
+    c = pmc.get("counters_mean_per_dispatch", {})
+    sec = ms * 1e-3
+    cyc = N_CU * CLOCK_GHZ * 1e9 * sec                      # CU-cycles in the window at max clock
+    out = {}
+
+    def put(k, achieved, peak, unit, note):
+        out[k] = {"achieved": round(achieved, 3), "peak": round(peak, 3), "unit": unit,
+                  "frac": round(achieved / peak, 4) if peak else None, "what": note}
+    if c.get("SQ_INSTS_VALU"):
+        put("valu_issue", launches * c["SQ_INSTS_VALU"] / sec / 1e9, N_CU * VALU_PER_CU_CYCLE * CLOCK_GHZ,
+            "G wave-instr/s", "VALU wave-instructions vs 2 per CU-cycle at 2.4 GHz")
+    if c.get("SQ_INSTS_SALU"):
+        put("salu_issue", launches * c["SQ_INSTS_SALU"] / sec / 1e9, N_CU * SALU_PER_CU_CYCLE * CLOCK_GHZ,
+            "G wave-instr/s", "SALU wave-instructions vs 1 per CU-cycle at 2.4 GHz")
+    if pmc.get("ta_busy_frac") is not None:
+        put("vmem_ta", pmc["ta_busy_frac"], 1.0, "busy fraction", "texture addresser (vector-memory issue) busy cycles")
+    if pmc.get("td_busy_frac") is not None:
+        put("vmem_td", pmc["td_busy_frac"], 1.0, "busy fraction", "texture data (vector-memory return) busy cycles")
+    peak_l1 = l1_peak()
+    if c.get("TCP_TOTAL_CACHE_ACCESSES_sum") and peak_l1:
+        put("l1", launches * c["TCP_TOTAL_CACHE_ACCESSES_sum"] / sec / 1e9, N_CU * peak_l1 * CLOCK_GHZ,
+            "G accesses/s", "vector-L1 (TCP) cache accesses vs the l1_peak probe's rate per CU-cycle")
+    if c.get("TCC_REQ_sum"):
+        put("l2", launches * c["TCC_REQ_sum"] * L2_REQ_BYTES / sec / 1e9, L2_PEAK_GBS, "GB/s",
+            "L2 (TCC) requests x 128 B vs the aggregate L2 bandwidth")
+    if pmc.get("hbm_bytes_per_launch"):
+        put("hbm", launches * pmc["hbm_bytes_per_launch"] / sec / 1e9, HBM_PEAK_GBS, "GB/s",
+            "DRAM bytes (FETCH_SIZE x 2 + WRITE_SIZE) vs 8 TB/s")
+    del cyc
+    return out
+
+
+def traffic_levels(pmc, launches=1.0):
+    """The measured traffic per level of the memory hierarchy, per launch: vector-L1 accesses,
+    L1 -> L2 read requests, L2 requests, DRAM bytes (rocprofv3 --pmc of the same launch)."""
+    if not pmc:
+        return None
+    c = pmc.get("counters_mean_per_dispatch", {})
+    g = lambda k: None if c.get(k) is None else int(round(launches * c[k]))   # noqa: E731
+    return {"tcp_accesses": g("TCP_TOTAL_CACHE_ACCESSES_sum"), "tcp_to_tcc_reads": g("TCP_TCC_READ_REQ_sum"),
+            "tcc_requests": g("TCC_REQ_sum"), "tcc_hit_rate": pmc.get("l2_hit_rate"),
+            "l1_hit_rate": None if not c.get("TCP_TOTAL_CACHE_ACCESSES_sum") or c.get("TCP_TCC_READ_REQ_sum") is None
+            else round(1 - c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"], 4),
+            "dram_read_bytes": None if pmc.get("hbm_read_bytes_per_launch") is None
+            else int(launches * pmc["hbm_read_bytes_per_launch"]),
+            "dram_write_bytes": None if pmc.get("hbm_write_bytes_per_launch") is None
+            else int(launches * pmc["hbm_write_bytes_per_launch"]),
+            "valu_instructions": g("SQ_INSTS_VALU"), "salu_instructions": g("SQ_INSTS_SALU"),
+            "vmem_read_instructions": g("SQ_INSTS_VMEM_RD"), "smem_instructions": g("SQ_INSTS_SMEM")}
+
+
+def roofline_block(name, nbytes, ms, pmc, scene_bytes, counted=None, launches=1.0):
+    """The roofline object of the dominant kernel (round 6: priced against the kernel's own
+    measured ceilings).
+
+    `bound` is the NEAREST measured ceiling -- the one with the largest achieved / peak among
+    measured_ceilings(): VALU and SALU issue, the vector-memory path (TA / TD busy), the vector
+    L1, the L2 and HBM -- so `frac` <= 1 by construction.  The reference's algorithmic bytes
+    (64 B per node-pair visit + 56 B per triangle test, Statistics of
+    single_ray_traverser.hpp:132-135) stay as the side block `algorithmic`; `build_bytes` is what
+    the build's own fetch sites moved (the counting build, bench.counted_bytes); `traffic_levels`
+    the measured bytes / requests per level.  Without counters: the bound is "unmeasured"."""
+    achieved_alg = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    traffic = None if pmc is None else pmc.get("hbm_bytes_per_launch")
+    ceil = measured_ceilings(pmc, ms, launches)
+    out = {"kernel": name, "mean_launch_ms": round(ms, 5), "traffic": traffic, "scene_device_bytes": scene_bytes,
+           "algorithmic_bytes_per_launch": nbytes,
+           "algorithmic": {"bytes_per_launch": nbytes, "achieved_gbs": round(achieved_alg, 1),
+                           "frac_l2": round(achieved_alg / L2_PEAK_GBS, 4),
+                           "frac_hbm": round(achieved_alg / HBM_PEAK_GBS, 4),
+                           "source": "reference Statistics per view (64 B / node pair + 56 B / triangle test); "
+                                     "not what this build fetches (see build_bytes), not a ceiling"},
+           "hbm_frac_algorithmic": round(achieved_alg / HBM_PEAK_GBS, 4)}
+    if counted:
+        cb = dict(counted)
+        cb["achieved_gbs"] = round(cb["total"] / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
+        out["build_bytes"] = cb
+    if not ceil:
+        out.update({"bound": "unmeasured", "achieved": round(achieved_alg, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                    "frac": None, "limiter": "unmeasured (no rocprofv3 --pmc summary for this launch)"})
+        return out
+    bname, b = max(ceil.items(), key=lambda kv: kv[1]["frac"] or 0.0)
+    out.update({"bound": bname, "achieved": b["achieved"], "peak": b["peak"], "unit": b["unit"], "frac": b["frac"],
+                "ceilings": ceil, "traffic_levels": traffic_levels(pmc, launches)})
+    out.update({k: pmc.get(k) for k in ("waitcnt_parked_frac", "issue_stall_frac", "active_inst_frac",
+                                        "l2_hit_rate", "valu_lane_utilisation") if pmc.get(k) is not None})
+    out["pmc_source"] = "profiles/pmc_summary.json (rocprofv3 --pmc of this launch, per dispatch)"
+    out["limiter"] = limiter_text(ceil, pmc, scene_bytes)
+    return out
+
+
+def limiter_text(ceil, pmc, scene_bytes):
+    """What the counters say bounds the launch, in numbers: each ceiling's fraction, nearest first,
+    then where the waves' cycles went."""
+    parts = [f"{k} {v['frac']:.2f}" for k, v in sorted(ceil.items(), key=lambda kv: -(kv[1]["frac"] or 0))]
+    wait, stall, act = pmc.get("waitcnt_parked_frac"), pmc.get("issue_stall_frac"), pmc.get("active_inst_frac")
+    txt = "ceilings (frac of peak): " + ", ".join(parts)
+    if wait is not None:
+        txt += (f"; wave-cycles: parked on s_waitcnt {wait:.2f}, issue-stalled {stall:.2f}, issuing {act:.2f}"
+                if stall is not None and act is not None else f"; waves parked on s_waitcnt {wait:.2f}")
+    top = max(v["frac"] or 0 for v in ceil.values())
+    if top < 0.7:
+        where = ("DRAM (scene larger than the 256-MiB Infinity Cache)" if scene_bytes and scene_bytes > 256 << 20
+                 else "MALL (scene larger than the L2s)" if scene_bytes and scene_bytes > 32 << 20
+                 else "L1 / L2 (scene L2-resident)")
+        txt += (f" -- no unit saturated: latency-bound (dependent record fetches served from {where}) "
+                "at the issue rate the resident waves sustain")
+    return txt
+
+
+def legacy_roofline_block(name, nbytes, ms, pmc, scene_bytes):
+    """Rounds 3-5's roofline object (kept so their committed bench lines still recompute,
+    tests/test_bench_roofline.py): algorithmic bytes priced against the L2 or HBM by a DRAM-bytes
+    rule -- a model bound, replaced in round 6 by roofline_block's measured ceilings.
 
     achieved = ALGORITHMIC bytes per launch / the launch's mean duration.  The
     bound is picked from the measured counters: DRAM bytes (FETCH_SIZE x2 + WRITE_SIZE, the gfx950
@@ -264,24 +415,115 @@ def roofline_block(name, nbytes, ms, pmc, scene_bytes):
     return out
 
 
-def roofline_step_block(nbytes, ms_step, world):
-    """The timed regime priced at the roofline: the algorithmic bytes of every frame of a step (all
-    ranks) / ms_per_step, per GPU, against the aggregate L2 (~34.5 TB/s) and against HBM (8 TB/s).
-    Steps overlap on several streams, so this is a sustained throughput, not a launch duration."""
+def step_trace_entry(cfg_name, arith):
+    """rocprofv3 kernel trace of bench.py's own timed loop for a config (tools/step_trace.py,
+    profiles/r06/step_trace_<config>_<arith>.json), or None."""
+    p = os.path.join(REPO, "profiles", "r06", f"step_trace_{cfg_name}_{arith}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
+
+
+def roofline_step_block(nbytes, ms_step, world, pmc=None, launches_per_step=None, trace=None):
+    """The timed regime (K steps over --streams streams) priced at its ceilings, per GPU.
+
+    Round 6: with the counters of the step's launch (`pmc`, per dispatch)
+    the step's own counts are launches_per_step x those, over ms_per_step: the same measured
+    ceilings as `roofline` (bound = the nearest, frac <= 1).  `trace` is the rocprofv3 kernel
+    trace of this very loop (tools/step_trace.py): the GPU's busy time per step and the summed
+    launch durations per step beside ms_per_step.  The algorithmic bytes per step stay as a side
+    field."""
     if not nbytes or ms_step <= 0:
         return None
     job = nbytes / (ms_step * 1e-3) / 1e9
     per_gpu = job / world
-    out = {"algorithmic_bytes_per_step": int(nbytes), "ms_per_step": round(ms_step, 5), "unit": "GB/s",
-           "achieved_job": round(job, 1), "achieved_per_gpu": round(per_gpu, 1),
-           "frac_l2": round(per_gpu / L2_PEAK_GBS, 4), "frac_hbm": round(per_gpu / HBM_PEAK_GBS, 4),
-           "source": "per-view reference Statistics, tests/golden/orbit/<config>.json (64 B/node pair + 56 B/test)"}
-    if out["frac_l2"] > 1.0:
-        # the per-ray bytes are not all L2 reads: a shadow packet reads a record once for the
-        # wavefront's ~60 rays through the scalar cache, and primary records hit the per-CU L1
-        out["above_l2_note"] = ("algorithmic (per-ray) bytes above the L2 rate: the shadow packets read each "
-                                "record once per wavefront through the scalar cache, primary records hit in L1")
+    out = {"algorithmic_bytes_per_step": int(nbytes), "ms_per_step": round(ms_step, 5),
+           "algorithmic": {"achieved_job_gbs": round(job, 1), "achieved_per_gpu_gbs": round(per_gpu, 1),
+                           "frac_l2": round(per_gpu / L2_PEAK_GBS, 4), "frac_hbm": round(per_gpu / HBM_PEAK_GBS, 4),
+                           "source": "per-view reference Statistics, tests/golden/orbit/<config>.json "
+                                     "(64 B/node pair + 56 B/test); not a ceiling"}}
+    ceil = measured_ceilings(pmc, ms_step, launches_per_step) if pmc and launches_per_step else {}
+    if ceil:
+        bname, b = max(ceil.items(), key=lambda kv: kv[1]["frac"] or 0.0)
+        out.update({"bound": bname, "achieved": b["achieved"], "peak": b["peak"], "unit": b["unit"],
+                    "frac": b["frac"], "launches_per_step": launches_per_step, "ceilings": ceil,
+                    "limiter": limiter_text(ceil, pmc, None)})
+    else:
+        out.update({"bound": "unmeasured", "frac": None})
+    if trace:
+        out["trace"] = {k: trace.get(k) for k in ("span_ms_per_step", "busy_ms_per_step", "kernel_ms_per_step",
+                                                  "mean_launch_ms", "overlap", "bench_ms_per_step", "steps",
+                                                  "streams")}
+        out["trace"]["source"] = "rocprofv3 --kernel-trace of bench.py's timed loop (tools/step_trace.py, profiles/r06/)"
     return out
+
+
+def legacy_roofline_step_block(nbytes, ms_step, world):
+    """Rounds 4-5's step block (kept so their committed lines recompute): the algorithmic bytes of a
+    step / ms_per_step, per GPU, against the L2 and HBM -- a model, not a measured ceiling."""
+    if not nbytes or ms_step <= 0:
+        return None
+    job = nbytes / (ms_step * 1e-3) / 1e9
+    per_gpu = job / world
+    return {"algorithmic_bytes_per_step": int(nbytes), "ms_per_step": round(ms_step, 5), "unit": "GB/s",
+            "achieved_job": round(job, 1), "achieved_per_gpu": round(per_gpu, 1),
+            "frac_l2": round(per_gpu / L2_PEAK_GBS, 4), "frac_hbm": round(per_gpu / HBM_PEAK_GBS, 4)}
+
+
+def counted_bytes(count_pkg, mesh, bvh, device, b12, s3, W, H, mode, tiling, with_float):
+    """The build's own bytes for one launch (round 6): the same launch through
+    the counting build (libceres_hip_count.so: the same kernels with a tally at every fetch site,
+    `make count`), {kind: bytes}, vector kinds per lane, scalar kinds per wavefront, + totals."""
+    import torch
+    sc = count_pkg.Scene(mesh, bvh, device=device)
+    F = len(b12)
+    rgb = torch.empty(F * 3 * W * H, dtype=torch.uint8, device=f"cuda:{device}")
+    px = torch.empty(F * 3 * W * H, dtype=torch.float32, device=f"cuda:{device}") if with_float else None
+    count_pkg.fetch_counters(device, reset=True)
+    sc.render_batch_device(b12, s3, W, H, mode=mode, tiling=tiling, d_pixels=0 if px is None else px.data_ptr(),
+                           d_rgb8=rgb.data_ptr(), stream=0)
+    c = count_pkg.fetch_counters(device, reset=True)
+    sc.close()
+    vec = sum(v for k, v in c.items() if k.endswith("_vector"))
+    scal = sum(v for k, v in c.items() if k.endswith("_scalar"))
+    c.update({"vector_total": vec, "scalar_total": scal, "total": vec + scal,
+              "note": "counting build: vector kinds x active lanes, scalar kinds once per wavefront; "
+                      "stores included (store_vector)"})
+    return c
+
+
+def load_count_package():
+    """The counting build as its own module instance (its own ctypes handle and code object), or
+    None when it was not built."""
+    import importlib.util
+    path = os.path.join(PKG_DIR, "variants", "libceres_hip_count.so")
+    if not os.path.exists(path):
+        return None
+    spec = importlib.util.spec_from_file_location("ceres_count_build", os.path.join(PKG_DIR, "__init__.py"),
+                                                  submodule_search_locations=[PKG_DIR])
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.LIB_PATH = path
+    mod.lib()
+    return mod
+
+
+def host_cpus():
+    """What the host exposes and what this process may use: the node's CPUs, the affinity mask,
+    the cgroup CPU quota (cpu.max), OMP_NUM_THREADS."""
+    info = {"node_cpus": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity_cpus"] = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    return info
 
 
 def choose_collect(requested, cfg, world, frames):
@@ -384,6 +626,8 @@ def main():
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-count", action="store_true",
+                    help="skip the counting build's pass (roofline.build_bytes: the build's own fetched bytes)")
     ap.add_argument("--no-orbit", action="store_true",
                     help="skip the second timed loop over the orbit views (`orbit_value`)")
     ap.add_argument("--no-alt", action="store_true",
@@ -392,8 +636,8 @@ def main():
     ap.add_argument("--collect", choices=("auto", "frames", "exchange", "gather"), default="auto",
                     help="N > 1: exchange = every frame's rows dealt over the ranks, each frame gathered to one "
                          "owner rank in one RCCL all-to-all; frames = each rank renders its F/N frames whole (no "
-                         "collective); gather = rows dealt, all frames to rank 0; auto = exchange, except frames "
-                         "for the tiled C4/C5 at N = 2 (DESIGN.md \"Multi-GPU\")")
+                         "collective); gather = rows dealt, all frames to rank 0; auto = frames, except exchange "
+                         "for the tiled C4/C5 at N >= 4 (choose_collect; DESIGN.md \"Multi-GPU\")")
     ap.add_argument("--prime-s", type=float, default=0.3,
                     help="untimed setup: seconds of steps before the W warmup steps (GPU clock ramp)")
     ap.add_argument("--streams", type=int, default=8,
@@ -730,9 +974,13 @@ def main():
         kname = "ceres_fused" if full_mode else "ceres_primary"
         if bb is not None:
             pmc_views = "" if views_kind == "config" else "_orbit"
-            roofline = roofline_block(kname, bb, batch_ms,
-                                      pmc_entry(args.config, f"{kname}_batch{nb_f}{pmc_views}_{args.arith}"),
-                                      scene.info()["device_bytes"])
+            batch_pmc = pmc_entry(args.config, f"{kname}_batch{nb_f}{pmc_views}_{args.arith}")
+            counted = None
+            if not args.no_count:
+                cp = load_count_package()
+                if cp is not None:
+                    counted = counted_bytes(cp, mesh, bvh, local_rank, vb12, vs3, W, H, mode, whole, bat_px is not None)
+            roofline = roofline_block(kname, bb, batch_ms, batch_pmc, scene.info()["device_bytes"], counted=counted)
             what = (f"{nb_f} copies of the config view" if views_kind == "config" else
                     f"{nb_f} orbit views (steps {vsteps[0]:g}..{vsteps[-1]:g} deg)")
             roofline.update(launch=f"ceres_render_batch_device, {what}, whole {W}x{H} frames, {n_b} launches "
@@ -767,6 +1015,13 @@ def main():
         roofline_solo = roofline_block(name, nbytes, mean_ms, pmc, scene.info()["device_bytes"])
         if roofline is None:
             roofline = roofline_solo
+    # the step's counts: its render launches (one per <= 56 frames per rank; rank 0's) x the counters of
+    # the 16-frame launch `roofline` prices (the step IS such launches: 16 copies of the config view)
+    step_pmc = None
+    launches_step = None
+    if full_mode and world == 1 and F % 16 == 0:
+        step_pmc = pmc_entry(args.config, f"ceres_fused_batch16{'' if views_kind == 'config' else '_orbit'}_{args.arith}")
+        launches_step = F // 16
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, cfg, meta[build]["rays"] if meta else rays_step // F, build=build)
 
@@ -775,8 +1030,10 @@ def main():
                            views_kind=views_kind, F=F, steps=args.steps, warmup=args.warmup, T=T,
                            rays_step=rays_step, hits_step=hits_step, full_mode=full_mode, row_block=args.row_block,
                            streams=S, float_fb=not args.no_float, arith=args.arith, roofline=roofline,
-                           roofline_step=roofline_step_block(bytes_step, T / args.steps * 1e3, world),
+                           roofline_step=roofline_step_block(bytes_step, T / args.steps * 1e3, world, step_pmc,
+                                                             launches_step, step_trace_entry(args.config, args.arith)),
                            roofline_solo=roofline_solo, cpu=cpu, parity=parity, alt=alt, orbit=orbit)
+        line["native"] = pkg.native_provenance()
         print(json.dumps(line), flush=True)
     scene.close()
     if world > 1:

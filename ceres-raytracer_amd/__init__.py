@@ -56,7 +56,8 @@ EXPORTED_SYMBOLS = (
     "ceres_orbit_cameras_f64_arith",
     "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_scene_shadow_stacks", "ceres_render_f32",
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_multi_f32", "ceres_device_count", "ceres_assemble_rgb8_packed", "ceres_render_records", "ceres_tiling_local_rows",
-    "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_orbit_cameras", "ceres_assemble_rgb8",
+    "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_fetch_counters",
+    "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
     "ceres_obj_load_arith", "ceres_proc_mesh_arith", "ceres_rotate_triangles_arith", "ceres_bvh_build_arith",
     "ceres_camera_basis_arith", "ceres_orbit_cameras_arith", "ceres_content_hash",
@@ -181,6 +182,7 @@ def lib():
     L.ceres_scene_read_timing.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                           _u64p]
     L.ceres_scene_wave_log.argtypes = [_vp, _u64p, _sz, ctypes.POINTER(_sz)]
+    L.ceres_fetch_counters.argtypes = [ctypes.c_int, _u64p, ctypes.c_int]
     L.ceres_content_hash.argtypes = [_vp, _sz]
     L.ceres_content_hash.restype = ctypes.c_uint64
     L.ceres_obj_load_arith.argtypes = L.ceres_obj_load.argtypes + [ctypes.c_int]
@@ -487,6 +489,50 @@ class Scene:
         p, q, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
         _check(lib().ceres_scene_read_timing(self._h, ctypes.byref(p), ctypes.byref(q), ctypes.byref(n)))
         return p.value, q.value, n.value
+
+
+def source_sha16(repo=None):
+    """sha256 (16 hex digits) of the sources libceres_hip.so is built from, in the Makefile's order
+    (build_info.o: include/*.h and include/ceres/*.hpp sorted by path, then csrc/*.cpp *.hip *.hpp
+    sorted by name); ceres_version() carries the value the loaded library was built with."""
+    import glob
+    import hashlib
+    repo = repo or os.path.dirname(_PKG)
+    inc = sorted(glob.glob(os.path.join(repo, "include", "*.h")) + glob.glob(os.path.join(repo, "include", "ceres", "*.hpp")))
+    csrc = os.path.join(_PKG, "csrc")
+    names = sorted(n for n in os.listdir(csrc) if n.endswith((".cpp", ".hip", ".hpp")))
+    h = hashlib.sha256()
+    for f in inc + [os.path.join(csrc, n) for n in names]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def native_provenance():
+    """Which native library this process loaded and whether it was built from the sources in this
+    tree: {lib, sha256 of the .so, sources_sha16 it was built with, sources_sha16 of the tree, match}."""
+    import hashlib
+    v = lib().ceres_version().decode()
+    built = v.rsplit(" src ", 1)[1] if " src " in v else None
+    with open(LIB_PATH, "rb") as fh:
+        so_sha = hashlib.sha256(fh.read()).hexdigest()
+    now = source_sha16()
+    return {"lib": os.path.relpath(LIB_PATH, os.path.dirname(_PKG)), "version": v, "so_sha256": so_sha,
+            "built_from_sources_sha16": built, "tree_sources_sha16": now, "built_from_this_tree": built == now}
+
+
+FETCH_KINDS = ("bvh2_vector", "bvh4_vector", "bvh4_scalar", "tri_vector", "tri_scalar", "shade_vector",
+               "store_vector", "order_scalar")
+COUNT_LIB_PATH = os.path.join(_PKG, "variants", "libceres_hip_count.so")
+
+
+def fetch_counters(device=0, reset=True):
+    """Bytes moved by the kernels' own fetch sites since the last reset (the counting build only,
+    `make count`; the product library raises CeresError EUNSUPPORTED): {kind: bytes}, vector kinds
+    per lane, scalar kinds per wavefront (include/ceres_render.h ceres_fetch_counters)."""
+    out = np.zeros(8, np.uint64)
+    _check(lib().ceres_fetch_counters(int(device), _p(out, ctypes.c_uint64), 1 if reset else 0))
+    return {k: int(v) for k, v in zip(FETCH_KINDS, out)}
 
 
 def render_multi(scenes, basis12, sun, W, H, row_block=8, mode=MODE_FULL, want_pixels=True, want_rgb8=True):

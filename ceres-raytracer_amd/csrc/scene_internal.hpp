@@ -71,6 +71,7 @@ struct ceres_scene {
     uint32_t dense_calls = 0;
     hipEvent_t ev_count = nullptr;
     int num_cus = 256;
+    size_t max_lds_per_block = 64 * 1024;   // hipDeviceProp_t::sharedMemPerBlock (set at scene creation)
     unsigned long long* d_wave_log = nullptr;   // stats scenes: per-wave diagnostic records
     size_t wave_log_waves = 0, last_grid_waves = 0;
     // optional per-launch device timing (ceres_scene_set_timing)

@@ -35,8 +35,10 @@
 // contracted scene; this header then renders, rotates and builds the camera basis in the same
 // arithmetic (CERES_ARITH_FMA / CERES_MODE_FMA).  Default: FMA when GCC optimises with FMA
 // enabled (__GNUC__ && !__clang__ && __FMA__ && __OPTIMIZE__), else contraction-free; override
-// with -DCERES_DROPIN_ARITH=CERES_ARITH_EXACT or CERES_ARITH_FMA (an automatic choice with FMA
-// enabled emits a #warning; -DCERES_DROPIN_QUIET silences it).  Link with -lceres_hip.
+// with -DCERES_DROPIN_ARITH=CERES_ARITH_EXACT or CERES_ARITH_FMA (the ambiguous automatic choice
+// -- FMA enabled, but clang or no optimisation -- emits a #warning, -DCERES_DROPIN_QUIET silences
+// it; the reference CMake configuration's choice is silent, -DCERES_DROPIN_VERBOSE announces it).
+// Link with -lceres_hip.
 #ifndef CERES_RENDER_HPP_DROPIN
 #define CERES_RENDER_HPP_DROPIN
 
@@ -60,10 +62,13 @@
 // preprocessor), so an automatic choice under -mfma is a guess: say so at compile time.  A caller
 // built with -ffp-contract=off must pass -DCERES_DROPIN_ARITH=CERES_ARITH_EXACT; clang contracts
 // within expressions by default, which matches neither reference build.
+// GCC + -mfma + optimisation is exactly the reference's own CMake configuration
+// (CMakeLists.txt:11-13), where the automatic FMA choice is right: that case is silent unless
+// CERES_DROPIN_VERBOSE asks; only the ambiguous cases below warn.
 #if defined(__GNUC__) && !defined(__clang__) && defined(__FMA__) && defined(__OPTIMIZE__)
 #define CERES_DROPIN_ARITH CERES_ARITH_FMA
-#if !defined(CERES_DROPIN_QUIET)
-#warning "ceres/render.hpp: CERES_DROPIN_ARITH auto-selected CERES_ARITH_FMA (GCC, -mfma, optimising = the reference CMake build); define CERES_DROPIN_ARITH (CERES_ARITH_EXACT for -ffp-contract=off callers) to silence"
+#if defined(CERES_DROPIN_VERBOSE)
+#warning "ceres/render.hpp: CERES_DROPIN_ARITH auto-selected CERES_ARITH_FMA (GCC, -mfma, optimising = the reference CMake build); define CERES_DROPIN_ARITH (CERES_ARITH_EXACT for -ffp-contract=off callers) to override"
 #endif
 #else
 #define CERES_DROPIN_ARITH CERES_ARITH_EXACT

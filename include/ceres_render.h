@@ -321,6 +321,17 @@ int ceres_scene_read_timing(ceres_scene* scene, double* kernel_ms, double* shado
  * the wavefront's primary node pairs, its shadow node pairs}.  Synchronises the device. */
 int ceres_scene_wave_log(ceres_scene* scene, uint64_t* out, size_t max_waves, size_t* n_waves);
 
+/* Diagnostic (round 6): the bytes the kernels' own fetch sites moved on `device` since the last
+ * reset -- out[8] = {64-B sibling-pair records by vector loads (per lane), BVH4 records by vector
+ * loads (per lane), BVH4 records through the scalar cache (per wavefront), triangles by vector
+ * loads (per lane), triangles through the scalar cache (per wavefront), shading fetches (hit
+ * triangle, orig index, vertex normals), framebuffer stores, tile-order entries}.  Only the
+ * counting build (`make count`: libceres_hip_count.so, compiled with -DCERES_COUNTING=1) tallies;
+ * the product library returns CERES_EUNSUPPORTED.  Synchronises the device; reset != 0 zeroes the
+ * tally afterwards.  No reference counterpart: it prices the build against the reference's
+ * Statistics (single_ray_traverser.hpp:132-135). */
+int ceres_fetch_counters(int device, uint64_t out[8], int reset);
+
 /* 64-bit content hash of a byte range (multithreaded; deterministic for a given byte string) --
  * what the drop-in include/ceres/render.hpp uses to honour render.hpp:86-156's per-call reading
  * of the caller's triangles / tri_norms / BVH while uploading a scene only when they change. */
@@ -331,6 +342,8 @@ uint64_t ceres_content_hash(const void* p, size_t bytes);
 const char* ceres_kernel_names(void);
 
 const char* ceres_last_error(void);
+/* "ceres-mi355x <version> (gfx950) src <16 hex>": the last field is the sha256 of the sources the
+ * library was built from (Makefile build_info.o), which bench.py checks against its own tree. */
 const char* ceres_version(void);
 
 #ifdef __cplusplus

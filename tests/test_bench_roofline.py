@@ -1,6 +1,11 @@
 """bench.py's roofline object (CPU): the bound is chosen from the measured counters, never
 hard-coded, and no field named as the bound exceeds its peak.
 
+Round 6: lines carrying `ceilings` are priced against the kernel's own
+measured ceilings (VALU / SALU issue, TA / TD busy, vector L1, L2, HBM) -- bound = the nearest,
+frac <= 1 -- and recompute through `bench.roofline_block`; older lines (no `ceilings`) recompute
+through `bench.legacy_roofline_block`, the rule they were priced with.
+
 Checked two ways: synthetic counter summaries through `bench.roofline_block`, and every committed
 bench line (`profiles/r03_end/sweep/bench_*.log`, `profiles/r0[45]/**/bench_*.log`) recomputed from its
 own algorithmic bytes, mean launch time and `profiles/pmc_summary.json` entry (round 5: the
@@ -25,24 +30,61 @@ def bench():
     return mod
 
 
+def _pmc(valu=567e6, salu=277e6, tcp=318e6, tcc=36e6, hbm=842e6, ta=0.21, td=0.26, wait=0.39):
+    return {"counters_mean_per_dispatch": {"SQ_INSTS_VALU": valu, "SQ_INSTS_SALU": salu,
+                                           "TCP_TOTAL_CACHE_ACCESSES_sum": tcp, "TCC_REQ_sum": tcc},
+            "hbm_bytes_per_launch": hbm, "ta_busy_frac": ta, "td_busy_frac": td, "waitcnt_parked_frac": wait,
+            "issue_stall_frac": 0.30, "active_inst_frac": 0.31, "l2_hit_rate": 0.83}
+
+
+def test_nearest_measured_ceiling_is_the_bound(bench):
+    """Round 6: bound = the ceiling with the largest achieved / peak; every ceiling <= 1 for counts a
+    real launch can produce; the algorithmic bytes are a side block, not a bound."""
+    rf = bench.roofline_block("ceres_fused", 21_806_559_872, 0.954, _pmc(), 3_764_016)
+    c = rf["ceilings"]
+    assert rf["bound"] == max(c, key=lambda k: c[k]["frac"])
+    assert rf["frac"] == c[rf["bound"]]["frac"] and 0 < rf["frac"] <= 1
+    # the round-5 C3 launch: VALU issue 567M / (256 x 2 x 2.4 GHz x 0.954 ms) = 0.48
+    assert abs(c["valu_issue"]["frac"] - 567e6 / (256 * 2 * 2.4e9 * 0.954e-3)) < 1e-3
+    assert abs(c["salu_issue"]["frac"] - 277e6 / (256 * 2.4e9 * 0.954e-3)) < 1e-3
+    assert abs(c["hbm"]["frac"] - 842e6 / 0.954e-3 / 8e12) < 1e-3
+    assert rf["algorithmic"]["frac_hbm"] > 2 and "bound" not in rf["algorithmic"]
+    assert rf["limiter"].startswith("ceilings (frac of peak): " + rf["bound"])
+    # an HBM-streaming launch: hbm is the nearest ceiling
+    hb = bench.roofline_block("k", 1e9, 0.2, _pmc(valu=1e6, salu=1e6, tcp=1e6, tcc=1e6, hbm=1.2e9, ta=0.1, td=0.1), 1 << 30)
+    assert hb["bound"] == "hbm" and hb["unit"] == "GB/s" and 0.7 < hb["frac"] <= 1
+    none = bench.roofline_block("k", 1e9, 1.0, None, 1 << 20)
+    assert none["bound"] == "unmeasured" and none["frac"] is None and none["limiter"].startswith("unmeasured")
+
+
+def test_step_block_prices_launch_counts_over_the_step(bench):
+    """roofline_step: the step's launches x the launch's counters over ms_per_step."""
+    rs = bench.roofline_step_block(21.8e9, 0.8, 1, _pmc(), 1, {"busy_ms_per_step": 0.79, "kernel_ms_per_step": 0.95})
+    assert abs(rs["ceilings"]["valu_issue"]["frac"] - 567e6 / (256 * 2 * 2.4e9 * 0.8e-3)) < 1e-3
+    assert rs["bound"] == max(rs["ceilings"], key=lambda k: rs["ceilings"][k]["frac"]) and rs["frac"] <= 1
+    assert rs["trace"]["busy_ms_per_step"] == 0.79
+    assert bench.roofline_step_block(21.8e9, 0.8, 1)["bound"] == "unmeasured"
+
+
 def test_bound_follows_counters(bench):
+    """The legacy (rounds 3-5) rule, kept for their committed lines."""
     nbytes, ms = 1_362_909_224, 0.1647
-    l2 = bench.roofline_block("ceres_fused", nbytes, ms, {"hbm_bytes_per_launch": 52e6,
+    l2 = bench.legacy_roofline_block("ceres_fused", nbytes, ms, {"hbm_bytes_per_launch": 52e6,
                                                          "waitcnt_parked_frac": 0.36, "ta_busy_frac": 0.10,
                                                          "l2_hit_rate": 0.67}, 3_764_016)
     assert l2["bound"] == "l2" and l2["peak"] == bench.L2_PEAK_GBS
     assert 0 < l2["frac"] <= 1 and l2["hbm_frac_algorithmic"] > 1     # bytes served on-die
     assert "L2-resident" in l2["limiter"]
-    hbm = bench.roofline_block("k", 1e9, 0.2, {"hbm_bytes_per_launch": 0.9e9,
+    hbm = bench.legacy_roofline_block("k", 1e9, 0.2, {"hbm_bytes_per_launch": 0.9e9,
                                                "waitcnt_parked_frac": 0.2, "ta_busy_frac": 0.6}, 1 << 30)
     assert hbm["bound"] == "hbm" and hbm["peak"] == bench.HBM_PEAK_GBS
     assert hbm["limiter"] == "HBM bandwidth"                            # 4.5 TB/s of DRAM traffic
-    dram_lat = bench.roofline_block("k", 2e9, 3.0, {"hbm_bytes_per_launch": 1.5e9,
+    dram_lat = bench.legacy_roofline_block("k", 2e9, 3.0, {"hbm_bytes_per_launch": 1.5e9,
                                                     "waitcnt_parked_frac": 0.55, "l2_hit_rate": 0.75},
                                    1_260_000_000)
     assert dram_lat["bound"] == "hbm" and dram_lat["frac"] < 0.1
     assert dram_lat["limiter"].startswith("dependent-load latency") and "DRAM" in dram_lat["limiter"]
-    none = bench.roofline_block("k", 1e9, 1.0, None, 1 << 20)
+    none = bench.legacy_roofline_block("k", 1e9, 1.0, None, 1 << 20)
     assert none["traffic"] is None and none["limiter"].startswith("unmeasured")
 
 
@@ -50,7 +92,8 @@ def _bench_lines():
     out = []
     for p in sorted(glob.glob(os.path.join(REPO, "profiles", "r03_end", "sweep", "bench_*.log")) +
                     glob.glob(os.path.join(REPO, "profiles", "r04", "**", "bench_*.log"), recursive=True) +
-                    glob.glob(os.path.join(REPO, "profiles", "r05", "**", "bench_*.log"), recursive=True)):
+                    glob.glob(os.path.join(REPO, "profiles", "r05", "**", "bench_*.log"), recursive=True) +
+                    glob.glob(os.path.join(REPO, "profiles", "r06", "**", "bench_*.log"), recursive=True)):
         with open(p) as f:
             lines = [ln for ln in f if ln.startswith("{") and '"roofline"' in ln]
         if lines:
@@ -71,6 +114,11 @@ def _pmc_key(line, rf, which):
 
 
 def _session_pmc(name, cfg, key):
+    """(see below)"""
+    return _session_pmc_impl(name, cfg, key)
+
+
+def _session_pmc_impl(name, cfg, key):
     """The counters a round-5 session priced its bench line with: that session's own summary
     (`pmc_summary_*.json` beside the bench log, merged into profiles/pmc_summary.json on the box
     before the bench ran), which a later session's merge may have replaced globally."""
@@ -94,8 +142,17 @@ def test_committed_sweep_roofline_recomputes(bench, name, line):
         if which == "roofline_solo" and line.get("arith") == "exact" and rf["traffic"] is not None and \
                 (pmc or {}).get("hbm_bytes_per_launch") != rf["traffic"]:
             pmc = bench.pmc_entry(cfg, rf["kernel"])          # bench.py's fallback for the exact solo launch
-        again = bench.roofline_block(rf["kernel"], rf["algorithmic_bytes_per_launch"], rf["mean_launch_ms"],
-                                     pmc, rf["scene_device_bytes"])
+        new = "ceilings" in rf or rf.get("bound") == "unmeasured"
+        fn = bench.roofline_block if new else bench.legacy_roofline_block
+        again = fn(rf["kernel"], rf["algorithmic_bytes_per_launch"], rf["mean_launch_ms"], pmc, rf["scene_device_bytes"])
+        if new:
+            # round 6: the nearest measured ceiling, recomputed from the line's own launch time and
+            # the session's counters; every ceiling <= 1
+            assert again["bound"] == rf["bound"], (name, which)
+            if rf["bound"] != "unmeasured":
+                assert abs(again["frac"] - rf["frac"]) <= 1e-3, (name, which)
+                assert all(v["frac"] <= 1.0 for v in again["ceilings"].values()), (name, which, again["ceilings"])
+            continue
         if rf["traffic"] is None and pmc is not None:
             # the counters were collected after this line (same build, same launch): the line
             # recomputes to the priced block; only its bound may then differ
@@ -130,6 +187,9 @@ def _check_trace_agreement(name, line):
 
 @pytest.mark.parametrize("name,line", [x for x in _bench_lines() if "roofline_step" in x[1]])
 def test_committed_roofline_step_recomputes(bench, name, line):
+    if "algorithmic" in (line["roofline_step"] or {}):
+        _check_step_r06(bench, name, line)
+        return
     """roofline_step = the step's algorithmic bytes (every frame's pinned reference statistics, in the
     line's arithmetic) / ms_per_step, per GPU, against L2 and HBM."""
     rs = line["roofline_step"]
@@ -149,12 +209,49 @@ def test_committed_roofline_step_recomputes(bench, name, line):
     nbytes = sum(bench.algorithmic_bytes(bench.view_entry(fx[bench.step_key(np.float32(x))], build)["stats"])
                  for x in steps)
     assert nbytes == rs["algorithmic_bytes_per_step"]
-    again = bench.roofline_step_block(nbytes, line["ms_per_step"], line["n_gpus"])
+    again = bench.legacy_roofline_step_block(nbytes, line["ms_per_step"], line["n_gpus"])
     for k in ("achieved_job", "achieved_per_gpu", "frac_l2", "frac_hbm"):
         assert abs(again[k] - rs[k]) <= 1e-3 * abs(rs[k]) + 1e-3, k
     # per-ray bytes may exceed the L2 rate (packets: one scalar-cache read per wavefront for ~60
     # rays; L1 hits); bench.py says so in the block
     assert again["frac_l2"] <= 1.0 or rs.get("above_l2_note"), (name, again["frac_l2"])
+
+
+def _check_step_r06(bench, name, line):
+    """Round 6 step block: the algorithmic side block recomputes, the bound is the nearest measured
+    ceiling (<= 1), and a step trace of the same loop (when the line carries one) shows the GPU busy
+    for at most the step's wall time."""
+    rs = line["roofline_step"]
+    cfg = line["config"]["workload"].split(":")[0]
+    pmc = _session_pmc(name, cfg, f"ceres_fused_batch16_{line['arith']}") or \
+        bench.pmc_entry(cfg, f"ceres_fused_batch16_{line['arith']}")
+    again = bench.roofline_step_block(rs["algorithmic_bytes_per_step"], line["ms_per_step"], line["n_gpus"], pmc,
+                                      rs.get("launches_per_step"), None)
+    assert again["bound"] == rs["bound"], name
+    if rs["bound"] != "unmeasured":
+        assert abs(again["frac"] - rs["frac"]) <= 1e-3 and rs["frac"] <= 1.0, name
+    for k in ("achieved_per_gpu_gbs", "frac_l2", "frac_hbm"):
+        assert abs(again["algorithmic"][k] - rs["algorithmic"][k]) <= 1e-3 * abs(rs["algorithmic"][k]) + 1e-3, k
+    tr = rs.get("trace")
+    if tr:
+        assert tr["busy_ms_per_step"] <= tr["span_ms_per_step"] * 1.0001, name
+
+
+def test_step_trace_pairs_with_its_bench_line():
+    """the kept rocprofv3 trace of bench.py's own 8-stream loop (tools/step_trace.py)
+    shows the GPU busy per step within the step's wall time, the launches overlapping (summed
+    launch time per step above the busy time), and agrees with the ms_per_step the same run printed
+    (within 5 %: the profiler's own overhead)."""
+    files = glob.glob(os.path.join(REPO, "profiles", "r06", "step_trace_*.json"))
+    if not files:
+        pytest.skip("no step trace kept yet")
+    for p in files:
+        with open(p) as f:
+            t = json.load(f)
+        assert t["busy_ms_per_step"] <= t["span_ms_per_step"] * 1.0001, p
+        assert t["span_ms_per_step"] <= t["bench_ms_per_step"] * 1.05, p
+        assert t["busy_ms_per_step"] >= 0.8 * t["bench_ms_per_step"], p      # the GPU is the step's limiter
+        assert t["kernel_ms_per_step"] >= t["busy_ms_per_step"] * 0.999, p
 
 
 def test_headline_trace_pairing_is_kept():
