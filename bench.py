@@ -481,7 +481,8 @@ def counted_bytes(count_pkg, mesh, bvh, device, b12, s3, W, H, mode, tiling, wit
     rgb = torch.empty(F * 3 * W * H, dtype=torch.uint8, device=f"cuda:{device}")
     px = torch.empty(F * 3 * W * H, dtype=torch.float32, device=f"cuda:{device}") if with_float else None
     count_pkg.fetch_counters(device, reset=True)
-    sc.render_batch_device(b12, s3, W, H, mode=mode, tiling=tiling, d_pixels=0 if px is None else px.data_ptr(),
+    til = count_pkg.Tiling(tiling.row_block, tiling.rank, tiling.world)      # the count module's own ctypes type
+    sc.render_batch_device(b12, s3, W, H, mode=mode, tiling=til, d_pixels=0 if px is None else px.data_ptr(),
                            d_rgb8=rgb.data_ptr(), stream=0)
     c = count_pkg.fetch_counters(device, reset=True)
     sc.close()
