@@ -47,7 +47,7 @@ def summarize(rows, line, prefix="ceres_fused"):
     F = line["config"]["frames_per_step"]
     per_launch = 56                                  # kFramesPerLaunch: frames per kernel launch
     L = (F + per_launch - 1) // per_launch if line["n_gpus"] == 1 else None
-    ren = [r for r in rows if r[0].startswith(prefix)]
+    ren = [r for r in rows if prefix + "<" in r[0] or r[0].startswith(prefix)]
     timed = ren[-K * L:]
     t0, t1 = timed[0][1], max(r[2] for r in timed)
     # every kernel of any name inside the window (assembly, collectives) counts for the busy time
