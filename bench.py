@@ -482,10 +482,13 @@ def counted_bytes(count_pkg, mesh, bvh, device, b12, s3, W, H, mode, tiling, wit
     px = torch.empty(F * 3 * W * H, dtype=torch.float32, device=f"cuda:{device}") if with_float else None
     count_pkg.fetch_counters(device, reset=True)
     til = count_pkg.Tiling(tiling.row_block, tiling.rank, tiling.world)      # the count module's own ctypes type
+    err = torch.zeros(8, dtype=torch.int64, device=f"cuda:{device}")
     sc.render_batch_device(b12, s3, W, H, mode=mode, tiling=til, d_pixels=0 if px is None else px.data_ptr(),
-                           d_rgb8=rgb.data_ptr(), stream=0)
+                           d_rgb8=rgb.data_ptr(), d_counters=err.data_ptr(), stream=0)
     c = count_pkg.fetch_counters(device, reset=True)
     sc.close()
+    # this build also carries the production walk's stack guard (CERES_STACK_GUARD): its error word
+    c["guard_error_word"] = int(err[6].item())
     vec = sum(v for k, v in c.items() if k.endswith("_vector"))
     scal = sum(v for k, v in c.items() if k.endswith("_scalar"))
     c.update({"vector_total": vec, "scalar_total": scal, "total": vec + scal,
@@ -802,6 +805,22 @@ def main():
                 # ceres_finalize's error word: a traversal stack overflowed (single_ray_traverser.hpp:29
                 # asserts instead), so some frame of the batch is wrong -- never time a wrong render
                 raise SystemExit(f"bench.py: traversal stack overflow in the validation batch (error word {int(c[6]):#x})")
+            # The production kernels' BVH2 walk has no per-step stack check (the bound is exact by
+            # construction); the stats kernels -- the same walk in the same order, with clamps and
+            # the overflow flag -- trace this rank's views of the step once more, and the timed
+            # loop runs only if they report no overflow.
+            sc_stats = pkg.Scene(mesh, bvh, device=local_rank, stats=True)
+            cs = torch.zeros(8, dtype=torch.int64, device=dev)
+            for f0 in range(0, self.Fl, MAXF):
+                f1 = min(self.Fl, f0 + MAXF)
+                tmp = torch.empty((f1 - f0) * 3 * W * max(self.rows, 1), dtype=torch.uint8, device=dev)
+                sc_stats.render_batch_device(self.b12[f0:f1], self.s3[f0:f1], W, H, mode=mode, tiling=self.tiling,
+                                             d_rgb8=tmp.data_ptr(), d_counters=cs.data_ptr(), stream=stream.cuda_stream)
+                torch.cuda.synchronize(dev)
+                if int(cs[6].item()):
+                    raise SystemExit("bench.py: the stats kernels report a traversal stack overflow for the step's views")
+            sc_stats.close()
+            self.stack_checked = True
             mine = (list(zip(self.gather.owned_frames(), full)) if self.exchange
                     else ([(f, full[f]) for f in range(F)] if rank == 0 else []))
             head = b"P6 %d %d 255\n" % (W, H)
@@ -821,6 +840,8 @@ def main():
             ref_rays = sum(e["rays"] for e in keys) if all(keys) else None
             ref_hits = sum(e["hits"] for e in keys) if all(keys) else None
             checks = {"frames": F, "frames_checked": int(stat[0]), "frames_unpinned": int(stat[2]),
+                      "stack_bound_checked": "production error word (BVH4 walks) + a stats-kernel pass of the "
+                                             "step's views (BVH2 clamps + overflow flag): no overflow",
                       "all_frames_match_reference": bool(stat[2] == 0 and stat[1] == stat[0] == F),
                       "step_rays_match_reference": None if ref_rays is None else int(c[0]) == ref_rays,
                       "step_hits_match_reference": None if ref_hits is None else int(c[1]) == ref_hits}

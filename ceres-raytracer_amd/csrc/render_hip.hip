@@ -46,6 +46,9 @@
 
 #pragma clang fp contract(off)
 
+#ifndef CERES_COUNTING
+#define CERES_COUNTING 0                       // 1: the diagnostic build (make count): fetch tallies + stack guard
+#endif
 #ifndef CERES_TILES_PER_WAVE
 #define CERES_TILES_PER_WAVE 4                // fused kernel, batches: consecutive tile-order entries (1, 2, 4 or 8) per
 #endif                                        // wavefront (A/B, 16-frame batches x 8 streams: 4 beats 2 by 2 %; round 5
@@ -74,8 +77,8 @@
 #define CERES_TRUST_STACK_BOUND 1              // BVH2 steps of non-stats kernels: no stack clamps / overflow flag
 #endif
 #ifndef CERES_STACK_GUARD
-#define CERES_STACK_GUARD 1                    // production kernels: the BVH2 stack's guard slot (guarded_trace)
-#endif
+#define CERES_STACK_GUARD CERES_COUNTING       // the BVH2 stack's guard slot (guarded_trace): the diagnostic (counting)
+#endif                                         // build only -- in the product it cost 1.9 % (C3) / 6.5 % (C5) of a batch
 #ifndef CERES_LOCAL_ORDER
 #define CERES_LOCAL_ORDER 1                    // XCD-local Morton tile order (ensure_tile_order); 0: never
 #endif
@@ -210,9 +213,6 @@ enum FetchKind : int {
     kFOrderS,      // tile-order entries (scalar)
     kFKinds
 };
-#ifndef CERES_COUNTING
-#define CERES_COUNTING 0
-#endif
 #if CERES_COUNTING
 constexpr int kFetchShards = 16;
 __device__ unsigned long long g_fetch[kFetchShards][kFKinds];
@@ -573,14 +573,17 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     return have;
 }
 
-// trace() with the production kernels' stack guard (round 6).  Without the
-// stats kernels' clamps (CERES_TRUST_STACK_BOUND), a step writes the far child to slot sp, and
-// with the exact bound sp <= depth - 1 = stack_entries - 1, so slot stack_entries is never
-// written unless the bound is broken -- and a walk that overruns it must pass through it (sp
-// moves by one per step).  The slot holds a value no node index takes (stack_guard); a changed
-// guard sets the overflow flag, hence the error word: one LDS write and one read per ray, outside
-// the octant-specialised loops (a compare or a max per step cost the 24-bit-stack batch kernel
-// two VGPRs and a wave per SIMD).
+// trace() with a stack guard (round 6; CERES_STACK_GUARD: compiled into the
+// diagnostic build, libceres_hip_count.so).  Without the stats kernels' clamps
+// (CERES_TRUST_STACK_BOUND), a step writes the far child to slot sp, and with the exact bound
+// sp <= depth - 1 = stack_entries - 1, so slot stack_entries is never written unless the bound is
+// broken -- and a walk that overruns it must pass through it (sp moves by one per step).  The slot
+// holds a value no node index takes (stack_guard); a changed guard sets the overflow flag, hence
+// the error word.  One LDS write and one read per ray -- measured in the product: 16-frame batches
+// x 8 streams C3 +1.9 %, C5 +6.5 % (one more VGPR spill; the 24-bit-stack batch kernel 80 -> 84
+// VGPRs, a wave per SIMD less; profiles/r06/ab_guard), so the product relies on the exact bound,
+// and bench.py checks every timed view with the stats kernels (clamps + flag) and with this
+// build's guard before it times them.
 template <bool kStats, int kS, typename StkT, bool kRobust, int kOct, bool kG>
 __device__ __forceinline__ bool guarded_trace(const KParams& P, F3 o, F3 d, StkT stk, Hit& best, uint32_t& n_pairs,
                                               uint32_t& n_tests, bool& overflow) {

@@ -30,32 +30,80 @@ def dragon(gpu):
     sc.close()
 
 
+def _count_build():
+    import importlib.util
+    pkgdir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ceres-raytracer_amd")
+    path = os.path.join(pkgdir, "variants", "libceres_hip_count.so")
+    assert os.path.exists(path), "the diagnostic build is part of build() (make all)"
+    spec = importlib.util.spec_from_file_location("ceres_count_build_t", os.path.join(pkgdir, "__init__.py"),
+                                                  submodule_search_locations=[pkgdir])
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.LIB_PATH = path
+    mod.lib()
+    return mod
+
+
 def test_stack_guard_reports_an_overrun(gpu, dragon, monkeypatch):
-    """guarded_trace: the production kernels (no per-step clamps) keep a guard value in LDS slot
-    stack_entries, which an exact bound never reaches.  CERES_DEBUG_GUARD_SLOT moves the guard down
-    into slots deep walks DO write (the LDS carve-up and every index unchanged), so the guard is
-    overwritten: the render must fail with CERES_ESTACK -- single frames (work-stealing kernel)
-    and batches (packet kernel) alike -- and succeed again once the guard is back in place."""
+    """guarded_trace (the diagnostic build, libceres_hip_count.so, which bench.py runs over the timed
+    views): the walk without per-step clamps keeps a guard value in LDS slot stack_entries, which
+    an exact bound never reaches.  CERES_DEBUG_GUARD_SLOT moves the guard down into slots deep walks
+    DO write (the LDS carve-up and every index unchanged), so the guard is overwritten: the render
+    must fail with CERES_ESTACK -- single frames (work-stealing kernel) and batches (packet kernel)
+    alike -- and succeed again, with the product's bytes, once the guard is back in place."""
+    import torch
     pkg = gpu
-    cfg, mesh, bvh, cam, sc = dragon
+    cfg, mesh, bvh, cam, prod = dragon
+    cb = _count_build()
+    sc = cb.Scene(mesh, bvh)
     W, H = cfg["W"], cfg["H"]
     b12 = cam.basis(W, H)
-    _, rgb0, st0 = sc.render(b12, cfg["sun"], W, H, mode=pkg.MODE_FULL | pkg.MODE_FMA)
+    mode = pkg.MODE_FULL | pkg.MODE_FMA
+    _, rgb0, st0 = prod.render(b12, cfg["sun"], W, H, mode=mode)
     monkeypatch.setenv("CERES_DEBUG_GUARD_SLOT", "2")
-    with pytest.raises(pkg.CeresError, match="-5"):
-        sc.render(b12, cfg["sun"], W, H, mode=pkg.MODE_FULL | pkg.MODE_FMA)
-    import torch
+    with pytest.raises(cb.CeresError, match="-5"):
+        sc.render(b12, cfg["sun"], W, H, mode=mode)
     F = 4
     rgb = torch.zeros(F * 3 * W * H, dtype=torch.uint8, device="cuda")
     cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     sc.render_batch_device(np.repeat(b12[None], F, 0), np.repeat(np.asarray(cfg["sun"], np.float32)[None], F, 0), W, H,
-                           mode=pkg.MODE_FULL | pkg.MODE_FMA, d_rgb8=rgb.data_ptr(), d_counters=cnt.data_ptr(), stream=st)
+                           mode=mode, d_rgb8=rgb.data_ptr(), d_counters=cnt.data_ptr(), stream=st)
     torch.cuda.synchronize()
     assert int(cnt[6].item()) != 0, "the batch kernel's error word must report the overwritten guard"
     monkeypatch.delenv("CERES_DEBUG_GUARD_SLOT")
-    _, rgb1, st1 = sc.render(b12, cfg["sun"], W, H, mode=pkg.MODE_FULL | pkg.MODE_FMA)
+    _, rgb1, st1 = sc.render(b12, cfg["sun"], W, H, mode=mode)
     assert np.array_equal(rgb0, rgb1) and (st0["rays"], st0["hits"]) == (st1["rays"], st1["hits"])
+    sc.close()
+
+
+def test_counting_build_tallies_fetches(gpu, dragon):
+    """The diagnostic build's fetch tallies (bench.py roofline.build_bytes): zero before a render,
+    then every kind a dragon batch exercises is non-zero, the stores equal 15 B per pixel (float +
+    RGB8), and the product library refuses the call (EUNSUPPORTED) instead of reporting zeros."""
+    import torch
+    pkg = gpu
+    cfg, mesh, bvh, cam, _ = dragon
+    cb = _count_build()
+    sc = cb.Scene(mesh, bvh)
+    W, H = cfg["W"], cfg["H"]
+    F = 4
+    b12 = np.repeat(cam.basis(W, H)[None], F, 0)
+    s3 = np.repeat(np.asarray(cfg["sun"], np.float32)[None], F, 0)
+    rgb = torch.zeros(F * 3 * W * H, dtype=torch.uint8, device="cuda")
+    px = torch.zeros(F * 3 * W * H, dtype=torch.float32, device="cuda")
+    cb.fetch_counters(0, reset=True)
+    assert sum(cb.fetch_counters(0, reset=False).values()) == 0
+    sc.render_batch_device(b12, s3, W, H, mode=pkg.MODE_FULL | pkg.MODE_FMA, d_pixels=px.data_ptr(),
+                           d_rgb8=rgb.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    c = cb.fetch_counters(0, reset=True)
+    assert c["store_vector"] == 15 * F * W * H
+    for k in ("bvh2_vector", "bvh4_scalar", "tri_scalar", "shade_vector", "order_scalar"):
+        assert c[k] > 0, k
+    assert c["bvh2_vector"] % 64 == 0 and c["tri_vector"] % 48 == 0
+    with pytest.raises(pkg.CeresError, match="-6"):
+        pkg.fetch_counters(0)
+    sc.close()
 
 
 @pytest.mark.parametrize("sun", [(np.inf, 0.0, 0.0), (0.0, -np.inf, 3.0), (np.nan, 1.0, 1.0), (1e38, -3e38, 2e38)])
