@@ -15,7 +15,7 @@ step() { local t=$1; shift; local name=$1; shift; timeout -k 10 "$t" "$@" > "$OU
          if [ $rc -ne 0 ]; then echo "STOP after $name"; exit $rc; fi; }
 has() { case " ${STEPS:-tests bench} " in *" $1 "*) return 0;; esac; return 1; }
 if has tests; then
-  step 900 pytest_gpu python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:-}
+  step 900 pytest_gpu python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:-}
 fi
 if has bench; then
   step 400 bench_dragon_1080 python bench.py ${BENCH_ARGS:-}
