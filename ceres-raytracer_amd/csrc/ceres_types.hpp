@@ -167,7 +167,6 @@ struct KParams {
     uint32_t tile_packed;                        // fused kernel: tile_order entries are pack_tile() words
     const uint32_t* tile_order;                  // fused kernel: block -> batch tile (centre first)
     const SiblingPair* pairs;
-    const SiblingPair* blocks;                   // two-level blocks of the same pairs (build_pair_blocks; trace_blk)
     const Node4* nodes4;                         // shadow-ray BVH4 over the same leaf slots
     const QNode4* qnodes4;                       // its compressed copy (CERES_MODE_QBVH4 only)
     const Tri48* tris;
@@ -207,7 +206,6 @@ int relayout_bvh(const RefNode* nodes, size_t n_nodes, const uint64_t* prim, siz
 int build_shadow_bvh4(const std::vector<SiblingPair>& pairs, std::vector<Node4>& out, uint32_t& stack_bound,
                       uint32_t& not_collapsed);
 int order_shadow_bvh4(std::vector<Node4>& nodes, uint32_t& first_bound);
-int build_pair_blocks(const std::vector<SiblingPair>& pairs, std::vector<SiblingPair>& blocks);
 int relayout_bvh64(const RefNode64* nodes, size_t n_nodes, const uint64_t* prim, size_t n_tri, const Tri96* tris,
                    std::vector<SiblingPair64>& pairs, std::vector<Tri96>& leaf_tris, std::vector<uint32_t>& orig,
                    uint32_t& depth, uint32_t& root_leaf_count, uint32_t& root_leaf_first);

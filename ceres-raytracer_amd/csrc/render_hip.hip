@@ -76,11 +76,8 @@
 #ifndef CERES_TRUST_STACK_BOUND
 #define CERES_TRUST_STACK_BOUND 1              // BVH2 steps of non-stats kernels: no stack clamps / overflow flag
 #endif
-#ifndef CERES_BLK_WALK
-#define CERES_BLK_WALK 1                       // one-frame launches walk the BVH2 in two-level blocks (trace_blk)
-#endif
-#ifndef CERES_BLK_MINW
-#define CERES_BLK_MINW 1                       // VGPR budget (waves/SIMD) of the 16-bit-stack trace_blk kernel (1: none)
+#ifndef CERES_PAIR_STORES
+#define CERES_PAIR_STORES 1                    // batch kernels: a wavefront's tile pairs store back to back (PairStash)
 #endif
 #ifndef CERES_STACK_GUARD
 #define CERES_STACK_GUARD CERES_COUNTING       // the BVH2 stack's guard slot (guarded_trace): the diagnostic (counting)
@@ -579,109 +576,6 @@ __device__ __forceinline__ bool trace(const KParams& P, F3 o, F3 d, StkT stk, Hi
     return have;
 }
 
-// Two-level BVH2 walk (round 6): trace()'s exact walk -- the same steps in the
-// same order, the same slab tests, leaf tests and stack -- over 192-B two-level records
-// (build_pair_blocks): record p = pair p followed by the pairs of its two children (when inner).
-// One iteration fetches ONE record and runs up to TWO of the reference's steps: the step at pair p,
-// then -- when it descends -- the step at the near child, whose pair came with the record.  So a
-// descending ray waits for one dependent fetch per two levels instead of one per level, and every
-// lane of the wavefront fetches into the same registers once per iteration (a lane that takes its
-// child from registers while another fetches into them would make the whole wavefront wait for
-// the fetch before its triangle tests).  A lane whose first step pops or ends runs no second step
-// in that iteration.  The records are bit-identical copies of the pairs and their child words are
-// pair indices, so every decision -- hence every pixel and count -- is trace()'s.  Used where the
-// walk is latency-bound (one-frame launches: a frame ends with its slowest tiles; DRAM-resident
-// scenes), not in the issue-bound batch kernel (12 loads per two levels instead of 8).
-template <int kS, typename StkT, bool kRobust, int kOct, bool kG>
-__device__ __forceinline__ bool trace_blk(const KParams& P, F3 o, F3 d, StkT stk, Hit& best, bool& overflow) {
-    const float tmin = 0.0f;
-    float tmax = FLT_MAX;                                           // ray.hpp:17-21
-    constexpr bool kU = CERES_RCP_UNIFORM == 1 || (CERES_RCP_UNIFORM == 2 && kOct == -2);
-    if (P.root_leaf_count) {                                          // root is a leaf: trace()'s own path
-        uint32_t a = 0, b = 0;
-        return trace<false, false, kS, StkT, kRobust, -1, kG>(P, o, d, stk, best, a, b, overflow);
-    }
-    const Slab<kRobust> sl = make_slab<kRobust>(o, d);
-    if constexpr (!kRobust && kOct == -1 && (CERES_OCTANT_SLAB & 1)) {
-        bool r = false;
-        if (with_uniform_octant(sl, [&](auto k) {
-                r = trace_blk<kS, StkT, kRobust, decltype(k)::value, kG>(P, o, d, stk, best, overflow);
-            }))
-            return r;
-    }
-    if (P.root_box_ok) {                                              // exact early miss (set_root_box)
-        float e, x;
-        slab_box<kRobust, kOct>(sl, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
-                                P.root_box[5], tmin, tmax, e, x);
-        if (!(e <= x)) return false;
-    }
-    uint32_t sp = 0;
-    best.slot = kNoSlot;
-    const float4* R = reinterpret_cast<const float4*>(P.blocks);      // 12 float4 per pair
-    CERES_COUNT_V(kFBvh2V, 192);
-    float4 A = R[0], B = R[1], C = R[2], A1 = R[4], B1 = R[5], C1 = R[6], A2 = R[8], B2 = R[9], C2 = R[10];
-    uint4 L = reinterpret_cast<const uint4*>(R)[3], L1 = reinterpret_cast<const uint4*>(R)[7];
-    uint4 L2 = reinterpret_cast<const uint4*>(R)[11];
-    auto leaves = [&](const uint4& W, bool hl, bool hr) {             // left leaf, then right leaf (:89-107)
-        const uint32_t nl = hl ? W.x : 0u, nr = hr ? W.z : 0u;
-        const uint32_t n_leaf = nl + nr, k2 = W.w - nl;
-        for (uint32_t j = 0; j < n_leaf; ++j) {
-            const uint32_t idx = (j < nl ? W.y : k2) + j;
-            float t, u, v;
-            const bool h = tri_test_u<kG, kU>(P.tris, idx, o, d, tmin, tmax, t, u, v);
-            best.slot = h ? idx : best.slot; best.t = h ? t : best.t;
-            best.u = h ? u : best.u; best.v = h ? v : best.v;
-            tmax = h ? t : tmax;
-        }
-    };
-    while (true) {                                                    // single_ray_traverser.hpp:82-123
-        // ---- the step at this record's pair
-        uint32_t top = stk[(sp ? sp - 1 : 0) * kS];
-        float le, lx, re, rx;
-        slab_box<kRobust, kOct>(sl, A.x, A.y, A.z, A.w, B.x, B.y, tmin, tmax, le, lx);
-        slab_box<kRobust, kOct>(sl, B.z, B.w, C.x, C.y, C.z, C.w, tmin, tmax, re, rx);
-        bool hit_l = le <= lx, hit_r = re <= rx;
-        bool go_l = hit_l && !L.x, go_r = hit_r && !L.z;
-        bool both = go_l && go_r, none = !go_l && !go_r;
-        bool swap = le > re;                                          // near first, ties left (:109-115)
-        bool done = none && sp == 0;                                  // :118-121
-        const bool right = both ? swap : !go_l;
-        uint32_t nxt = none ? top : (right ? L.w : L.y);
-        stk[sp * kS] = swap ? L.y : L.w;                              // the far child (kept only on a push)
-        sp = sp + (both ? 1u : 0u) - (none ? 1u : 0u);
-        const bool desc = !none;                                      // the near child's pair is in the record
-        const float4 cA = right ? A2 : A1, cB = right ? B2 : B1, cC = right ? C2 : C1;
-        const uint4 cL = right ? L2 : L1;
-        leaves(L, hit_l, hit_r);
-        // ---- the step at the near child (its pair from registers), in the same iteration
-        bool hl2 = false, hr2 = false;
-        if (desc) {
-            top = stk[(sp ? sp - 1 : 0) * kS];
-            slab_box<kRobust, kOct>(sl, cA.x, cA.y, cA.z, cA.w, cB.x, cB.y, tmin, tmax, le, lx);
-            slab_box<kRobust, kOct>(sl, cB.z, cB.w, cC.x, cC.y, cC.z, cC.w, tmin, tmax, re, rx);
-            hl2 = le <= lx; hr2 = re <= rx;
-            go_l = hl2 && !cL.x; go_r = hr2 && !cL.z;
-            both = go_l && go_r; none = !go_l && !go_r;
-            swap = le > re;
-            done = none && sp == 0;
-            nxt = none ? top : (both ? (swap ? cL.w : cL.y) : (go_l ? cL.y : cL.w));
-            stk[sp * kS] = swap ? cL.y : cL.w;
-            sp = sp + (both ? 1u : 0u) - (none ? 1u : 0u);
-        }
-        // ---- the next record (every lane that goes on: one fetch into the same registers)
-        if (!done) {
-            const float4* nq = R + 12 * size_t(nxt);
-            A = nq[0]; B = nq[1]; C = nq[2]; L = reinterpret_cast<const uint4*>(nq)[3];
-            A1 = nq[4]; B1 = nq[5]; C1 = nq[6]; L1 = reinterpret_cast<const uint4*>(nq)[7];
-            A2 = nq[8]; B2 = nq[9]; C2 = nq[10]; L2 = reinterpret_cast<const uint4*>(nq)[11];
-            CERES_COUNT_V(kFBvh2V, 192);
-        }
-        if (desc) leaves(cL, hl2, hr2);
-        if (done) break;
-    }
-    return best.slot != kNoSlot;
-}
-
 // trace() with a stack guard (round 6; CERES_STACK_GUARD: compiled into the
 // diagnostic build, libceres_hip_count.so).  Without the stats kernels' clamps
 // (CERES_TRUST_STACK_BOUND), a step writes the far child to slot sp, and with the exact bound
@@ -693,15 +587,13 @@ __device__ __forceinline__ bool trace_blk(const KParams& P, F3 o, F3 d, StkT stk
 // VGPRs, a wave per SIMD less; profiles/r06/ab_guard), so the product relies on the exact bound,
 // and bench.py checks every timed view with the stats kernels (clamps + flag) and with this
 // build's guard before it times them.
-template <bool kStats, int kS, typename StkT, bool kRobust, int kOct, bool kG, bool kBlk = false>
+template <bool kStats, int kS, typename StkT, bool kRobust, int kOct, bool kG>
 __device__ __forceinline__ bool guarded_trace(const KParams& P, F3 o, F3 d, StkT stk, Hit& best, uint32_t& n_pairs,
                                               uint32_t& n_tests, bool& overflow) {
     constexpr bool kGuard = !kStats && CERES_TRUST_STACK_BOUND && CERES_STACK_GUARD;
     const uint32_t slot = P.stack_entries * kS;
     if (kGuard) stk[slot] = stack_guard<StkT>();
-    bool hit;
-    if constexpr (kBlk && !kStats) hit = trace_blk<kS, StkT, kRobust, kOct, kG>(P, o, d, stk, best, overflow);
-    else hit = trace<false, kStats, kS, StkT, kRobust, kOct, kG>(P, o, d, stk, best, n_pairs, n_tests, overflow);
+    const bool hit = trace<false, kStats, kS, StkT, kRobust, kOct, kG>(P, o, d, stk, best, n_pairs, n_tests, overflow);
     if (kGuard) overflow |= uint32_t(stk[slot]) != stack_guard<StkT>();
     return hit;
 }
@@ -1161,6 +1053,21 @@ struct StealLdsT {
     uint32_t from[kS];               // donor lane, by thief rank
 };
 
+// Paired framebuffer stores of the batch kernel (round 6; CERES_PAIR_STORES).  A
+// wavefront of a batch takes consecutive tiles of the tile order, and consecutive tiles of the
+// Morton / row-run orders are horizontal neighbours (tiles 2k and 2k + 1 differ in the lowest x
+// bit), so each 8-pixel row of an even tile shares a 64-B sector with the next tile's row: floats
+// at 96 B per tile row (a pair of rows = 192 B = three whole sectors when the pair starts at an
+// even tile), RGB8 at 24 B.  Stored tile by tile, the shared sector arrives at the L2 as two
+// partial writes tens of microseconds apart and leaves it twice when the line is evicted in
+// between (DRAM writes 1.3x the framebuffers, round 5).  Here the even tile's pixels wait in LDS and
+// both tiles' stores issue back to back, so the two halves of a sector meet in the L2.
+struct PairStash {
+    float c[3][64];                  // colour of lane k's pixel of the even tile
+    uint32_t f[64], lr[64], i[64];   // its frame, local row, column; f = 0xffffffff: no pixel
+};
+struct NoStash {};
+
 // Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
 // intra-wavefront work stealing; on return L.blocked[tid] holds the lane's answer.  Must be
 // reached by all 64 lanes of the wavefront (it loops on wavefront ballots).
@@ -1379,7 +1286,7 @@ __device__ __forceinline__ void shade_pixel(const KParams& P, uint32_t f, uint32
 // launch: the shadow work of early tiles overlaps the primary work of later ones.
 constexpr int kFusedB = 64;      // single-wavefront workgroups (LDS is released per workgroup)
 constexpr size_t kLdsPerCu = 160 * 1024;   // LDS per CU (MI355X_MICROARCH.md)
-template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ, bool kG, int kTPWo = 0, bool kBlk = false>
+template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ, bool kG, int kTPWo = 0>
 __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     constexpr int kB = kFusedB;
     // kernels that trace shadow packets keep only the generic per-lane any-hit loop as fallback
@@ -1387,6 +1294,26 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ StealLdsT<kB> L;
     const uint32_t lane = threadIdx.x, tid = lane;
+    // paired stores (PairStash): batch kernels of 16-bit-stack scenes, whose LDS has room (2.8 KB of
+    // stacks per wavefront; the 24-bit-stack kernels are LDS-bound)
+    constexpr uint32_t kTPWp = (kStats || kSteal) ? 1 : kTPWo ? uint32_t(kTPWo) : uint32_t(CERES_TILES_PER_WAVE);
+    constexpr bool kPair = CERES_PAIR_STORES && !kStats && !kSteal && kTPWp >= 2 && std::is_same<StkT, uint16_t*>::value;
+    __shared__ typename std::conditional<kPair, PairStash, NoStash>::type S;
+    // a pixel's colour: stored now, or (the even tile of a pair) stashed for the odd tile's stores
+    auto emit = [&](uint32_t q, bool last, bool act, uint32_t f_, uint32_t lr_, uint32_t i_, float c0, float c1, float c2) {
+        if constexpr (kPair) {
+            if (!(q & 1u) && !last) {
+                S.c[0][lane] = c0; S.c[1][lane] = c1; S.c[2][lane] = c2;
+                S.f[lane] = act ? f_ : 0xffffffffu; S.lr[lane] = lr_; S.i[lane] = i_;
+                return;
+            }
+            if (q & 1u) {                                              // the even tile's pixels first
+                const uint32_t pf = S.f[lane];
+                if (pf != 0xffffffffu) store_pixel(P, pf, S.lr[lane], S.i[lane], S.c[0][lane], S.c[1][lane], S.c[2][lane]);
+            }
+        }
+        if (act) store_pixel(P, f_, lr_, i_, c0, c1, c2);
+    };
     // traversal stacks [entry][lane]: 16-, 24- or 32-bit entries, the narrowest every node index
     // of the scene fits (host choice)
     StkT stk;
@@ -1454,17 +1381,18 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     RayWork w{};
     uint64_t t_start = 0;
     if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
+    // the last tile of this wavefront (a stashed even tile with no odd partner is stored at once)
+    const bool last_q = q + 1 == kTPW || (kTPW > 1 && slot_q + 1 >= n_tiles);
     if (!kStats && P.cull && tile_misses_root(P, f, active, i, global_row(P, lr))) {
-        if (active) store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);        // render.hpp:116-117, every pixel a miss
+        emit(q, last_q, active, f, lr, i, 0.f, 0.f, 0.f);               // render.hpp:116-117, every pixel a miss
         continue;
     }
     if (active) {
         const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
         // kOct -1: the traversal dispatches on a wave-uniform octant; -2: generic loop only
         constexpr int kOctMode = (!kSteal || (CERES_OCTANT_SLAB & 4)) ? -1 : -2;
-        // (kBlk: the two-level block walk, trace_blk -- latency-bound one-frame launches)
-        hit = guarded_trace<kStats, kB, StkT, kRobust, kOctMode, kG, kBlk>(P, f3(P.cam[f].eye), view, stk, h, n_pairs,
-                                                                         n_tests, overflow);
+        hit = guarded_trace<kStats, kB, StkT, kRobust, kOctMode, kG>(P, f3(P.cam[f].eye), view, stk, h, n_pairs,
+                                                                   n_tests, overflow);
         if (P.rec_prim) {
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
             P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
@@ -1504,7 +1432,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
                                     P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
     float col[3] = {0.f, 0.f, 0.f};                                    // a miss: render.hpp:116-117
     if (hit) shade_pixel<kG>(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded, col);
-    if (active) store_pixel(P, f, lr, i, col[0], col[1], col[2]);
+    emit(q, last_q, active, f, lr, i, col[0], col[1], col[2]);
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
         // primary hits, wave primary pairs, wave shadow pairs
@@ -1643,7 +1571,7 @@ void ceres::scene_release(ceres_scene* s) {
     for (auto& o : s->orders) dfree(o.d);
     for (auto& d : s->retired) dfree(d);
     s->orders.clear(); s->retired.clear(); s->retired_bytes = 0;
-    dfree(s->d_pairs); dfree(s->d_blocks); dfree(s->d_nodes4); dfree(s->d_qnodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
+    dfree(s->d_pairs); dfree(s->d_nodes4); dfree(s->d_qnodes4); dfree(s->d_tris); dfree(s->d_orig); dfree(s->d_norms);
     dfree(s->d_shards); dfree(s->d_counters); dfree(s->d_wave_log); dfree(s->d_pixels); dfree(s->d_rgb8);
     for (auto e : s->ev_pool) (void)hipEventDestroy(e);
     for (auto e : s->ev_used) (void)hipEventDestroy(e);
@@ -2174,10 +2102,6 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
                 P.wave_log = s->d_wave_log;
                 s->last_grid_waves = waves;
             }
-            // the two-level BVH2 walk (trace_blk) for one-frame launches: their time is the slowest
-            // tiles' dependent fetch chains (CERES_BLK_WALK: 0 never)
-            const bool use_blk = CERES_BLK_WALK && steal && !stats && !robust && !qbvh && s->d_blocks;
-            P.blocks = s->d_blocks;
             // VGPR budgets: 16-bit-stack scenes (LDS for 7+ waves/SIMD) are compiled for 7 waves,
             // C5-size scenes keep the unconstrained allocation
             constexpr int w32 = CERES_FUSED_MINW32;
@@ -2189,14 +2113,6 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
                         if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, false, T, true, G>), fgrid, fblock, flds, stream, P);
                         else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, false, T, true, G>), fgrid, fblock, flds, stream, P);
                         else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, false, T, true, G>), fgrid, fblock, flds, stream, P);
-                        return;
-                    }
-                }
-                if constexpr (!R && T) {
-                    if (use_blk) {                                   // two-level BVH2 blocks (trace_blk)
-                        if (st16) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, CERES_BLK_MINW, false, true, false, G, 0, true>), fgrid, fblock, flds, stream, P);
-                        else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, false, true, false, G, 0, true>), fgrid, fblock, flds, stream, P);
-                        else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, false, true, false, G, 0, true>), fgrid, fblock, flds, stream, P);
                         return;
                     }
                 }
@@ -2338,8 +2254,7 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
     std::vector<Node4> nodes4;
     uint32_t stack4 = 0, not_collapsed = 0;
     if (!rlc && build_shadow_bvh4(pairs, nodes4, stack4, not_collapsed)) return nullptr;
-    std::vector<SiblingPair> blocks;
-    if (!rlc && build_pair_blocks(pairs, blocks)) return nullptr;
+
     // scenes whose nearest-first BVH4 stack costs waves (lds_limits_waves) get their inner
     // children ordered for the first-passing-child bound (order_shadow_bvh4; their single-frame
     // launches then walk in that order); the others keep the build order, which the nearest-first
@@ -2381,11 +2296,6 @@ ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* n
         HIP_TRY(hipMalloc(&s->d_shards, sizeof(Shard) * kShards));
         HIP_TRY(hipMalloc(&s->d_counters, 8 * sizeof(uint64_t)));
         HIP_TRY(hipMemcpy(s->d_pairs, pairs.data(), pairs.size() * sizeof(SiblingPair), hipMemcpyHostToDevice));
-        if (!blocks.empty()) {
-            HIP_TRY(hipMalloc(&s->d_blocks, blocks.size() * sizeof(SiblingPair)));
-            HIP_TRY(hipMemcpy(s->d_blocks, blocks.data(), blocks.size() * sizeof(SiblingPair), hipMemcpyHostToDevice));
-            s->n_slots = blocks.size();
-        }
         HIP_TRY(hipMemcpy(s->d_tris, leaf_tris.data(), n_tri * sizeof(Tri48), hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(s->d_orig, orig.data(), n_tri * sizeof(uint32_t), hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(s->d_norms, norm36, n_tri * 36, hipMemcpyHostToDevice));
@@ -2469,8 +2379,7 @@ int ceres_scene_info(const ceres_scene* s, uint32_t* depth, uint32_t* stack_entr
     if (stack_entries) *stack_entries = s->stack_entries;
     if (n_pairs) *n_pairs = s->n_pairs;
     if (device_bytes)
-        *device_bytes = (s->n_pairs + s->n_slots) * sizeof(SiblingPair) + s->n_nodes4 * sizeof(Node4) +
-                        s->n_tri * (sizeof(Tri48) + 4 + 36);
+        *device_bytes = s->n_pairs * sizeof(SiblingPair) + s->n_nodes4 * sizeof(Node4) + s->n_tri * (sizeof(Tri48) + 4 + 36);
     return CERES_OK;
 }
 

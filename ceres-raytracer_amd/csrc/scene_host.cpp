@@ -727,30 +727,6 @@ int order_shadow_bvh4(std::vector<Node4>& nodes, uint32_t& first_bound) {
 }
 
 
-// Two-level records of the BVH2 sibling pairs (round 6; the single-frame kernels' trace_blk,
-// render_hip.hip): record p (192 B, three 64-B slots) = pair p, then the pair of its left child and
-// the pair of its right child when those children are inner nodes (zero slots otherwise, never
-// read: the walk takes a child's pair only when it descends into that inner child).  Child words
-// keep their pair indices, which are also record indices, so one fetch of record p gives a walk the
-// reference's step at pair p and its step at the child it descends into.  Every pair is stored in
-// its own record and in its parent's (about 2.5x the pairs' bytes).
-int build_pair_blocks(const std::vector<SiblingPair>& pairs, std::vector<SiblingPair>& blocks) {
-    const size_t n = pairs.size();
-    blocks.assign(3 * n, SiblingPair{});
-    for (size_t p = 0; p < n; ++p) {
-        const SiblingPair& r = pairs[p];
-        blocks[3 * p] = r;
-        if (!r.lcount) {
-            if (r.lfirst >= n) return set_error(CERES_EINVAL, "build_pair_blocks: child pair %u out of range", r.lfirst);
-            blocks[3 * p + 1] = pairs[r.lfirst];
-        }
-        if (!r.rcount) {
-            if (r.rfirst >= n) return set_error(CERES_EINVAL, "build_pair_blocks: child pair %u out of range", r.rfirst);
-            blocks[3 * p + 2] = pairs[r.rfirst];
-        }
-    }
-    return CERES_OK;
-}
 
 }  // namespace ceres
 

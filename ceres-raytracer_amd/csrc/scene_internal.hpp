@@ -23,8 +23,6 @@ struct ceres_scene {
     uint32_t shadow_stack_first = 1;       // ... of first-passing-child walks (order_shadow_bvh4; <= the above)
     size_t n_nodes4 = 0;
     SiblingPair* d_pairs = nullptr;
-    SiblingPair* d_blocks = nullptr;       // two-level blocks of the pairs (build_pair_blocks; trace_blk), 4 slots each
-    size_t n_slots = 0;
     Node4* d_nodes4 = nullptr;
     ceres::QNode4* d_qnodes4 = nullptr;   // compressed shadow BVH4, built on first CERES_MODE_QBVH4 render
     // fused-kernel tile orders, one per (frame size, tiling, batch, tile), never rewritten or

@@ -43,6 +43,16 @@ if has abs; then
     step 600 ab_solo_$c python tools/ab.py $c ${ABS_ROUNDS:-15} $AB_LIBS
   done
 fi
+if has wr; then
+  # DRAM write bytes of one 16-frame batch launch per library ($WR_LIBS), rocprofv3 --pmc WRITE_SIZE
+  for lib in ${WR_LIBS:-ceres-raytracer_amd/libceres_hip.so}; do
+    t=$(basename $lib .so)
+    for c in ${WR_CFGS:-dragon_1080}; do
+      CERES_LIB=$lib step 240 wr_${c}_$t rocprofv3 --pmc WRITE_SIZE FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv \
+          -d $OUT/wr/${c}_$t -o run -- python3 tools/batch_launch.py $c fma 16 5
+    done
+  done
+fi
 if has sweep; then
   for c in ${SWEEP:-bunny_640 bunny_1080_primary bunny_1080 dragon_4096 proc_c5}; do
     step 600 bench_$c python bench.py --config $c ${SWEEP_ARGS:-}
