@@ -98,6 +98,12 @@
 #define CERES_RCP_UNIFORM 2                    // rcp_exact's IEEE-division fallback behind a wave-uniform branch
 #endif                                         // (ballot) instead of a divergent one: 0 nowhere, 1 in every
                                                // kernel, 2 in the single-frame kernel only
+#ifndef CERES_RCP_IFTHEN
+#define CERES_RCP_IFTHEN 1                     // rcp_exact (non-uniform form): fast quotient everywhere, division in an if-then
+#endif
+#ifndef CERES_PK_PACKET
+#define CERES_PK_PACKET 1                      // packet_any4: slab fmas two children at a time (v_pk_fma_f32)
+#endif
 #ifndef CERES_LOAD_ALWAYS
 #define CERES_LOAD_ALWAYS 1                    // trace(): finished lanes load a (cached) record too -- no branch
                                                // (batch kernel; A/B profiles/r04/s4 "ldall": batches -0.7..-1.5 %)
@@ -149,6 +155,14 @@ __device__ __forceinline__ float rcp_exact(float x) {
         }
         const float r0 = __builtin_amdgcn_rcpf(x);
         return __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+    }
+    if constexpr (CERES_RCP_IFTHEN) {
+        // the fast quotient in every lane, the division only in the (rare) lanes that need it: a
+        // one-sided branch (no else arm: two fewer exec-mask instructions per triangle test)
+        const float r0 = __builtin_amdgcn_rcpf(x);
+        float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+        if (__builtin_expect(m - 0x00800000u >= 0x7e000000u - 0x00800000u, 0)) r = 1.0f / x;
+        return r;
     }
     if (__builtin_expect(m - 0x00800000u >= 0x7e000000u - 0x00800000u, 0)) return 1.0f / x;
     const float r0 = __builtin_amdgcn_rcpf(x);
@@ -768,6 +782,9 @@ template <int kOct, bool kG>
 __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<false>& sl, F3 o, F3 d, uint64_t act,
                                                 uint32_t lane) {
     constexpr float tmin = 0.0f, tmax = FLT_MAX;
+    typedef float F2s __attribute__((ext_vector_type(2)));
+    const F2s IX2{sl.ix, sl.ix}, IY2{sl.iy, sl.iy}, IZ2{sl.iz, sl.iz};   // CERES_PK_PACKET splats
+    const F2s SX2{sl.sx, sl.sx}, SY2{sl.sy, sl.sy}, SZ2{sl.sz, sl.sz};
     uint64_t occ = 0, m = act;
     uint32_t cur = 0, sp = 0;
     int s_node = 0, s_lo = 0, s_hi = 0;                               // stack entry k in lane k
@@ -786,11 +803,37 @@ __device__ __forceinline__ uint64_t packet_any4(const KParams& P, const Slab<fal
         // inner or empty (node4_leaves_first).  An empty slot holds the inverted infinite box, which
         // the octant-selected slab test always fails (entry +inf, exit -inf), so no empty-slot test.
         uint64_t hm[4];
+        if constexpr (CERES_PK_PACKET) {
+            // the same fmas two children at a time (v_pk_fma_f32: children 0-1 and 2-3 of one bound row
+            // with the lane's splatted inverse direction / offset; each half is the scalar fma bit for bit)
+            typedef float F2v __attribute__((ext_vector_type(2)));
+            auto pk = [&](float a, float b, const F2v& i2, const F2v& s2) { return __builtin_elementwise_fma(F2v{a, b}, i2, s2); };
+            const F2v lx01 = pk(LX.x, LX.y, IX2, SX2), lx23 = pk(LX.z, LX.w, IX2, SX2);
+            const F2v hx01 = pk(HX.x, HX.y, IX2, SX2), hx23 = pk(HX.z, HX.w, IX2, SX2);
+            const F2v ly01 = pk(LY.x, LY.y, IY2, SY2), ly23 = pk(LY.z, LY.w, IY2, SY2);
+            const F2v hy01 = pk(HY.x, HY.y, IY2, SY2), hy23 = pk(HY.z, HY.w, IY2, SY2);
+            const F2v lz01 = pk(LZ.x, LZ.y, IZ2, SZ2), lz23 = pk(LZ.z, LZ.w, IZ2, SZ2);
+            const F2v hz01 = pk(HZ.x, HZ.y, IZ2, SZ2), hz23 = pk(HZ.z, HZ.w, IZ2, SZ2);
+            const float ax[4] = {lx01.x, lx01.y, lx23.x, lx23.y}, bx[4] = {hx01.x, hx01.y, hx23.x, hx23.y};
+            const float ay[4] = {ly01.x, ly01.y, ly23.x, ly23.y}, by[4] = {hy01.x, hy01.y, hy23.x, hy23.y};
+            const float az[4] = {lz01.x, lz01.y, lz23.x, lz23.y}, bz[4] = {hz01.x, hz01.y, hz23.x, hz23.y};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            float e, x;
-            slab_box<false, kOct>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e, x);
-            hm[c] = __ballot(e <= x) & m;
+            for (int c = 0; c < 4; ++c) {
+                // the octant picks each axis's entry / exit slab (slab_box<false, kOct>)
+                const float nx = (kOct & 1) ? bx[c] : ax[c], fx = (kOct & 1) ? ax[c] : bx[c];
+                const float ny = (kOct & 2) ? by[c] : ay[c], fy = (kOct & 2) ? ay[c] : by[c];
+                const float nz = (kOct & 4) ? bz[c] : az[c], fz = (kOct & 4) ? az[c] : bz[c];
+                const float e = fmaxf(nx, fmaxf(ny, fmaxf(nz, tmin)));
+                const float x = fminf(fx, fminf(fy, fminf(fz, tmax)));
+                hm[c] = __ballot(e <= x) & m;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float e, x;
+                slab_box<false, kOct>(sl, lx[c], hx[c], ly[c], hy[c], lz[c], hz[c], tmin, tmax, e, x);
+                hm[c] = __ballot(e <= x) & m;
+            }
         }
         // triangles of every passing leaf child, for the lanes that reach it and are not yet occluded
 #pragma unroll
@@ -1063,9 +1106,8 @@ struct StealLdsT {
 // between (DRAM writes 1.3x the framebuffers, round 5).  Here the even tile's pixels wait in LDS and
 // both tiles' stores issue back to back, so the two halves of a sector meet in the L2.
 struct PairStash {
-    float c[3][64];                  // colour of lane k's pixel of the even tile
-    uint32_t f[64], lr[64], i[64];   // its frame, local row, column; f = 0xffffffff: no pixel
-};
+    float c[3][64];                  // colour of lane k's pixel of the even tile (its position is
+};                                   // decoded again from the wavefront's tile-order entry)
 struct NoStash {};
 
 // Any-hit traversal of the wavefront's shadow rays (lane `tid` owns one ray when has_job) with
@@ -1299,17 +1341,39 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     constexpr uint32_t kTPWp = (kStats || kSteal) ? 1 : kTPWo ? uint32_t(kTPWo) : uint32_t(CERES_TILES_PER_WAVE);
     constexpr bool kPair = CERES_PAIR_STORES && !kStats && !kSteal && kTPWp >= 2 && std::is_same<StkT, uint16_t*>::value;
     __shared__ typename std::conditional<kPair, PairStash, NoStash>::type S;
-    // a pixel's colour: stored now, or (the even tile of a pair) stashed for the odd tile's stores
-    auto emit = [&](uint32_t q, bool last, bool act, uint32_t f_, uint32_t lr_, uint32_t i_, float c0, float c1, float c2) {
+    // this lane's pixel of tile-order entry t: frame, local row, column, and whether it exists
+    auto tile_pixel = [&](uint32_t t, uint32_t& f_, uint32_t& lr_, uint32_t& i_) {
+        uint32_t by_, bx_;
+        if (P.tile_packed) {                        // bit fields (pack_tile), wave-uniform
+            bx_ = t & ((1u << kTileXBits) - 1u);
+            by_ = (t >> kTileXBits) & ((1u << kTileYBits) - 1u);
+            f_ = t >> (kTileXBits + kTileYBits);
+        } else {
+            const uint32_t per_frame_ = P.tiles_x * P.row_blocks_per_frame;
+            f_ = t / per_frame_;
+            const uint32_t rem = t - f_ * per_frame_;
+            by_ = rem / P.tiles_x; bx_ = rem - by_ * P.tiles_x;
+        }
+        // lanes in Morton order over the tile: every quad of lanes (4k..4k+3) is a 2x2 pixel block,
+        // so the quads the texture addresser processes together hold neighbouring rays (A/B: solo
+        // C3 -2.4 %, C5 batches -1.5 %)
+        const uint32_t lx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4), ly = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
+        i_ = bx_ * 8u + lx;
+        lr_ = by_ * 8u + ly;
+        return i_ < P.W && lr_ < P.local_rows;
+    };
+    // a pixel's colour: stored now, or (the even tile of a pair) stashed for the odd tile's stores;
+    // t_prev: the even tile's order entry (its pixel positions are decoded again, not stashed)
+    auto emit = [&](uint32_t q, bool last, uint32_t t_prev, bool act, uint32_t f_, uint32_t lr_, uint32_t i_, float c0, float c1,
+                    float c2) {
         if constexpr (kPair) {
             if (!(q & 1u) && !last) {
                 S.c[0][lane] = c0; S.c[1][lane] = c1; S.c[2][lane] = c2;
-                S.f[lane] = act ? f_ : 0xffffffffu; S.lr[lane] = lr_; S.i[lane] = i_;
                 return;
             }
             if (q & 1u) {                                              // the even tile's pixels first
-                const uint32_t pf = S.f[lane];
-                if (pf != 0xffffffffu) store_pixel(P, pf, S.lr[lane], S.i[lane], S.c[0][lane], S.c[1][lane], S.c[2][lane]);
+                uint32_t pf, plr, pi;
+                if (tile_pixel(t_prev, pf, plr, pi)) store_pixel(P, pf, plr, pi, S.c[0][lane], S.c[1][lane], S.c[2][lane]);
             }
         }
         if (act) store_pixel(P, f_, lr_, i_, c0, c1, c2);
@@ -1358,23 +1422,12 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     const uint4 tq = q < 4 ? tiles4 : tiles4b;
     const uint32_t qq = q & 3;
     const uint32_t t = kTPW == 1 ? tiles4.x : qq == 0 ? tq.x : qq == 1 ? tq.y : qq == 2 ? tq.z : tq.w;
-    uint32_t f, by, bx;
-    if (P.tile_packed) {                        // bit fields (pack_tile), wave-uniform
-        bx = t & ((1u << kTileXBits) - 1u);
-        by = (t >> kTileXBits) & ((1u << kTileYBits) - 1u);
-        f = t >> (kTileXBits + kTileYBits);
-    } else {
-        f = t / per_frame;
-        const uint32_t rem = t - f * per_frame;
-        by = rem / P.tiles_x; bx = rem - by * P.tiles_x;
-    }
-    // lanes in Morton order over the tile: every quad of lanes (4k..4k+3) is a 2x2 pixel block,
-    // so the quads the texture addresser processes together hold neighbouring rays (A/B: solo
-    // C3 -2.4 %, C5 batches -1.5 %)
-    const uint32_t lx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4), ly = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
-    const uint32_t i = bx * kTile + lx;
-    const uint32_t lr = by * kTile + ly;
-    const bool active = i < P.W && lr < P.local_rows;
+    // the previous entry (paired stores: the even tile of this odd one)
+    const uint32_t qp = (q - 1) & 3;
+    const uint4 tp = q - 1 < 4 ? tiles4 : tiles4b;
+    const uint32_t t_prev = qp == 0 ? tp.x : qp == 1 ? tp.y : qp == 2 ? tp.z : tp.w;
+    uint32_t f, lr, i;
+    const bool active = tile_pixel(t, f, lr, i);
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;
     bool hit = false;
     Hit h{0, 0.f, 0.f, 0.f};
@@ -1384,7 +1437,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     // the last tile of this wavefront (a stashed even tile with no odd partner is stored at once)
     const bool last_q = q + 1 == kTPW || (kTPW > 1 && slot_q + 1 >= n_tiles);
     if (!kStats && P.cull && tile_misses_root(P, f, active, i, global_row(P, lr))) {
-        emit(q, last_q, active, f, lr, i, 0.f, 0.f, 0.f);               // render.hpp:116-117, every pixel a miss
+        emit(q, last_q, t_prev, active, f, lr, i, 0.f, 0.f, 0.f);       // render.hpp:116-117, every pixel a miss
         continue;
     }
     if (active) {
@@ -1432,7 +1485,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
                                     P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
     float col[3] = {0.f, 0.f, 0.f};                                    // a miss: render.hpp:116-117
     if (hit) shade_pixel<kG>(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded, col);
-    emit(q, last_q, active, f, lr, i, col[0], col[1], col[2]);
+    emit(q, last_q, t_prev, active, f, lr, i, col[0], col[1], col[2]);
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
         // primary hits, wave primary pairs, wave shadow pairs

@@ -48,7 +48,7 @@ if has wr; then
   for lib in ${WR_LIBS:-ceres-raytracer_amd/libceres_hip.so}; do
     t=$(basename $lib .so)
     for c in ${WR_CFGS:-dragon_1080}; do
-      CERES_LIB=$lib step 240 wr_${c}_$t rocprofv3 --pmc WRITE_SIZE FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv \
+      CERES_LIB=$lib step 240 wr_${c}_$t rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv \
           -d $OUT/wr/${c}_$t -o run -- python3 tools/batch_launch.py $c fma 16 5
     done
   done
