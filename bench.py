@@ -627,7 +627,10 @@ def main():
     ap.add_argument("--views", choices=("config", "orbit"), default="config",
                     help="config: every frame of the step is the config's own view (C3 = static.cpp's camera, "
                          "the headline); orbit: frame f = the anim.cpp orbit view f x 360/F degrees about z")
-    ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--row-block", type=int, default=16,
+                    help="rows per block of the row-interleaved partitions (round 6: 16, was 8 -- the one-GPU "
+                         "rehearsal at N = 8 predicts 0.919 render-only weak efficiency for C3 against 0.875 with "
+                         "8-row blocks, C4 0.920 against 0.897; profiles/r06/rehearsal)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-count", action="store_true",

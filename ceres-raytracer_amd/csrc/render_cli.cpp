@@ -63,7 +63,7 @@ struct Opts {
     Num<double> d;
     int rot_axis = -1;
     size_t W = 1920, H = 1080;
-    int mode = CERES_MODE_FULL, proc = 0, device = 0, bench = 0, gpus = 1, row_block = 8;
+    int mode = CERES_MODE_FULL, proc = 0, device = 0, bench = 0, gpus = 1, row_block = 16;
     bool json = false, gpu_bvh = false, f64 = false;
     int arith = CERES_ARITH_FMA;                   // --fma (default) / --exact
     int orbit_count = 0, frames = 1;

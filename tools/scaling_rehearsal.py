@@ -46,7 +46,7 @@ def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "dragon_1080"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     k = int(sys.argv[3]) if len(sys.argv) > 3 else 16
-    rb = int(sys.argv[4]) if len(sys.argv) > 4 else 8            # bench.py --row-block
+    rb = int(sys.argv[4]) if len(sys.argv) > 4 else 16           # bench.py --row-block (round 6: 16)
     cfg = pkg.configs.CONFIGS[name]
     meta = load_golden(name)
     W, H = cfg["W"], cfg["H"]
