@@ -1044,8 +1044,9 @@ def main():
     # the 16-frame launch `roofline` prices (the step IS such launches: 16 copies of the config view)
     step_pmc = None
     launches_step = None
-    if full_mode and world == 1 and F % 16 == 0:
-        step_pmc = pmc_entry(args.config, f"ceres_fused_batch16{'' if views_kind == 'config' else '_orbit'}_{args.arith}")
+    if world == 1 and F % 16 == 0:
+        kstep = "ceres_fused" if full_mode else "ceres_primary"
+        step_pmc = pmc_entry(args.config, f"{kstep}_batch16{'' if views_kind == 'config' else '_orbit'}_{args.arith}")
         launches_step = F // 16
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, cfg, meta[build]["rays"] if meta else rays_step // F, build=build)

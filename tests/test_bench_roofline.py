@@ -176,8 +176,9 @@ def _check_trace_agreement(name, line):
     rf = line["roofline"]
     cfg = line["config"]["workload"].split(":")[0]
     # the trace kept in the same directory as the bench line (one session, one build)
-    for p in glob.glob(os.path.join(REPO, "profiles", os.path.dirname(name),
-                                    f"trace_batch_{cfg}_{line['arith']}_kernel_stats.csv")):
+    d = os.path.join(REPO, "profiles", os.path.dirname(name))
+    for p in (glob.glob(os.path.join(d, f"trace_batch_{cfg}_{line['arith']}_kernel_stats.csv")) +
+              glob.glob(os.path.join(d, f"trace_{cfg}_batch16_{line['arith']}_kernel_stats.csv"))):   # round 6 naming
         with open(p) as f:
             rows = [r for r in csv.DictReader(f) if rf["kernel"] + "<" in r["Name"]]
         assert rows, p
@@ -223,8 +224,11 @@ def _check_step_r06(bench, name, line):
     for at most the step's wall time."""
     rs = line["roofline_step"]
     cfg = line["config"]["workload"].split(":")[0]
-    pmc = _session_pmc(name, cfg, f"ceres_fused_batch16_{line['arith']}") or \
-        bench.pmc_entry(cfg, f"ceres_fused_batch16_{line['arith']}")
+    kern = (line.get("roofline") or {}).get("kernel", "ceres_fused")
+    key = f"{kern}_batch16_{line['arith']}"
+    pmc = _session_pmc(name, cfg, key) or bench.pmc_entry(cfg, key)
+    if rs["bound"] == "unmeasured":
+        pmc = None                                      # (round-6 lines before the primary-only step fix)
     again = bench.roofline_step_block(rs["algorithmic_bytes_per_step"], line["ms_per_step"], line["n_gpus"], pmc,
                                       rs.get("launches_per_step"), None)
     assert again["bound"] == rs["bound"], name
