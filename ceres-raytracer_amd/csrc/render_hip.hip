@@ -1633,6 +1633,8 @@ void ceres::scene_release(ceres_scene* s) {
     s->band_events.clear();
     dfree(s->d_band_counters);
     dfree(s->d_lit); dfree(s->d_lit_count);
+    if (s->h_lit_pinned) (void)hipHostFree(s->h_lit_pinned);
+    s->h_lit_pinned = nullptr;
     if (s->h_small) (void)hipHostFree(s->h_small);
     s->h_small = nullptr;
     if (s->ev_count) (void)hipEventDestroy(s->ev_count);
@@ -2531,13 +2533,21 @@ static int render_f32_compact(ceres_scene* s, const float basis12[12], const flo
                               uint8_t* rgb8, size_t W, size_t H, ceres_stats* stats) {
     const size_t np = W * H;
     // records for at most kCompactMaxLitFrac of the pixels (a full-frame record buffer
-    // was 1.33x the float framebuffer); a denser frame overflows it and takes the full copy
+    // was 1.33x the float framebuffer); a denser frame overflows it and takes the full copy.
+    // Round 6: the records go straight into pinned host memory (the compaction kernel's stores
+    // cross the host link as it runs: no separate copy, one synchronisation per call instead of
+    // two); CERES_COMPACT_ZC=0 keeps the device buffer + copy.
+    static const bool zc = [] { const char* e = std::getenv("CERES_COMPACT_ZC"); return !(e && e[0] == '0'); }();
     const size_t cap = size_t(double(np) * kCompactMaxLitFrac) + 1;
-    if (s->lit_cap < cap) {
+    if (s->lit_cap < cap || s->lit_zc != zc) {
         dfree(s->d_lit);
-        HIP_TRY(hipMalloc(&s->d_lit, cap * sizeof(uint4)));
+        if (s->h_lit_pinned) { (void)hipHostFree(s->h_lit_pinned); s->h_lit_pinned = nullptr; }
+        if (zc) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_lit_pinned), cap * sizeof(uint4)));
+        else HIP_TRY(hipMalloc(&s->d_lit, cap * sizeof(uint4)));
         s->lit_cap = cap;
+        s->lit_zc = zc;
     }
+    uint4* lit_out = zc ? s->h_lit_pinned : s->d_lit;
     if (!s->d_lit_count) HIP_TRY(hipMalloc(&s->d_lit_count, sizeof(uint32_t)));
     if (!s->h_small) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_small), 16 * sizeof(uint64_t)));
     if (!s->ev_count) HIP_TRY(hipEventCreateWithFlags(&s->ev_count, hipEventDisableTiming));
@@ -2555,7 +2565,7 @@ static int render_f32_compact(ceres_scene* s, const float basis12[12], const flo
         return rc;
     HIP_TRY(hipEventRecord(b, s->stream));
     hipLaunchKernelGGL(dev::ceres_compact_lit, dim3(uint32_t((np + 255) / 256)), dim3(256), 0, s->stream, s->d_pixels,
-                       uint32_t(np), s->d_lit, s->d_lit_count, uint32_t(cap));
+                       uint32_t(np), lit_out, s->d_lit_count, uint32_t(cap));
     HIP_TRY(hipGetLastError());
     uint64_t* hs = reinterpret_cast<uint64_t*>(s->h_small);
     HIP_TRY(hipMemcpyAsync(hs + 8, s->d_band_counters, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, s->stream));
@@ -2568,13 +2578,14 @@ static int render_f32_compact(ceres_scene* s, const float basis12[12], const flo
     const bool dense = n > cap;                                      // records overflowed: the full copy
     if (dense)
         HIP_TRY(hipMemcpyAsync(pixels, s->d_pixels, 3 * np * sizeof(float), hipMemcpyDeviceToHost, s->stream));
-    else if (n) {
+    else if (n && !zc) {
         if (s->h_lit.size() < n) s->h_lit.resize(n);
         HIP_TRY(hipMemcpyAsync(s->h_lit.data(), s->d_lit, n * sizeof(uint4), hipMemcpyDeviceToHost, s->stream));
     }
     if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, s->d_rgb8, 3 * np, hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
-    if (!dense) host_scatter_lit(pixels, reinterpret_cast<const uint32_t*>(s->h_lit.data()), n);
+    if (dense || (n && !zc) || rgb8) HIP_TRY(hipStreamSynchronize(s->stream));
+    if (!dense)                                                       // (zero-copy: complete at ev_count)
+        host_scatter_lit(pixels, reinterpret_cast<const uint32_t*>(zc ? s->h_lit_pinned : s->h_lit.data()), n);
     s->last_lit_frac = double(n) / double(np);
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, a, b));

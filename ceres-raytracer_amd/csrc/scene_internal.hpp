@@ -67,6 +67,8 @@ struct ceres_scene {
     size_t lit_cap = 0;
     uint32_t* h_small = nullptr;       // pinned: lit count + 8 counters
     std::vector<uint4> h_lit;
+    uint4* h_lit_pinned = nullptr;     // zero-copy records (pinned host memory the compaction kernel writes)
+    bool lit_zc = false;
     double last_lit_frac = 0.0;        // the previous call's lit fraction (dense frames take the full copy)
     uint32_t dense_calls = 0;
     hipEvent_t ev_count = nullptr;
