@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_scene_shadow_stacks", "ceres_render_f32",
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_multi_f32", "ceres_device_count", "ceres_assemble_rgb8_packed", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_fetch_counters",
+    "ceres_cpu_scene_create", "ceres_cpu_scene_destroy", "ceres_render_cpu_f32",
     "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
     "ceres_obj_load_arith", "ceres_proc_mesh_arith", "ceres_rotate_triangles_arith", "ceres_bvh_build_arith",
@@ -183,6 +184,12 @@ def lib():
                                           _u64p]
     L.ceres_scene_wave_log.argtypes = [_vp, _u64p, _sz, ctypes.POINTER(_sz)]
     L.ceres_fetch_counters.argtypes = [ctypes.c_int, _u64p, ctypes.c_int]
+    L.ceres_cpu_scene_create.argtypes = [_fp, _sz, _fp, _vp, _sz, _u64p]
+    L.ceres_cpu_scene_create.restype = _vp
+    L.ceres_cpu_scene_destroy.argtypes = [_vp]
+    L.ceres_cpu_scene_destroy.restype = None
+    L.ceres_render_cpu_f32.argtypes = [_vp, _fp, _fp, ctypes.c_int, _fp, ctypes.POINTER(ctypes.c_uint8), _sz, _sz,
+                                       ctypes.POINTER(_Stats), ctypes.c_int]
     L.ceres_content_hash.argtypes = [_vp, _sz]
     L.ceres_content_hash.restype = ctypes.c_uint64
     L.ceres_obj_load_arith.argtypes = L.ceres_obj_load.argtypes + [ctypes.c_int]
@@ -366,6 +373,44 @@ def build_bvh_device(d_tri48, n_tri, d_nodes32, d_prim32, stream=0, arith=ARITH_
     _check(lib().ceres_bvh_build_device_arith(d_tri48, n_tri, d_nodes32, d_prim32, ctypes.byref(m), stream or None,
                                               int(arith)))
     return m.value
+
+
+class CpuScene:
+    """The CPU path's scene (ceres_cpu_scene_create): render<float>() on host cores, chosen
+    explicitly (./render --cpu); the GPU classes never fall back to it."""
+
+    def __init__(self, mesh, bvh):
+        if mesh.f64:
+            raise CeresError("CpuScene: single-precision scenes only")
+        L = lib()
+        self._h = L.ceres_cpu_scene_create(_p(mesh.tri, ctypes.c_float), len(mesh), _p(mesh.norm, ctypes.c_float),
+                                           bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0], _p(bvh.prim, ctypes.c_uint64))
+        if not self._h:
+            raise CeresError("ceres_cpu_scene_create: " + L.ceres_last_error().decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ceres_cpu_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render(self, basis12, sun, W, H, mode=MODE_FULL, threads=0, want_pixels=True, want_rgb8=True):
+        """ceres_render_cpu_f32: (pixels [H*W*3] f32 | None, rgb8 | None, stats dict)."""
+        b = np.ascontiguousarray(basis12, np.float32)
+        s = np.ascontiguousarray(sun, np.float32)
+        px = np.empty(3 * W * H, np.float32) if want_pixels else None
+        rgb = np.empty(3 * W * H, np.uint8) if want_rgb8 else None
+        st = _Stats()
+        _check(lib().ceres_render_cpu_f32(self._h, _p(b, ctypes.c_float), _p(s, ctypes.c_float), int(mode),
+                                          _p(px, ctypes.c_float), _p(rgb, ctypes.c_uint8), W, H, ctypes.byref(st),
+                                          int(threads)))
+        return px, rgb, dict(rays=st.rays, hits=st.hits, primary_rays=st.primary_rays, shadow_rays=st.shadow_rays,
+                             node_pairs=st.node_pairs, tri_tests=st.tri_tests, ms=st.ms)
 
 
 class Scene:

@@ -9,7 +9,7 @@
 //                [--rotate x|y|z deg] [--size W H] [-o|--out file.ppm] [--primary-only]
 //                [--proc N] [--device D] [--bench reps] [--json]
 //                [--orbit ax ay az step_deg count] [--frames N] [--gpu-bvh] [--double|-d]
-//                [--gpus N] [--row-block R] [--robust] [--qbvh] [--exact | --fma]
+//                [--gpus N] [--row-block R] [--robust] [--qbvh] [--exact | --fma] [--cpu [--threads T]]
 //
 // Arithmetic (float and double pipelines): --fma (the default) computes every step as the reference's own
 // CMake build does (CMakeLists.txt:11-13, g++ -O3 -mavx2 -mfma: GCC contracts a*b+c into FMA at
@@ -35,8 +35,12 @@
 // the first frame, and once more per further frame; N frames are written as
 // <out-stem>_000.ppm ... (one file when N = 1), "Total Rays" summed like anim.cpp:127.
 //
+// --cpu renders on the host cores instead (ceres_render_cpu_f32: the product's CPU path, the same
+// images, rays and hits; float pipeline, one process; --threads T, default the OpenMP default) --
+// SURVEY.md §7 step 3's "config 1 works with no GPU".  It is only ever chosen by the flag:
+//
 // Exit status: 0 on success, 1 on a load/render error (message on stderr), 2 on bad usage.
-// There is no CPU fallback: without a gfx950 device the render step fails.
+// There is no CPU fallback: without --cpu and without a gfx950 device the render step fails.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -45,6 +49,7 @@
 #include <vector>
 #include <algorithm>
 #include <cctype>
+#include <type_traits>
 
 #include "ceres_render.h"
 
@@ -67,6 +72,8 @@ struct Opts {
     bool json = false, gpu_bvh = false, f64 = false;
     int arith = CERES_ARITH_FMA;                   // --fma (default) / --exact
     int orbit_count = 0, frames = 1;
+    bool cpu = false;                              // --cpu: ceres_render_cpu_f32 on the host cores
+    int threads = 0;                               // --threads (0: the OpenMP default)
 };
 
 int usage() {
@@ -74,7 +81,8 @@ int usage() {
                  "usage: render <obj> [--eye x y z] [--dir x y z] [--up x y z] [--fov deg] [--sun x y z]\n"
                  "              [--rotate x|y|z deg] [--size W H] [-o out.ppm] [--primary-only] [--proc N]\n"
                  "              [--device D] [--bench reps] [--json] [--orbit ax ay az step_deg count] [--frames N]\n"
-                 "              [--gpu-bvh] [--double] [--gpus N] [--row-block R] [--robust] [--qbvh] [--exact|--fma]\n");
+                 "              [--gpu-bvh] [--double] [--gpus N] [--row-block R] [--robust] [--qbvh] [--exact|--fma]\n"
+                 "              [--cpu [--threads T]]\n");
     return 2;
 }
 
@@ -122,6 +130,8 @@ bool parse(int argc, char** argv, Opts& o) {
         else if (a == "--row-block") { if (!have(1)) return false; o.row_block = std::atoi(argv[++i]); if (o.row_block < 1) return false; }
         else if (a == "--bench") { if (!have(1)) return false; o.bench = std::atoi(argv[++i]); }
         else if (a == "--json") o.json = true;
+        else if (a == "--cpu") o.cpu = true;
+        else if (a == "--threads") { if (!have(1)) return false; o.threads = std::atoi(argv[++i]); if (o.threads < 0) return false; }
         else if (a == "--gpu-bvh") o.gpu_bvh = true;
         else if (a == "--double" || a == "-d") o.f64 = true;                   // anim.cpp:146-147
         else if (a == "--orbit") {
@@ -191,6 +201,9 @@ template <> struct Api<double> {
 
 double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
+template <class S, class Render>
+int frames_loop(const Opts& o, const Num<S>& v, Render&& render, const char* where);
+
 template <class S>
 int run(const Opts& o, const Num<S>& v) {
     using A = Api<S>;
@@ -208,6 +221,18 @@ int run(const Opts& o, const Num<S>& v) {
     std::printf("%g\n", now_s() - t0);
     std::printf("BVH of %zu node(s) and %zu reference(s)\n", n_nodes, n_tri);
 
+    if constexpr (std::is_same<S, float>::value) {
+        if (o.cpu) {
+            ceres_cpu_scene* cs = ceres_cpu_scene_create(tri, n_tri, norm, nodes, n_nodes, prim);
+            ceres_free(nodes); ceres_free(prim); ceres_free(tri); ceres_free(norm);
+            if (!cs) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
+            const int rc = frames_loop(o, v, [&](const S* basis, const S* sun, uint8_t* rgb, ceres_stats* st) {
+                return ceres_render_cpu_f32(cs, basis, sun, o.mode, nullptr, rgb, o.W, o.H, st, o.threads);
+            }, "CPU");
+            ceres_cpu_scene_destroy(cs);
+            return rc;
+        }
+    }
     ceres_scene* scene = A::scene(tri, n_tri, norm, nodes, n_nodes, prim, o.device);
     // --gpus N: one scene copy per further rank, on the next devices (mod the device count)
     std::vector<ceres_scene*> ranks(1, scene);
@@ -231,12 +256,22 @@ int run(const Opts& o, const Num<S>& v) {
                                             o.W, o.H, st)
                           : A::render(scene, basis, sun, o.mode, rgb, o.W, o.H, st);
     };
+    const int rc = frames_loop(o, v, render, "HIP");
+    destroy();
+    return rc;
+}
+
+// The frame loop of static.cpp / anim.cpp (render :130 / :104-110, PPM :135-147, "Total Rays"
+// anim.cpp:127) over `render`; `where` names the render path in the progress lines.
+template <class S, class Render>
+int frames_loop(const Opts& o, const Num<S>& v, Render&& render, const char* where) {
+    using A = Api<S>;
 
     // frame poses: count + k orbit rotations for frame k (count = 0, frames = 1: the plain camera)
     const uint32_t n_pose = uint32_t(o.orbit_count + o.frames);
     std::vector<S> bases(12 * size_t(n_pose)), suns(3 * size_t(n_pose));
     if (A::orbit(v, o.W, o.H, n_pose, bases.data(), suns.data(), o.arith) != CERES_OK) {
-        std::fprintf(stderr, "error: %s\n", ceres_last_error()); destroy(); return 1;
+        std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1;
     }
     std::vector<uint8_t> rgb(3 * o.W * o.H);
     ceres_stats st{};
@@ -245,12 +280,14 @@ int run(const Opts& o, const Num<S>& v) {
     for (int k = 0; k < o.frames; ++k) {
         const S* basis = bases.data() + 12 * size_t(o.orbit_count + k);
         const S* sun = suns.data() + 3 * size_t(o.orbit_count + k);
-        if (o.gpus > 1) std::printf("Rendering image %d (%zux%zu) on %d HIP ranks from device %d...\n", k, o.W, o.H, o.gpus, o.device);
-        else std::printf("Rendering image %d (%zux%zu) on HIP device %d...\n", k, o.W, o.H, o.device);
+        if (o.cpu) std::printf("Rendering image %d (%zux%zu) on the %s%s...\n", k, o.W, o.H, where,
+                               o.threads ? (" with " + std::to_string(o.threads) + " threads").c_str() : "");
+        else if (o.gpus > 1) std::printf("Rendering image %d (%zux%zu) on %d %s ranks from device %d...\n", k, o.W, o.H, o.gpus, where, o.device);
+        else std::printf("Rendering image %d (%zux%zu) on %s device %d...\n", k, o.W, o.H, where, o.device);
         const double t1 = now_s();
         int rc = render(basis, sun, rgb.data(), &st);
         const double t2 = now_s();
-        if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); destroy(); return 1; }
+        if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
         std::printf("%g\n", t2 - t1);
         std::printf("Rays: %llu\tHits: %llu\n", (unsigned long long)st.rays, (unsigned long long)st.hits);   // anim.cpp:109
         tot_rays += st.rays;
@@ -259,7 +296,7 @@ int run(const Opts& o, const Num<S>& v) {
             const double b1 = now_s();
             rc = render(basis, sun, rgb.data(), &s2);
             e2e.push_back((now_s() - b1) * 1e3);          // the whole call: launch + kernel + RGB8 copy to the host
-            if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); destroy(); return 1; }
+            if (rc != CERES_OK) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
             ms.push_back(s2.ms);
         }
         std::string path = o.out;
@@ -277,7 +314,6 @@ int run(const Opts& o, const Num<S>& v) {
             std::fclose(f);
         } else {
             std::fprintf(stderr, "error: cannot write %s\n", path.c_str());
-            destroy();
             return 1;
         }
     }
@@ -291,7 +327,10 @@ int run(const Opts& o, const Num<S>& v) {
                     (unsigned long long)st.rays, (unsigned long long)st.hits, o.W, o.H, st.ms, med,
                     med > 0 ? double(st.rays) / (med * 1e3) : 0.0, e2e_med);
     }
-    destroy();
+    if (o.json && o.cpu)                                              // the reference's Statistics, all rays
+        std::printf("{\"node_pairs\": %llu, \"tri_tests\": %llu, \"primary_rays\": %llu, \"shadow_rays\": %llu}\n",
+                    (unsigned long long)st.node_pairs, (unsigned long long)st.tri_tests,
+                    (unsigned long long)st.primary_rays, (unsigned long long)st.shadow_rays);
     return 0;
 }
 
@@ -301,5 +340,9 @@ int main(int argc, char** argv) {
     Opts o;
     if (!parse(argc, argv, o)) return usage();
     if (o.arith == CERES_ARITH_FMA) o.mode |= CERES_MODE_FMA;
+    if (o.cpu && (o.f64 || o.gpus > 1 || o.gpu_bvh || (o.mode & CERES_MODE_QBVH4))) {
+        std::fprintf(stderr, "error: --cpu renders the float pipeline in one process (not with --double, --gpus, --gpu-bvh, --qbvh)\n");
+        return 2;
+    }
     return o.f64 ? run<double>(o, o.d) : run<float>(o, o.f);
 }

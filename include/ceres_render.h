@@ -332,6 +332,24 @@ int ceres_scene_wave_log(ceres_scene* scene, uint64_t* out, size_t max_waves, si
  * Statistics (single_ray_traverser.hpp:132-135). */
 int ceres_fetch_counters(int device, uint64_t out[8], int reset);
 
+/* ---- the CPU path (./render --cpu) ----
+ * render<float>() on host cores, chosen explicitly -- no call falls back to it.  The scene is the
+ * product's layout built on the host (sibling-pair records, leaf-ordered triangles) from the same
+ * arrays ceres_scene_create takes; the render walks it in the reference's order
+ * (single_ray_traverser.hpp:68-126, shadow rays traced closest-hit like render.hpp:135-136) with
+ * the arithmetic of the gfx950 kernels, so images, rays and hits equal the reference's in both
+ * arithmetics (CERES_MODE_FMA or not), with CERES_MODE_ROBUST / CERES_MODE_PRIMARY as on the GPU
+ * (CERES_MODE_QBVH4: CERES_EUNSUPPORTED).  pixels (3*W*H floats, render.hpp:107 layout) and/or rgb8
+ * (the PPM body) may be NULL; stats->node_pairs / tri_tests are the reference's Statistics
+ * (single_ray_traverser.hpp:132-135) over all rays, stats->ms the wall time.  threads <= 0: the
+ * OpenMP default.  Replaces render<float>() (render.hpp:86-156) for a caller without a GPU. */
+typedef struct ceres_cpu_scene ceres_cpu_scene;
+ceres_cpu_scene* ceres_cpu_scene_create(const float* tri48, size_t n_tri, const float* norm36, const void* nodes32,
+                                        size_t n_nodes, const uint64_t* prim64);
+void ceres_cpu_scene_destroy(ceres_cpu_scene* scene);
+int ceres_render_cpu_f32(const ceres_cpu_scene* scene, const float basis12[12], const float sun[3], int mode,
+                         float* pixels, uint8_t* rgb8, size_t width, size_t height, ceres_stats* stats, int threads);
+
 /* 64-bit content hash of a byte range (multithreaded; deterministic for a given byte string) --
  * what the drop-in include/ceres/render.hpp uses to honour render.hpp:86-156's per-call reading
  * of the caller's triangles / tri_norms / BVH while uploading a scene only when they change. */
