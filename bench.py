@@ -57,7 +57,7 @@ Also reported (rank 0):
                 --streams streams, so this is a throughput, not a launch duration).
   roofline_solo one whole frame of frame 0's view per launch (the latency regime), as `roofline`.
   orbit         the same timed loop over the orbit views (`orbit_value`), value + shadow-ray fraction.
-  partition_alt N > 1: the same step under the other partition (frames <-> exchange).
+  partition_alt N > 1: the same step under the other partition (frames <-> bands).
   cpu_baseline  the REFERENCE hot path (oracle/_ref/ref_render, reference CMake flags) timed
                 on this host's cores on a bounded sample of the same workload (N = 1 only);
                 falls back to the oracle restatement if the reference binary is absent.
@@ -535,24 +535,25 @@ def choose_collect(requested, cfg, world, frames):
     units -- each rank renders its 16 frames whole with no data-path collective ("frames"; render.hpp
     :104-153 touches one frame, pixels are independent) -- except for the configs BASELINE.json
     defines as ONE framebuffer tiled across the GPUs (configs.py "tiled": C4, C5) at N >= 4, whose
-    frames' rows are dealt over the ranks and gathered to their owners with one RCCL all-to-all per
-    step ("exchange", the north star's framebuffer partition).  At N = 2 those take "frames" too:
-    the single xGMI link would carry 16 split frames' rows per step and outlast the render (C4
-    1.23x).  The other partition is timed in the same run and reported beside it (alt_collect):
-    round 5's one-GPU rehearsal predicts C3 at N = 8 at 0.995 weak efficiency with frames and 0.71-0.86
-    with the exchange (tools/scaling_rehearsal.py, profiles/r05/s36).  Partitions that deal whole
-    frames need F to be a multiple of N, else every frame goes to rank 0 ("gather")."""
+    frames are cut into contiguous bands -- rank r renders band (r + f) mod N of frame f -- and each
+    band is sent point to point into its owner rank's frame ("bands", the north star's framebuffer
+    partition; round 6: no un-interleave, one-GPU rehearsal at N = 8 with the exchange's traffic
+    emulated C3 0.826 / C4 0.765 against 0.759 / 0.714 for "exchange", the round-5 row-interleaved
+    blocks + all-to-all + assembly, which stays selectable).  At N = 2 those take "frames" too: the
+    single xGMI link would carry 16 split frames' rows per step and outlast the render (C4 1.23x).
+    The other partition is timed in the same run and reported beside it (alt_collect).  Partitions
+    that deal whole frames need F to be a multiple of N, else every frame goes to rank 0 ("gather")."""
     collect = requested
     if collect == "auto":
-        collect = "exchange" if cfg.get("tiled") and world >= 4 else "frames"
-    if collect in ("frames", "exchange") and frames % world:
+        collect = "bands" if cfg.get("tiled") and world >= 4 else "frames"
+    if collect in ("frames", "exchange", "bands") and frames % world:
         collect = "gather"
     return collect
 
 
 def alt_collect(collect):
     """The other partition bench.py reports beside the headline one at N > 1 (`partition_alt`)."""
-    return "frames" if collect in ("exchange", "gather") else "exchange"
+    return "frames" if collect in ("exchange", "bands", "gather") else "bands"
 
 
 def result_line(*, config_name, cfg, world, backend, collect, views_kind, F, steps, warmup, T, rays_step,
@@ -586,11 +587,14 @@ def result_line(*, config_name, cfg, world, backend, collect, views_kind, F, ste
                    "row_block": row_block if world > 1 and not untiled else H,
                    "parallelism": (f"untiled: unsplit frames x{world}, rank q renders frames q, q+{world}, ... "
                                    "whole, no collective" if untiled else
-                                   f"framebuffer rows interleaved over {world} GPU(s) in blocks of {row_block} rows"
-                                   + ((" + one RCCL all-to-all per step: frame f gathered to its owner rank "
-                                       "(pipelined)" if collect == "exchange" else
-                                       " + one RCCL gather per step to rank 0 (pipelined)")
-                                      if world > 1 else "")
+                                   (f"framebuffer cut into {world} contiguous bands of {row_block} rows, rank r renders "
+                                    f"band (r + f) mod {world} of frame f; RCCL point-to-point sends each band into its "
+                                    "owner rank's frame in place (pipelined, no assembly)" if collect == "bands" else
+                                    f"framebuffer rows interleaved over {world} GPU(s) in blocks of {row_block} rows"
+                                    + ((" + one RCCL all-to-all per step: frame f gathered to its owner rank "
+                                        "(pipelined)" if collect == "exchange" else
+                                        " + one RCCL gather per step to rank 0 (pipelined)")
+                                       if world > 1 else ""))
                                    if world > 1 else "one GPU, whole frames"),
                    "collect": collect if world > 1 else None,
                    "float_framebuffer": float_fb, "streams": streams},
@@ -598,10 +602,11 @@ def result_line(*, config_name, cfg, world, backend, collect, views_kind, F, ste
         # receives per step, 1/N of them from each peer over that peer's direct link (one link per
         # peer in a fully connected 8-GPU node) at 76.8 GB/s per link and direction
         "collective": None if world == 1 or untiled else {
-            "kind": "all_to_all" if collect == "exchange" else "gather",
-            "recv_bytes_per_rank_step": (world - 1) * (F // world if collect == "exchange" else F) * H * 3 * W
+            "kind": {"exchange": "all_to_all", "bands": "p2p_bands"}.get(collect, "gather"),
+            "recv_bytes_per_rank_step": (world - 1) * (F // world if collect in ("exchange", "bands") else F) * H * 3 * W
             // world,
-            "xgmi_link_ms_est": round((F // world if collect == "exchange" else F) * H * 3 * W / world / 76.8e6, 4),
+            "xgmi_link_ms_est": round((F // world if collect in ("exchange", "bands") else F) * H * 3 * W / world / 76.8e6,
+                                      4),
             "ms_per_step": round(T / steps * 1e3, 5)},
         "roofline": roofline, "roofline_step": roofline_step,
         "roofline_solo": roofline_solo, "cpu_baseline": cpu, "parity": parity,
@@ -640,7 +645,7 @@ def main():
     ap.add_argument("--no-alt", action="store_true",
                     help="N > 1: skip the timed loop of the other partition (`partition_alt`)")
     ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
-    ap.add_argument("--collect", choices=("auto", "frames", "exchange", "gather"), default="auto",
+    ap.add_argument("--collect", choices=("auto", "frames", "exchange", "bands", "gather"), default="auto",
                     help="N > 1: exchange = every frame's rows dealt over the ranks, each frame gathered to one "
                          "owner rank in one RCCL all-to-all; frames = each rank renders its F/N frames whole (no "
                          "collective); gather = rows dealt, all frames to rank 0; auto = frames, except exchange "
@@ -721,7 +726,7 @@ def main():
             self.collect, self.kind = collect, kind
             b12, s3, steps_deg = view_set(kind)
             self.owner = world > 1 and collect == "frames"              # unsplit frames: no collective
-            self.exchange = world > 1 and collect in ("exchange", "frames")
+            self.exchange = world > 1 and collect in ("exchange", "frames", "bands")
             if self.exchange:
                 # batch order for the all-to-all: rank q owns batch frames q*k .. q*k+k-1, which are
                 # orbit frames q, q + N, q + 2N, ... (batch frame 0 = orbit frame 0 = the config view)
@@ -736,6 +741,10 @@ def main():
                 mine = self.gather.owned_frames()
                 self.Fl = len(mine)
                 b12, s3 = b12[mine], s3[mine]
+            elif collect == "bands":   # contiguous bands rotated per frame, received in place (no assembly)
+                self.gather = D.FrameBands(W, H, rank, world, frames=F, device=dev, slots=slots)
+                self.row_block = self.gather.band
+                self.tiling = pkg.Tiling(*self.gather.tiling_args())
             elif self.exchange:   # each frame to one owner rank: a rank's ingress is (N-1)/N of its k frames
                 self.gather = D.FrameExchange(W, H, self.row_block, rank, world, frames=F, device=dev, slots=slots)
             else:                 # every frame -> rank 0
@@ -750,13 +759,18 @@ def main():
                                    for _ in range((self.Fl + MAXF - 1) // MAXF)]
             self.counters = torch.zeros(8, dtype=torch.int64, device=dev)
 
+        def call_tiling(self, f0):
+            """The tiling of a call whose frame 0 is batch frame f0 (bands rotate with the frame)."""
+            t = self.tiling
+            return pkg.Tiling(t.row_block, (t.rank + f0) % t.world, t.world, 1) if t.bands else t
+
         def render(self, slot, st, with_counters=False):
             # one launch per (at most) 64 frames of the step; frame f's rows at f * 3 * W * rows
             px = self.d_px[slot % S]
             fb = 3 * W * max(self.rows, 1)
             for c, f0 in enumerate(range(0, self.Fl, MAXF)):
                 f1 = min(self.Fl, f0 + MAXF)
-                scene.render_batch_device(self.b12[f0:f1], self.s3[f0:f1], W, H, mode=mode, tiling=self.tiling,
+                scene.render_batch_device(self.b12[f0:f1], self.s3[f0:f1], W, H, mode=mode, tiling=self.call_tiling(f0),
                                           d_pixels=0 if px is None else px.data_ptr() + 4 * fb * f0,
                                           d_rgb8=self.gather.local_ptr(slot) + fb * f0,
                                           d_counters=self.chunk_counters[c].data_ptr() if with_counters else 0,
@@ -817,7 +831,7 @@ def main():
             for f0 in range(0, self.Fl, MAXF):
                 f1 = min(self.Fl, f0 + MAXF)
                 tmp = torch.empty((f1 - f0) * 3 * W * max(self.rows, 1), dtype=torch.uint8, device=dev)
-                sc_stats.render_batch_device(self.b12[f0:f1], self.s3[f0:f1], W, H, mode=mode, tiling=self.tiling,
+                sc_stats.render_batch_device(self.b12[f0:f1], self.s3[f0:f1], W, H, mode=mode, tiling=self.call_tiling(f0),
                                              d_rgb8=tmp.data_ptr(), d_counters=cs.data_ptr(), stream=stream.cuda_stream)
                 torch.cuda.synchronize(dev)
                 if int(cs[6].item()):

@@ -78,7 +78,10 @@ class _Stats(ctypes.Structure):
 
 
 class Tiling(ctypes.Structure):
-    _fields_ = [("row_block", ctypes.c_uint32), ("rank", ctypes.c_uint32), ("world", ctypes.c_uint32)]
+    """ceres_tiling: bands = 0 -- row blocks dealt round-robin; bands = 1 -- frame f of a call renders
+    the contiguous band (rank + f) mod world of row_block rows (distributed.FrameBands)."""
+    _fields_ = [("row_block", ctypes.c_uint32), ("rank", ctypes.c_uint32), ("world", ctypes.c_uint32),
+                ("bands", ctypes.c_uint32)]
 
 
 _lib = None

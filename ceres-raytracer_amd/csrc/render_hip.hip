@@ -82,6 +82,9 @@
 #ifndef CERES_STACK_GUARD
 #define CERES_STACK_GUARD CERES_COUNTING       // the BVH2 stack's guard slot (guarded_trace): the diagnostic (counting)
 #endif                                         // build only -- in the product it cost 1.9 % (C3) / 6.5 % (C5) of a batch
+#ifndef CERES_ASSEMBLE_NT
+#define CERES_ASSEMBLE_NT 0                    // ceres_assemble: nontemporal loads / stores
+#endif
 #ifndef CERES_LOCAL_ORDER
 #define CERES_LOCAL_ORDER 1                    // XCD-local Morton tile order (ensure_tile_order); 0: never
 #endif
@@ -915,8 +918,9 @@ __device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32
     }
 }
 
-__device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t lr) {
+__device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t f, uint32_t lr) {
     if (P.world == 1) return lr;                                      // one rank: local rows are the frame's rows
+    if (P.bands) return ((P.rank + f) % P.world) * P.row_block + lr;  // the frame's band (ceres_tiling.bands)
     return ((lr / P.row_block) * P.world + P.rank) * P.row_block + lr % P.row_block;
 }
 
@@ -1010,17 +1014,17 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     const uint32_t lx = lane & 7, ly = lane >> 3;
     const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + lx;
     const uint32_t lr = by * 16 + (wave >> 1) * 8 + ly;
-    const bool active = i < P.W && lr < P.local_rows;
+    const bool active = i < P.W && lr < P.local_rows && (!P.bands || global_row(P, f, lr) < P.H);
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;          // batch pixel (< 2^32, host-checked)
     bool hit = false;
     Hit h{0, 0.f, 0.f, 0.f};
     uint32_t n_pairs = 0, n_tests = 0;
     bool overflow = false;
-    const bool culled = !kStats && P.cull && tile_misses_root(P, f, active, i, global_row(P, lr));
+    const bool culled = !kStats && P.cull && tile_misses_root(P, f, active, i, global_row(P, f, lr));
     if (culled) {
         if (active) store_pixel(P, f, lr, i, 0.f, 0.f, 0.f);        // render.hpp:116-117, every pixel a miss
     } else if (active) {
-        const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
+        const F3 view = primary_dir<kG>(P, f, i, global_row(P, f, lr));
         hit = guarded_trace<kStats, kBlock, uint32_t*, kRobust, -1, kG>(P, f3(P.cam[f].eye), view, stk, h, n_pairs, n_tests,
                                                                       overflow);
         if (P.rec_prim) {
@@ -1314,7 +1318,7 @@ __device__ __forceinline__ void shade_pixel(const KParams& P, uint32_t f, uint32
     if (blocked) {
         ++occluded;
     } else {
-        const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
+        const F3 view = primary_dir<kG>(P, f, i, global_row(P, f, lr));
         CERES_COUNT_V(kFShadeV, 40);
         shade<kG>(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
     }
@@ -1360,7 +1364,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
         const uint32_t lx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4), ly = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
         i_ = bx_ * 8u + lx;
         lr_ = by_ * 8u + ly;
-        return i_ < P.W && lr_ < P.local_rows;
+        return i_ < P.W && lr_ < P.local_rows && (!P.bands || global_row(P, f_, lr_) < P.H);
     };
     // a pixel's colour: stored now, or (the even tile of a pair) stashed for the odd tile's stores;
     // t_prev: the even tile's order entry (its pixel positions are decoded again, not stashed)
@@ -1436,12 +1440,12 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
     // the last tile of this wavefront (a stashed even tile with no odd partner is stored at once)
     const bool last_q = q + 1 == kTPW || (kTPW > 1 && slot_q + 1 >= n_tiles);
-    if (!kStats && P.cull && tile_misses_root(P, f, active, i, global_row(P, lr))) {
+    if (!kStats && P.cull && tile_misses_root(P, f, active, i, global_row(P, f, lr))) {
         emit(q, last_q, t_prev, active, f, lr, i, 0.f, 0.f, 0.f);       // render.hpp:116-117, every pixel a miss
         continue;
     }
     if (active) {
-        const F3 view = primary_dir<kG>(P, f, i, global_row(P, lr));
+        const F3 view = primary_dir<kG>(P, f, i, global_row(P, f, lr));
         // kOct -1: the traversal dispatches on a wave-uniform octant; -2: generic loop only
         constexpr int kOctMode = (!kSteal || (CERES_OCTANT_SLAB & 4)) ? -1 : -2;
         hit = guarded_trace<kStats, kB, StkT, kRobust, kOctMode, kG>(P, f3(P.cam[f].eye), view, stk, h, n_pairs,
@@ -1588,7 +1592,16 @@ __global__ __launch_bounds__(256) void ceres_assemble(const uint8_t* __restrict_
         const uint8_t* s = src + base + (size_t(f) * n + (n - 1 - k)) * row_bytes;
         uint8_t* d = dst + size_t(oy) * row_bytes;
         for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
-            if (kVec) reinterpret_cast<uint4*>(d)[u] = reinterpret_cast<const uint4*>(s)[u];
+            if (kVec) {
+#if CERES_ASSEMBLE_NT
+                // streamed through the caches (nontemporal): the un-interleave runs beside later
+                // steps' renders, whose BVH / triangle lines it would otherwise evict
+                const U4v x = __builtin_nontemporal_load(reinterpret_cast<const U4v*>(s) + u);
+                __builtin_nontemporal_store(x, reinterpret_cast<U4v*>(d) + u);
+#else
+                reinterpret_cast<uint4*>(d)[u] = reinterpret_cast<const uint4*>(s)[u];
+#endif
+            }
             else d[u] = s[u];
         }
     }
@@ -1647,6 +1660,11 @@ void ceres::scene_release(ceres_scene* s) {
 
 namespace {
 
+size_t local_rows_of(size_t H, uint32_t rb, uint32_t rank, uint32_t world);
+size_t local_rows_of(size_t H, const ceres_tiling& t) {
+    if (t.bands && t.world > 1) return t.row_block;                 // every frame: one band of row_block rows
+    return local_rows_of(H, t.row_block, t.rank, t.world);
+}
 size_t local_rows_of(size_t H, uint32_t rb, uint32_t rank, uint32_t world) {
     const size_t nblocks = (H + rb - 1) / rb;
     size_t rows = 0;
@@ -1691,6 +1709,7 @@ int upload_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
         }
     }
     o.W = W; o.H = H; o.row_block = t.row_block; o.rank = t.rank; o.world = t.world; o.frames = frames; o.tile = tile;
+    o.bands = t.bands;
     o.packed = packed;
     // padded to a multiple of 8 entries (zeros): the fused kernel reads its tile-order entries
     // up to eight at a time through the scalar cache
@@ -1755,7 +1774,7 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
                       uint32_t tpw) {
     const uint32_t tile_key = tile | tpw << 16;                    // the order depends on the tiles per wave
     for (auto& o : s->orders)
-        if (o.W == W && o.H == H && o.row_block == t.row_block && o.rank == t.rank && o.world == t.world &&
+        if (o.W == W && o.H == H && o.row_block == t.row_block && o.rank == t.rank && o.world == t.world && o.bands == t.bands &&
             o.frames == frames && o.tile == tile_key && o.packed == packed) {
             o.used = ++s->order_clock;
             *out = o.d;
@@ -1778,7 +1797,8 @@ int ensure_tile_order(ceres_scene* s, size_t W, size_t H, const ceres_tiling& t,
     for (uint32_t f = 0; f < frames; ++f)
         for (uint32_t y = 0; y < by; ++y) {
             const size_t lr = std::min<size_t>(size_t(y) * tile + tile / 2, rows - 1);
-            const size_t j = ((lr / t.row_block) * t.world + t.rank) * t.row_block + lr % t.row_block;
+            const size_t j = (t.bands && t.world > 1) ? ((t.rank + f) % t.world) * t.row_block + lr
+                                                      : ((lr / t.row_block) * t.world + t.rank) * t.row_block + lr % t.row_block;
             for (uint32_t x = 0; x < bx; ++x) {
                 const double dx = double(x) * tile + tile / 2 - cx, dy = double(j) - cy;
                 const uint32_t id = (f * by + y) * bx + x;
@@ -2026,7 +2046,7 @@ static int check_fused_lds(const ceres_scene* s, const KParams& P, int stw, size
 int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const float* sun, int mode, size_t W, size_t H,
                  const ceres_tiling* tiling, float* d_pixels, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream,
                  int32_t* d_rec_prim, float* d_rec_tuv, int8_t* d_rec_shadow, bool first, bool last,
-                 uint32_t batch_frames) {
+                 uint64_t batch_primary) {
     if (!s || !basis12 || !sun) return set_error(CERES_EINVAL, "render: null argument");
     if (s->f64) return set_error(CERES_EINVAL, "scene is double precision: use ceres_render_f64");
     if (frames == 0 || frames > uint32_t(kFramesPerLaunch))
@@ -2040,7 +2060,10 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
     ceres_tiling t{uint32_t(H), 0, 1};
     if (tiling) t = *tiling;
     if (t.world == 0 || t.rank >= t.world || t.row_block == 0) return set_error(CERES_EINVAL, "render: bad tiling");
-    const size_t rows = local_rows_of(H, t.row_block, t.rank, t.world);
+    if (t.world == 1) t.bands = 0;
+    if (t.bands && (t.bands != 1 || size_t(t.row_block) * t.world < H))
+        return set_error(CERES_EINVAL, "render: bands of %u rows x %u ranks do not cover %zu rows", t.row_block, t.world, H);
+    const size_t rows = local_rows_of(H, t);
     if (size_t(frames) * W * rows > 0xffffffffull) return set_error(CERES_EINVAL, "render: more than 2^32 pixels per batch");
     const uint32_t bx = uint32_t((W + 15) / 16), by = uint32_t((rows + 15) / 16);
     if (size_t(by) * frames > 65535u) return set_error(CERES_EINVAL, "render: frames x row blocks exceeds the grid limit");
@@ -2062,6 +2085,7 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
     P.frames = frames;
     P.W = uint32_t(W); P.H = uint32_t(H);
     P.row_block = t.row_block; P.rank = t.rank; P.world = t.world; P.local_rows = uint32_t(rows);
+    P.bands = t.bands;
     P.row_blocks_per_frame = by;
     P.stack_entries = s->stack_entries;
     P.shadow_stack_entries = s->shadow_stack_entries;
@@ -2216,7 +2240,7 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
     }
     if (d_counters && last) {
         hipLaunchKernelGGL(dev::ceres_finalize, dim3(1), dim3(64), 0, stream, s->d_shards,
-                           uint64_t(batch_frames) * W * rows, d_counters);
+                           batch_primary, d_counters);
         HIP_TRY(hipGetLastError());
         s->shards_dirty = false;
     }
@@ -2231,22 +2255,35 @@ int launch(ceres_scene* s, uint32_t frames, const float* basis12, const float* s
     if (frames == 0 || frames > uint32_t(kMaxFrames))
         return set_error(CERES_EINVAL, "render: %u frames per batch (1..%d)", frames, kMaxFrames);
     if (!basis12 || !sun) return set_error(CERES_EINVAL, "render: null argument");
-    if (frames <= uint32_t(kFramesPerLaunch))
-        return launch_chunk(s, frames, basis12, sun, mode, W, H, tiling, d_pixels, d_rgb8, d_counters, stream, d_rec_prim,
-                            d_rec_tuv, d_rec_shadow, true, true, frames);
     ceres_tiling t{uint32_t(H), 0, 1};
     if (tiling) t = *tiling;
     if (t.world == 0 || t.rank >= t.world || t.row_block == 0) return set_error(CERES_EINVAL, "render: bad tiling");
-    const size_t fp = W * local_rows_of(H, t.row_block, t.rank, t.world);   // pixels per frame on this rank
+    // the batch's primary rays (render.hpp:102: one per pixel this rank renders): with bands, a
+    // frame's band may end below its row_block rows (the last band of the frame)
+    uint64_t primary = uint64_t(frames) * W * local_rows_of(H, t);
+    if (t.bands && t.world > 1) {
+        primary = 0;
+        for (uint32_t f = 0; f < frames; ++f) {
+            const size_t b = (t.rank + f) % t.world, top = b * size_t(t.row_block);
+            primary += uint64_t(W) * (top < H ? std::min<size_t>(t.row_block, H - top) : 0);
+        }
+    }
+    if (frames <= uint32_t(kFramesPerLaunch))
+        return launch_chunk(s, frames, basis12, sun, mode, W, H, tiling, d_pixels, d_rgb8, d_counters, stream, d_rec_prim,
+                            d_rec_tuv, d_rec_shadow, true, true, primary);
+    const size_t fp = W * local_rows_of(H, t);                      // pixels per frame on this rank
     // equal chunks (64 frames: 32 + 32, not 56 + 8 -- a small last launch is all tail)
     const uint32_t n_launch = (frames + kFramesPerLaunch - 1) / kFramesPerLaunch;
     for (uint32_t c = 0, f0 = 0; c < n_launch; ++c) {
         const uint32_t n = frames / n_launch + (c < frames % n_launch ? 1u : 0u);
         const size_t o = size_t(f0) * fp;
-        if (int rc = launch_chunk(s, n, basis12 + 12 * size_t(f0), sun + 3 * size_t(f0), mode, W, H, tiling,
+        // bands: the chunk's frame 0 is the call's frame f0, so its band rotation starts at rank + f0
+        ceres_tiling tc = t;
+        if (t.bands) tc.rank = (t.rank + f0) % t.world;
+        if (int rc = launch_chunk(s, n, basis12 + 12 * size_t(f0), sun + 3 * size_t(f0), mode, W, H, &tc,
                                   d_pixels ? d_pixels + 3 * o : nullptr, d_rgb8 ? d_rgb8 + 3 * o : nullptr, d_counters,
                                   stream, d_rec_prim ? d_rec_prim + o : nullptr, d_rec_tuv ? d_rec_tuv + 3 * o : nullptr,
-                                  d_rec_shadow ? d_rec_shadow + o : nullptr, f0 == 0, f0 + n >= frames, frames))
+                                  d_rec_shadow ? d_rec_shadow + o : nullptr, f0 == 0, f0 + n >= frames, primary))
             return rc;
         f0 += n;
     }
@@ -2289,7 +2326,7 @@ const char* ceres_kernel_names(void) {
 size_t ceres_tiling_local_rows(size_t height, const ceres_tiling* t) {
     if (!t) return height;
     if (t->world == 0 || t->row_block == 0 || t->rank >= t->world) return 0;
-    return local_rows_of(height, t->row_block, t->rank, t->world);
+    return local_rows_of(height, *t);
 }
 
 ceres_scene* ceres_scene_create(const float* tri48, size_t n_tri, const float* norm36, const void* nodes32,
@@ -2457,6 +2494,18 @@ int ceres_render_batch_device(ceres_scene* s, uint32_t frames, const float* basi
                   static_cast<hipStream_t>(stream));
 }
 
+// Workgroup rows of the un-interleave grid (its y extent; each workgroup strides over the output
+// rows).  A grid of one workgroup per output row (16 x 1080-row frames: 34,560 workgroups) floods
+// the dispatcher and takes wave slots from the render launches it runs beside (the exchange's
+// assembly overlaps the next steps' renders); a bounded grid copies in the background.
+// CERES_ASSEMBLE_ROWS overrides (A/B; 0 = one workgroup per row).
+constexpr size_t kAssembleGridRows = 65535;   // default cap (A/B pending)
+static uint32_t assemble_grid_rows(size_t out_rows) {
+    static const long env = [] { const char* e = std::getenv("CERES_ASSEMBLE_ROWS"); return e ? std::strtol(e, nullptr, 10) : -1L; }();
+    const size_t cap = env < 0 ? size_t(kAssembleGridRows) : env == 0 ? size_t(65535) : size_t(env);
+    return uint32_t(std::max<size_t>(1, std::min<size_t>({out_rows, cap, 65535})));
+}
+
 int ceres_assemble_rgb8(const uint8_t* d_gathered, size_t rank_stride_bytes, uint8_t* d_out, uint32_t frames,
                         size_t W, size_t H, uint32_t row_block, uint32_t world, void* stream) {
     if (!d_gathered || !d_out || frames == 0 || W == 0 || H == 0 || row_block == 0 || world == 0)
@@ -2470,8 +2519,7 @@ int ceres_assemble_rgb8(const uint8_t* d_gathered, size_t rank_stride_bytes, uin
     const bool vec = row_bytes % 16 == 0 && rank_stride_bytes % 16 == 0 &&
                      reinterpret_cast<uintptr_t>(d_gathered) % 16 == 0 && reinterpret_cast<uintptr_t>(d_out) % 16 == 0;
     const uint32_t units = vec ? row_bytes / 16 : row_bytes;
-    const dim3 grid(uint32_t(std::min<size_t>((units + 255) / 256, 64)),
-                    uint32_t(std::min<size_t>(size_t(frames) * H, 65535)));
+    const dim3 grid(uint32_t(std::min<size_t>((units + 255) / 256, 64)), assemble_grid_rows(size_t(frames) * H));
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (vec)
         hipLaunchKernelGGL(dev::ceres_assemble<true>, grid, dim3(256), 0, st, d_gathered, rank_stride_bytes, d_out,
@@ -2493,8 +2541,7 @@ int ceres_assemble_rgb8_packed(const uint8_t* d_gathered, uint8_t* d_out, uint32
     const bool vec = row_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(d_gathered) % 16 == 0 &&
                      reinterpret_cast<uintptr_t>(d_out) % 16 == 0;
     const uint32_t units = vec ? row_bytes / 16 : row_bytes;
-    const dim3 grid(uint32_t(std::min<size_t>((units + 255) / 256, 64)),
-                    uint32_t(std::min<size_t>(size_t(frames) * H, 65535)));
+    const dim3 grid(uint32_t(std::min<size_t>((units + 255) / 256, 64)), assemble_grid_rows(size_t(frames) * H));
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (vec)
         hipLaunchKernelGGL((dev::ceres_assemble<true, true>), grid, dim3(256), 0, st, d_gathered, size_t(0), d_out, frames,

@@ -33,7 +33,7 @@ struct ceres_scene {
     // per-launch events, and no stall while the working set of shapes fits the cache.
     struct TileOrder {
         size_t W = 0, H = 0;
-        uint32_t row_block = 0, rank = 0, world = 0, frames = 0, tile = 0;
+        uint32_t row_block = 0, rank = 0, world = 0, frames = 0, tile = 0, bands = 0;
         bool packed = false;           // entries (f << 26) | (y << 13) | x (pack_tile) instead of linear ids
         uint32_t* d = nullptr;
         size_t cap = 0;                // entries allocated at d

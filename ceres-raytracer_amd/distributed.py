@@ -37,6 +37,26 @@ def exchange_order(frames, world):
     return np.asarray([m * world + q for q in range(world) for m in range(k)], np.int64)
 
 
+def band_height(H, world):
+    """Rows per band of the band partition (FrameBands): ceil(H / world), rounded up to a multiple of
+    the kernel's 8-row tiles when every band stays non-empty."""
+    bh = -(-H // world)
+    bh8 = -(-bh // 8) * 8
+    return bh8 if (world - 1) * bh8 < H else bh
+
+
+def band_rows(H, bh, b):
+    """Rows of band b (the last band is shorter)."""
+    return max(0, min(bh, H - b * bh))
+
+
+def band_groups(frames, rank, world):
+    """Batch frames whose band `b` this rank renders, per band: frame f's band on rank r is
+    (r + f) mod world, so over the step's frames every rank renders every band equally often
+    (a frame's cost is concentrated in its central bands; rotating keeps the ranks balanced)."""
+    return [[f for f in range(frames) if (rank + f) % world == b] for b in range(world)]
+
+
 def rank_rows(H, row_block, rank, world):
     """Closed form of len(row_map(...)[rank]) -- the formula ceres_assemble uses on the device."""
     nb = (H + row_block - 1) // row_block
@@ -267,6 +287,108 @@ class FrameExchange:
             for s, used in enumerate(self.reused):
                 if used:
                     torch.cuda.current_stream(self.device).wait_event(self.assembled[s])
+
+
+class FrameBands:
+    """Per-rank bands of an F-frame batch (F = k * world) -> frames [q*k, (q+1)*k) of the batch
+    assembled on rank q, with nothing to un-interleave.
+
+    The renders use ceres_tiling.bands (Tiling(band_height, rank, world, bands=1)): frame f of the
+    batch is cut into `world` contiguous bands and rank r renders band (r + f) mod world, so over
+    the step's frames every rank renders every band equally often (the frames' cost sits in their
+    central bands).  A rank's buffer holds its band of every frame, frame-major, `band_height` rows
+    per frame with the band's valid rows at the END (ceres_tiling: positions row_block - n .. of the
+    frame, top row first) -- a contiguous slice of the frame's PPM body.  start() sends each band
+    to the frame's owner and receives the owner's bands straight into their rows of its PPM
+    bodies: point-to-point RCCL (batch_isend_irecv; one message per (frame, peer)), no staging
+    buffer and no assembly kernel (FrameExchange un-interleaves row blocks after its all-to-all,
+    which costs ~9 % of an N = 8 step in the one-GPU rehearsal).  Own bands are copied locally.
+    Same slot protocol as FrameExchange.
+    """
+
+    def __init__(self, W, H, rank, world, frames=None, device="cpu", group=None, slots=2):
+        import torch
+        frames = world if frames is None else frames
+        if frames % world:
+            raise ValueError("FrameBands: frames (%d) must be a multiple of world (%d)" % (frames, world))
+        self.W, self.H, self.rank, self.world, self.group = W, H, rank, world, group
+        self.frames, self.slots = frames, slots
+        self.k = frames // world
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.band = band_height(H, world) if world > 1 else H
+        self.local_rows = self.band                  # every frame: one band (ceres_tiling_local_rows)
+        self.row_bytes = 3 * W
+        self.is_dst = True
+        self.bufs = [torch.zeros((frames * self.band, self.row_bytes), dtype=torch.uint8, device=self.device)
+                     for _ in range(slots)]
+        self.full = [torch.zeros((self.k, H, self.row_bytes), dtype=torch.uint8, device=self.device)
+                     for _ in range(slots)] if world > 1 else None
+        self.work = [None] * slots
+
+    def tiling_args(self):
+        """(row_block, rank, world, bands) of this rank's renders."""
+        return (self.band, self.rank, self.world, 1 if self.world > 1 else 0)
+
+    def owned_frames(self):
+        return list(range(self.rank * self.k, (self.rank + 1) * self.k))
+
+    def local_ptr(self, slot=0):
+        return self.bufs[slot].data_ptr()
+
+    def _band_view(self, slot, f):
+        """This rank's band of batch frame f in its buffer (the band's valid rows only)."""
+        b = (self.rank + f) % self.world
+        n = band_rows(self.H, self.band, b)
+        return self.bufs[slot][f * self.band + self.band - n:(f + 1) * self.band], b, n
+
+    def _frame_slice(self, slot, m, b):
+        """Rows of band b in owned frame m's PPM body (top row first: band b's global rows
+        b*band .. b*band + n - 1 are PPM rows H - b*band - n .. H - b*band - 1)."""
+        n = band_rows(self.H, self.band, b)
+        top = self.H - b * self.band - n
+        return self.full[slot][m, top:top + n]
+
+    def start(self, slot=0):
+        import torch.distributed as dist
+        if self.world == 1:
+            return
+        ops = []
+        for m, f in enumerate(self.owned_frames()):  # own bands of own frames: local copies
+            src, b, n = self._band_view(slot, f)
+            if n:
+                self._frame_slice(slot, m, b).copy_(src)
+        for q in range(self.world):                 # this rank's bands of q's frames -> q
+            if q == self.rank:
+                continue
+            for f in range(q * self.k, (q + 1) * self.k):
+                src, b, n = self._band_view(slot, f)
+                if n:
+                    ops.append(dist.P2POp(dist.isend, src.view(-1), q, group=self.group))
+        for r in range(self.world):                 # r's bands of this rank's frames, in place
+            if r == self.rank:
+                continue
+            for m, f in enumerate(self.owned_frames()):
+                b = (r + f) % self.world
+                if band_rows(self.H, self.band, b):
+                    ops.append(dist.P2POp(dist.irecv, self._frame_slice(slot, m, b).view(-1), r, group=self.group))
+        self.work[slot] = dist.batch_isend_irecv(ops) if ops else []
+
+    def finish(self, slot=0):
+        """Complete `slot`: this rank's k frames (batch frames owned_frames()) as (k, H, 3W) PPM
+        bodies (for GPUs: ordered on the current stream)."""
+        if self.world == 1:
+            return self.bufs[slot][: self.frames * self.H].view(self.frames, self.H, self.row_bytes)
+        w = self.work[slot]
+        self.work[slot] = None
+        if w is None:
+            raise RuntimeError("FrameBands.finish without start")
+        for x in w:
+            x.wait()
+        return self.full[slot]
+
+    def wait_assembled(self):
+        pass
 
 
 class FrameOwner:

@@ -90,11 +90,19 @@ typedef struct {
     double   ms;              /* device time of the render (HIP events), host-buffer API only */
 } ceres_stats;
 
-/* Row partition across ranks: rows are dealt in blocks of `row_block` rows, block b to rank
- * b % world; world = 1 renders the whole frame.  Local row k of a rank is
- * global row j = ((k / row_block) * world + rank) * row_block + k % row_block. */
+/* Row partition across ranks; world = 1 renders the whole frame.
+ * bands = 0: rows are dealt in blocks of `row_block` rows, block b to rank b % world; local row k
+ *   of a rank is global row j = ((k / row_block) * world + rank) * row_block + k % row_block.
+ * bands = 1: frame f of the call (0-based) is cut into `world` contiguous bands of `row_block`
+ *   rows (the last one shorter; row_block * world >= height) and the rank renders band
+ *   (rank + f) mod world: local row k is global row j = band * row_block + k, every frame has
+ *   row_block local rows, those with j >= height are not rendered (their RGB8 positions, the
+ *   first ones of the frame's buffer, are not written).  Rotating the band from frame to frame
+ *   keeps ranks balanced over a batch; a band is a contiguous slice of the frame's PPM body, so
+ *   an owner rank can receive it in place (no un-interleave). */
 typedef struct {
     uint32_t row_block, rank, world;
+    uint32_t bands;
 } ceres_tiling;
 
 /* ---- host-side scene preparation (what static.cpp / anim.cpp run before render()) ---- */

@@ -240,6 +240,103 @@ def test_frame_exchange_alltoall(world, row_block, slots, k):
     assert all(res.values()), res
 
 
+def test_band_geometry():
+    """ceres_tiling.bands: world contiguous bands of band_height rows (multiple of the 8-row tile
+    when every band stays non-empty) cover every row once; the library's local row count is the
+    band height; over a step every rank renders every band equally often (band_groups)."""
+    pkg = import_package()
+    import ceres_raytracer_amd.distributed as D
+    for H in (1, 7, 15, 16, 61, 217, 1080, 2160, 4096):
+        for world in (2, 3, 4, 5, 8):
+            if world > H:
+                continue
+            bh = D.band_height(H, world)
+            rows = [D.band_rows(H, bh, b) for b in range(world)]
+            assert sum(rows) == H, (H, world, bh, rows)
+            # bands are non-empty unless the frame is too short to give every rank a row of ceil(H / N)
+            assert all(n > 0 for n in rows) or (world - 1) * -(-H // world) >= H, (H, world, rows)
+            assert bh * world >= H and (bh % 8 == 0 or (world - 1) * (-(-bh // 8) * 8) >= H)
+            for r in range(world):
+                assert pkg.local_rows(H, pkg.Tiling(bh, r, world, 1)) == bh
+    for world, k in ((2, 16), (8, 16), (3, 2)):
+        for r in range(world):
+            g = D.band_groups(k * world, r, world)
+            assert [len(x) for x in g] == [k] * world
+            assert sorted(f for x in g for f in x) == list(range(k * world))
+    assert D.band_height(1080, 8) == 136 and D.band_rows(1080, 136, 7) == 128
+
+
+def _bands_worker(rank, world, port, W, H, slots, q, k):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import import_package as ip
+    ip()
+    import torch
+    import torch.distributed as dist
+    import ceres_raytracer_amd.distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(23)
+        steps = 3 * slots
+        F = k * world
+        bodies = [rng.integers(0, 256, size=(H, 3 * W), dtype=np.uint8) for _ in range(steps * F)]
+        g = D.FrameBands(W, H, rank, world, frames=F, device="cpu", slots=slots)
+        assert g.owned_frames() == list(range(rank * k, rank * k + k))
+        bh = g.band
+        assert g.local_rows == bh and g.tiling_args() == (bh, rank, world, 1)
+        ok = True
+        owner = [None] * slots
+
+        def check(slot):
+            nonlocal ok
+            full = g.finish(slot)
+            st = owner[slot]
+            for m, f in enumerate(g.owned_frames()):
+                ok &= bool(np.array_equal(full[m].numpy(), bodies[st * F + f]))
+            owner[slot] = None
+
+        for st in range(steps):
+            slot = st % slots
+            if owner[slot] is not None:
+                check(slot)
+            g.bufs[slot].fill_(0)
+            for f in range(F):                       # as the kernel writes RGB8 with ceres_tiling.bands
+                b = (rank + f) % world
+                for i in range(D.band_rows(H, bh, b)):   # local row i = global row b*bh + i at position bh-1-i
+                    j = b * bh + i
+                    g.bufs[slot][f * bh + bh - 1 - i] = torch.from_numpy(bodies[st * F + f][H - 1 - j].copy())
+            g.start(slot)
+            owner[slot] = st
+        for slot in range(slots):
+            if owner[slot] is not None:
+                check(slot)
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,slots,k,H", [(2, 2, 1, 61), (3, 3, 2, 61), (4, 2, 4, 97), (5, 4, 2, 33), (8, 8, 16, 61)])
+def test_frame_bands_p2p(world, slots, k, H):
+    """bench.py --collect bands: each rank renders band (rank + f) mod N of every frame f and the
+    bands travel point to point into their owner's PPM bodies (no un-interleave), `slots` steps in
+    flight, gloo on CPU; ragged last bands.  (8, 8, 16) is the N = 8 bench shape (128 frames per
+    step, 16 owned per rank) on small frames."""
+    import_package()
+    W = 13
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bands_worker, args=(r, world, port, W, H, slots, q, k)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+        assert p.exitcode == 0
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert all(res.values()), res
+
+
 def test_packed_permutation_matches_padded():
     """packed_row_permutation = batch_row_permutation with the padding rows squeezed out."""
     import_package()
@@ -344,8 +441,8 @@ def test_frame_owner_gloo_step(world, k):
 
 def test_bench_partition_choice():
     """bench.py --collect auto: whole frames per rank with no data-path collective for the
-    frame-unit configs (C3, bunny) at every N > 1; the tiled 4096^2 / 4K configs (C4, C5) deal their
-    frames' rows over the ranks and gather them with one RCCL all-to-all per step at N >= 4, and
+    frame-unit configs (C3, bunny) at every N > 1; the tiled 4096^2 / 4K configs (C4, C5) cut their
+    frames into rotated contiguous bands sent point to point to the owner ranks at N >= 4, and
     render whole frames at N = 2 (one xGMI link, DESIGN.md "Multi-GPU"); explicit choices are kept;
     a frame count that is not a multiple of N falls back to the gather.  The other partition is
     reported beside it (`alt_collect`)."""
@@ -359,12 +456,15 @@ def test_bench_partition_choice():
         assert bench.choose_collect("auto", C["bunny_1080"], n, 16 * n) == "frames"
     for name in ("dragon_4096", "proc_c5"):
         assert bench.choose_collect("auto", C[name], 2, 32) == "frames"
-        assert bench.choose_collect("auto", C[name], 4, 64) == "exchange"
-        assert bench.choose_collect("auto", C[name], 8, 128) == "exchange"
+        assert bench.choose_collect("auto", C[name], 4, 64) == "bands"
+        assert bench.choose_collect("auto", C[name], 8, 128) == "bands"
     assert bench.choose_collect("exchange", C["dragon_1080"], 4, 64) == "exchange"
+    assert bench.choose_collect("bands", C["dragon_1080"], 4, 64) == "bands"
     assert bench.choose_collect("gather", C["dragon_1080"], 4, 64) == "gather"
     assert bench.choose_collect("frames", C["dragon_1080"], 3, 16) == "gather"
-    assert bench.alt_collect("exchange") == "frames" and bench.alt_collect("frames") == "exchange"
+    assert bench.choose_collect("bands", C["dragon_1080"], 3, 16) == "gather"
+    assert bench.alt_collect("bands") == "frames" and bench.alt_collect("frames") == "bands"
+    assert bench.alt_collect("exchange") == "frames"
 
 
 def _line_worker(rank, world, port, q):
@@ -391,6 +491,7 @@ def _line_worker(rank, world, port, q):
         res = {}
         for col in (collect, bench.alt_collect(collect)):
             g = (D.FrameOwner(W, H, rank, world, frames=F, device="cpu", slots=2) if col == "frames" else
+                 D.FrameBands(W, H, rank, world, frames=F, device="cpu", slots=2) if col == "bands" else
                  D.FrameExchange(W, H, rb, rank, world, frames=F, device="cpu", slots=2))
             rows = D.row_map(H, rb, world)[rank] if col == "exchange" else np.arange(H)
 
@@ -405,6 +506,13 @@ def _line_worker(rank, world, port, q):
                 if col == "frames":
                     for m, f in enumerate(g.owned_frames()):
                         g.bufs[slot][m * H:(m + 1) * H] = torch.from_numpy(body(int(order[f]), step))
+                elif col == "bands":                     # band (rank + f) mod N of every frame, ceres_tiling.bands
+                    bh = g.band
+                    for f in range(F):
+                        b = body(int(order[f]), step)
+                        band = (rank + f) % world
+                        for kk in range(D.band_rows(H, bh, band)):
+                            g.bufs[slot][f * bh + bh - 1 - kk] = torch.from_numpy(b[H - 1 - (band * bh + kk)].copy())
                 else:                                    # this rank's rows of every frame, ceres_tiling layout
                     n = len(rows)
                     for f in range(F):
@@ -464,5 +572,5 @@ def test_bench_line_world2_gloo():
     assert line["n_gpus"] == line["world_size"] == 2 and line["backend"] == "gloo"
     assert line["config"]["collect"] == "frames"
     assert line["config"]["views"] == "config" and "copies of the config view" in line["config"]["workload"]
-    assert line["partition_alt"]["collect"] == "exchange" and line["partition_alt"]["value"] > 0
+    assert line["partition_alt"]["collect"] == "bands" and line["partition_alt"]["value"] > 0
     assert line["scaling"] == "weak" and line["value"] > 0

@@ -154,3 +154,81 @@ def test_bench_frames_partition_matches_reference(pkg, name, world, build):
     ref = [fx["%08x" % int(np.asarray(x, np.float32).view(np.uint32))] for x in steps]
     ref = [e["ref"] if build == "ref" else e for e in ref]
     assert (rays, hits) == (sum(e["rays"] for e in ref), sum(e["hits"] for e in ref))
+
+
+BANDS_CASES = [("dragon_1080", 2, "ref"), ("dragon_1080", 8, "ref"), ("dragon_1080", 4, "exact"),
+               ("dragon_4096", 8, "ref"), ("bunny_640", 4, "exact"), ("proc_c5", 4, "ref")]
+
+
+@pytest.mark.parametrize("name,world,build", BANDS_CASES)
+def test_bench_bands_partition_matches_reference(pkg, name, world, build):
+    """bench.py --collect bands (the tiled C4 / C5 at N >= 4; C3's partition_alt): rank r renders
+    band (r + f) mod N of every batch frame f (ceres_tiling.bands, one launch per 64 frames, the
+    rotation carried across launches and the library's 56-frame chunks); every band placed in its
+    rows of the owner's PPM body (the layout distributed.FrameBands receives in place) gives the
+    reference's frame, and the ranks' rays / hits add up to the step's reference counts."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device (no CPU fallback exists)")
+    import ceres_raytracer_amd.distributed as D
+    cfg = configs.CONFIGS[name]
+    W, H = cfg["W"], cfg["H"]
+    meta, _, _ = load_golden(name)
+    fx = load_orbit(name)["by_step_bits"]
+    arith = pkg.ARITH_FMA if build == "ref" else pkg.ARITH_EXACT
+    scene, cam = _scene(pkg, name, arith)
+    F = 16 * world
+    b12, s3, steps = pkg.bench_views(cam, cfg["sun"], W, H, F, basis0=_basis0(meta, cfg, build))
+    order = D.exchange_order(F, world)
+    b12, s3, steps = b12[order], s3[order], steps[order]
+    mode = pkg.cfg_mode(cfg, arith)
+    st = torch.cuda.current_stream().cuda_stream
+    bh = D.band_height(H, world)
+    full = torch.zeros((F, H, 3 * W), dtype=torch.uint8, device="cuda")
+    counters = torch.zeros(8, dtype=torch.int64, device="cuda")
+    rays = hits = 0
+    for r in range(world):
+        assert pkg.local_rows(H, pkg.Tiling(bh, r, world, 1)) == bh
+        buf = torch.zeros((F, bh, 3 * W), dtype=torch.uint8, device="cuda")
+        for f0 in range(0, F, MAXF):
+            f1 = min(F, f0 + MAXF)
+            counters.zero_()
+            scene.render_batch_device(b12[f0:f1], s3[f0:f1], W, H, mode=mode, tiling=pkg.Tiling(bh, (r + f0) % world, world, 1),
+                                      d_rgb8=buf[f0].data_ptr(), d_counters=counters.data_ptr(), stream=st)
+            torch.cuda.synchronize()
+            c = counters.cpu().numpy()
+            assert c[6] == 0, "traversal stack overflow"
+            rays += int(c[0]); hits += int(c[1])
+        for f in range(F):
+            b = (r + f) % world
+            n = D.band_rows(H, bh, b)
+            if n:
+                top = H - b * bh - n
+                full[f, top:top + n] = buf[f, bh - n:]
+        del buf
+    head = b"P6 %d %d 255\n" % (W, H)
+    bad = []
+    ref_rays = ref_hits = 0
+    for f in range(F):
+        e0 = fx["%08x" % int(np.asarray(steps[f], np.float32).view(np.uint32))]
+        e = e0["ref"] if build == "ref" else e0
+        ref_rays += e["rays"]; ref_hits += e["hits"]
+        if hashlib.sha256(head + full[f].cpu().numpy().tobytes()).hexdigest() != e["sha256"]:
+            bad.append((f, e0["k"]))
+    assert not bad, f"frames differing from the reference (batch frame, orbit view k): {bad}"
+    assert (rays, hits) == (ref_rays, ref_hits)
+
+
+def test_band_tiling_rejects_uncovered_frames(pkg):
+    """ceres_tiling.bands needs row_block * world >= height (every row in some band)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device (no CPU fallback exists)")
+    cfg = configs.CONFIGS["bunny_640"]
+    scene, cam = _scene(pkg, "bunny_640", pkg.ARITH_EXACT)
+    W, H = cfg["W"], cfg["H"]
+    out = torch.zeros(3 * W * H, dtype=torch.uint8, device="cuda")
+    b12 = np.asarray(cam.basis(W, H), np.float32)[None]
+    with pytest.raises(pkg.CeresError):
+        scene.render_batch_device(b12, np.asarray(cfg["sun"], np.float32)[None], W, H, tiling=pkg.Tiling(8, 0, 4, 1),
+                                  d_rgb8=out.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)

@@ -35,6 +35,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 XGMI_GBS = float(os.environ.get("XGMI_GBS", "76.8"))     # per link and direction
+XSKIP = os.environ.get("XSKIP", "")
 
 
 def main():
@@ -82,7 +83,9 @@ def main():
         # exchange emulation: per step, the receive volume of one rank ((N-1)/N of k frames) copied on a
         # collective stream out of the render's output, then the assembly of its k frames
         recv_bytes = (N - 1) * k * H * 3 * W // N
-        coll = torch.cuda.Stream(device=dev)
+        # XPRIO=1: the collective stream at high priority (measured: C3 at N = 8 0.759 -> 0.711, the
+        # exchange's copies then displace more of the render; default off)
+        coll = torch.cuda.Stream(device=dev, priority=-1 if os.environ.get("XPRIO", "0") == "1" else 0)
         xrecv = [torch.empty(max(recv_bytes, 1), dtype=torch.uint8, device=dev) for _ in range(2)]
         xfull = torch.empty((k, H, 3 * W), dtype=torch.uint8, device=dev)
         xpack = torch.zeros((k * H, 3 * W), dtype=torch.uint8, device=dev)
@@ -133,9 +136,11 @@ def main():
                         done.record(st)
                         coll.wait_event(done)
                         with torch.cuda.stream(coll):
-                            xrecv[q % 2].copy_(srgb[q % S][:recv_bytes])
-                            pkg.assemble_rgb8_packed(xpack.data_ptr(), xfull.data_ptr(), k, W, H, row_block, N,
-                                                     coll.cuda_stream)
+                            if XSKIP != "copy":             # diagnosis: XSKIP=copy|asm drops one part
+                                xrecv[q % 2].copy_(srgb[q % S][:recv_bytes])
+                            if XSKIP != "asm":
+                                pkg.assemble_rgb8_packed(xpack.data_ptr(), xfull.data_ptr(), k, W, H, row_block, N,
+                                                         coll.cuda_stream)
                             ev = torch.cuda.Event()
                             ev.record(coll)
                         copied[q % S] = ev
@@ -163,6 +168,51 @@ def main():
                 torch.cuda.synchronize(dev)
             piped_f.append((time.perf_counter() - t0) * 1e3 / (reps * S // 2))
         del fpx, frgb
+        # --collect bands: rank r renders band (r + f) mod N of every frame f (ceres_tiling.bands: one
+        # launch per <= 64 frames, the band rotating from frame to frame inside the kernel) and the
+        # exchange lands every received band in place in its owner's frame (RCCL point-to-point into
+        # the PPM body slice; distributed.FrameBands): no un-interleave.  Emulated like the exchange
+        # above: the receive volume copied on the collective stream after each step, no assembly.
+        # (Round 6 first tried one launch per band, N per step: 0.807 render-only, 0.73 with the
+        # exchange for C3 at N = 8 -- the small launches' tails.)
+        piped_b, piped_bx = [], []
+        if N > 1:
+            bh = D.band_height(H, N)
+            bb = [torch.empty(F * 3 * W * bh, dtype=torch.uint8, device=dev) for _ in range(S)]
+            bp = [torch.empty(F * 3 * W * bh, dtype=torch.float32, device=dev) for _ in range(S)]
+            xband = torch.empty(max(recv_bytes, 1), dtype=torch.uint8, device=dev)
+            bcopied = [None] * S
+            fbb = 3 * W * bh
+            for r in range(N):
+                def band_step(q, st):
+                    for f0 in range(0, F, 64):
+                        f1 = min(F, f0 + 64)
+                        scene.render_batch_device(b12[f0:f1], s3[f0:f1], W, H, mode=mode,
+                                                  tiling=pkg.Tiling(bh, (r + f0) % N, N, 1),
+                                                  d_pixels=bp[q % S].data_ptr() + 4 * fbb * f0,
+                                                  d_rgb8=bb[q % S].data_ptr() + fbb * f0, stream=st.cuda_stream)
+
+                for exch, sink in ((False, piped_b), (True, piped_bx)):
+                    for it in range(2):                  # warm, then timed
+                        torch.cuda.synchronize(dev)
+                        t0 = time.perf_counter()
+                        for q in range(reps * S // 2):
+                            st = streams[q % S]
+                            if exch and bcopied[q % S] is not None:
+                                st.wait_event(bcopied[q % S])
+                            band_step(q, st)
+                            if exch:
+                                done = torch.cuda.Event()
+                                done.record(st)
+                                coll.wait_event(done)
+                                with torch.cuda.stream(coll):
+                                    xband.copy_(bb[q % S][:recv_bytes])
+                                    ev = torch.cuda.Event()
+                                    ev.record(coll)
+                                bcopied[q % S] = ev
+                        torch.cuda.synchronize(dev)
+                    sink.append((time.perf_counter() - t0) * 1e3 / (reps * S // 2))
+            del bb, bp, xband
         pipe_f_ms = max(piped_f)
         mrays_f = rays / (pipe_f_ms * 1e3)
         if N == 1:
@@ -208,6 +258,12 @@ def main():
                           "frames_partition_rank_ms": [round(x, 5) for x in piped_f],
                           "predicted_mrays_s_frames_partition": round(mrays_f, 1),
                           "predicted_weak_efficiency_frames_partition": round(mrays_f / (N * base_f), 3)}
+        if piped_b:
+            out["by_n"][N].update({
+                "bands_rank_ms": [round(x, 5) for x in piped_b],
+                "predicted_weak_efficiency_bands": round(rays / (max(piped_b) * 1e3) / (N * base_p), 3),
+                "bands_with_exchange_rank_ms": [round(x, 5) for x in piped_bx],
+                "predicted_weak_efficiency_bands_with_exchange": round(rays / (max(piped_bx) * 1e3) / (N * base_p), 3)})
         print(json.dumps({"N": N, **out["by_n"][N]}), file=sys.stderr, flush=True)
     scene.close()
     print(json.dumps(out))
