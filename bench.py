@@ -646,9 +646,11 @@ def main():
                     help="N > 1: skip the timed loop of the other partition (`partition_alt`)")
     ap.add_argument("--no-float", action="store_true", help="skip the float framebuffer (RGB8 only)")
     ap.add_argument("--collect", choices=("auto", "frames", "exchange", "bands", "gather"), default="auto",
-                    help="N > 1: exchange = every frame's rows dealt over the ranks, each frame gathered to one "
-                         "owner rank in one RCCL all-to-all; frames = each rank renders its F/N frames whole (no "
-                         "collective); gather = rows dealt, all frames to rank 0; auto = frames, except exchange "
+                    help="N > 1: bands = every frame cut into N contiguous bands, rank r renders band (r + f) mod N "
+                         "of frame f, each band sent point to point into its owner rank's frame (no un-interleave); "
+                         "exchange = rows dealt in blocks, each frame gathered to one owner rank in one RCCL "
+                         "all-to-all + un-interleave; frames = each rank renders its F/N frames whole (no "
+                         "collective); gather = rows dealt, all frames to rank 0; auto = frames, except bands "
                          "for the tiled C4/C5 at N >= 4 (choose_collect; DESIGN.md \"Multi-GPU\")")
     ap.add_argument("--prime-s", type=float, default=0.3,
                     help="untimed setup: seconds of steps before the W warmup steps (GPU clock ramp)")
