@@ -918,9 +918,13 @@ __device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32
     }
 }
 
+// kBands: the ceres_tiling.bands instantiations (frame f renders band (rank + f) mod world); a
+// separate instantiation, so the row-block kernels carry none of its registers (a runtime flag cost
+// 1 VGPR and 4-6 % of a C3 / C4 / C5 batch, profiles/r06/bands/ab_runtime_flag)
+template <bool kBands = false>
 __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t f, uint32_t lr) {
     if (P.world == 1) return lr;                                      // one rank: local rows are the frame's rows
-    if (P.bands) return ((P.rank + f) % P.world) * P.row_block + lr;  // the frame's band (ceres_tiling.bands)
+    if constexpr (kBands) return ((P.rank + f) % P.world) * P.row_block + lr;   // the frame's band
     return ((lr / P.row_block) * P.world + P.rank) * P.row_block + lr % P.row_block;
 }
 
@@ -1014,7 +1018,7 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     const uint32_t lx = lane & 7, ly = lane >> 3;
     const uint32_t i = blockIdx.x * 16 + (wave & 1) * 8 + lx;
     const uint32_t lr = by * 16 + (wave >> 1) * 8 + ly;
-    const bool active = i < P.W && lr < P.local_rows && (!P.bands || global_row(P, f, lr) < P.H);
+    const bool active = i < P.W && lr < P.local_rows;
     const uint32_t px = (f * P.local_rows + lr) * P.W + i;          // batch pixel (< 2^32, host-checked)
     bool hit = false;
     Hit h{0, 0.f, 0.f, 0.f};
@@ -1309,7 +1313,7 @@ __device__ __forceinline__ bool shadow_packet(const KParams& P, bool hit, const 
 }
 
 // Colour of a pixel with a primary hit, lit or occluded (render.hpp:139-150).
-template <bool kG>
+template <bool kG, bool kBands = false>
 __device__ __forceinline__ void shade_pixel(const KParams& P, uint32_t f, uint32_t lr, uint32_t i, uint32_t pix,
                                             bool blocked, F3 sun_line, uint32_t slot, float hu, float hv,
                                             uint32_t& occluded, float c[3]) {
@@ -1318,7 +1322,7 @@ __device__ __forceinline__ void shade_pixel(const KParams& P, uint32_t f, uint32
     if (blocked) {
         ++occluded;
     } else {
-        const F3 view = primary_dir<kG>(P, f, i, global_row(P, f, lr));
+        const F3 view = primary_dir<kG>(P, f, i, global_row<kBands>(P, f, lr));
         CERES_COUNT_V(kFShadeV, 40);
         shade<kG>(sun_line, P.norms + 9 * size_t(P.orig[slot]), view, hu, hv, c);
     }
@@ -1332,7 +1336,7 @@ __device__ __forceinline__ void shade_pixel(const KParams& P, uint32_t f, uint32
 // launch: the shadow work of early tiles overlaps the primary work of later ones.
 constexpr int kFusedB = 64;      // single-wavefront workgroups (LDS is released per workgroup)
 constexpr size_t kLdsPerCu = 160 * 1024;   // LDS per CU (MI355X_MICROARCH.md)
-template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ, bool kG, int kTPWo = 0>
+template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ, bool kG, int kTPWo = 0, bool kBands = false>
 __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     constexpr int kB = kFusedB;
     // kernels that trace shadow packets keep only the generic per-lane any-hit loop as fallback
@@ -1364,7 +1368,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
         const uint32_t lx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4), ly = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
         i_ = bx_ * 8u + lx;
         lr_ = by_ * 8u + ly;
-        return i_ < P.W && lr_ < P.local_rows && (!P.bands || global_row(P, f_, lr_) < P.H);
+        return i_ < P.W && lr_ < P.local_rows && (!kBands || global_row<true>(P, f_, lr_) < P.H);
     };
     // a pixel's colour: stored now, or (the even tile of a pair) stashed for the odd tile's stores;
     // t_prev: the even tile's order entry (its pixel positions are decoded again, not stashed)
@@ -1440,12 +1444,12 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     if (kStats && P.wave_log) t_start = __builtin_amdgcn_s_memrealtime();   // diagnostic wave timeline (100 MHz)
     // the last tile of this wavefront (a stashed even tile with no odd partner is stored at once)
     const bool last_q = q + 1 == kTPW || (kTPW > 1 && slot_q + 1 >= n_tiles);
-    if (!kStats && P.cull && tile_misses_root(P, f, active, i, global_row(P, f, lr))) {
+    if (!kStats && P.cull && tile_misses_root(P, f, active, i, global_row<kBands>(P, f, lr))) {
         emit(q, last_q, t_prev, active, f, lr, i, 0.f, 0.f, 0.f);       // render.hpp:116-117, every pixel a miss
         continue;
     }
     if (active) {
-        const F3 view = primary_dir<kG>(P, f, i, global_row(P, f, lr));
+        const F3 view = primary_dir<kG>(P, f, i, global_row<kBands>(P, f, lr));
         // kOct -1: the traversal dispatches on a wave-uniform octant; -2: generic loop only
         constexpr int kOctMode = (!kSteal || (CERES_OCTANT_SLAB & 4)) ? -1 : -2;
         hit = guarded_trace<kStats, kB, StkT, kRobust, kOctMode, kG>(P, f3(P.cam[f].eye), view, stk, h, n_pairs,
@@ -1488,7 +1492,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
         L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust, kQ, kPacketsCompiled ? -2 : -1, kG>(
                                     P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
     float col[3] = {0.f, 0.f, 0.f};                                    // a miss: render.hpp:116-117
-    if (hit) shade_pixel<kG>(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded, col);
+    if (hit) shade_pixel<kG, kBands>(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded, col);
     emit(q, last_q, t_prev, active, f, lr, i, col[0], col[1], col[2]);
     if (kStats && P.wave_log) {
         // [start, after primary, end] (100-MHz ticks), longest primary chain, shadow loop trips,
@@ -2071,6 +2075,9 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
         return set_error(CERES_EINVAL, "render: hit records need all three arrays");
     if (qbvh && (robust || (s->flags & CERES_SCENE_STATS)))
         return set_error(CERES_EUNSUPPORTED, "render: CERES_MODE_QBVH4 takes neither CERES_MODE_ROBUST nor a stats scene");
+    if (t.bands && (mode != CERES_MODE_FULL || robust || qbvh || (s->flags & CERES_SCENE_STATS) || d_rec_prim))
+        return set_error(CERES_EUNSUPPORTED, "render: ceres_tiling.bands takes the full mode of a non-stats scene "
+                                             "(not ROBUST, QBVH4, PRIMARY or hit records)");
     HIP_TRY(hipSetDevice(s->device));
     if (qbvh && mode == CERES_MODE_FULL && !s->d_qnodes4)
         if (int rc = build_qnodes4(s)) return rc;
@@ -2123,7 +2130,7 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
                         fbx <= (1u << kTileXBits) && fby <= (1u << kTileYBits);
     // tiles per wavefront of the fused kernel: 1 for the stealing single-frame and the stats
     // kernels; batch_tiles_per_wave for batches (the kernel instantiation must match the order)
-    const uint32_t tpw = (!stats && frames > 1) ? batch_tiles_per_wave(size_t(W) * rows, stack_width(s->n_pairs, s->n_nodes4), qbvh)
+    const uint32_t tpw = (!stats && (frames > 1 || t.bands)) ? batch_tiles_per_wave(size_t(W) * rows, stack_width(s->n_pairs, s->n_nodes4), qbvh)
                                                 : 1u;
     if (full && rows)
         if (int rc = ensure_tile_order(s, W, H, t, rows, frames, fbx, fby, ftile, stream, &tile_order, packed, tpw)) return rc;
@@ -2140,7 +2147,7 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
             const int stw = stack_width(s->n_pairs, s->n_nodes4);
             const bool st16 = stw == 2;
             // work stealing for one-frame launches (latency), one ray per lane for batches (throughput)
-            const bool steal = frames == 1;
+            const bool steal = frames == 1 && !t.bands;            // band launches: the batch kernel
             // BVH4 stack: the batch kernels' walks descend into the first passing child and need
             // only shadow_stack_first entries (order_shadow_bvh4); the stealing loop descends into
             // the nearest child (bunny solo -20 % against first-child order) and needs the
@@ -2215,7 +2222,19 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
                 if (steal) fused_g(rt, std::true_type{});
                 else fused_g(rt, std::false_type{});
             };
-            if (robust) fused_s(std::true_type{});
+            // ceres_tiling.bands: their own instantiations of the batch kernel (kBands)
+            auto fused_bands = [&](auto gt) {
+                constexpr bool G = decltype(gt)::value;
+                if (st16) {
+                    if (tpw == 2) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, CERES_FUSED_MINW16, false, false, false, G, 2, true>), fgrid, fblock, flds, stream, P);
+                    else hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, CERES_FUSED_MINW16, false, false, false, G, 0, true>), fgrid, fblock, flds, stream, P);
+                } else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, false, false, false, G, 0, true>), fgrid, fblock, flds, stream, P);
+                else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, false, false, false, G, 0, true>), fgrid, fblock, flds, stream, P);
+            };
+            if (t.bands) {
+                if (gfma) fused_bands(std::true_type{});
+                else fused_bands(std::false_type{});
+            } else if (robust) fused_s(std::true_type{});
             else fused_s(std::false_type{});
         } else {
             const size_t lds = size_t(s->stack_entries + 1) * dev::kBlock * 4;
