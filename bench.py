@@ -830,10 +830,15 @@ def main():
             # loop runs only if they report no overflow.
             sc_stats = pkg.Scene(mesh, bvh, device=local_rank, stats=True)
             cs = torch.zeros(8, dtype=torch.int64, device=dev)
+            # (band launches have no stats kernels: there the pass deals the same frames' rows in row
+            # blocks -- over the ranks it still traces every ray of the step)
+            st_til = pkg.Tiling(args.row_block, rank, world) if self.tiling.bands else None
+            st_rows = pkg.local_rows(H, st_til) if st_til is not None else self.rows
             for f0 in range(0, self.Fl, MAXF):
                 f1 = min(self.Fl, f0 + MAXF)
-                tmp = torch.empty((f1 - f0) * 3 * W * max(self.rows, 1), dtype=torch.uint8, device=dev)
-                sc_stats.render_batch_device(self.b12[f0:f1], self.s3[f0:f1], W, H, mode=mode, tiling=self.call_tiling(f0),
+                tmp = torch.empty((f1 - f0) * 3 * W * max(st_rows, 1), dtype=torch.uint8, device=dev)
+                sc_stats.render_batch_device(self.b12[f0:f1], self.s3[f0:f1], W, H, mode=mode,
+                                             tiling=st_til if st_til is not None else self.call_tiling(f0),
                                              d_rgb8=tmp.data_ptr(), d_counters=cs.data_ptr(), stream=stream.cuda_stream)
                 torch.cuda.synchronize(dev)
                 if int(cs[6].item()):

@@ -23,4 +23,9 @@ for c in ${SWEEP:-dragon_1080 bunny_640 bunny_1080_primary bunny_1080 dragon_409
   timeout -k 10 600 python bench.py --config $c > $OUT/bench_$c.log 2>&1 || { echo "bench $c failed"; tail -5 $OUT/bench_$c.log; exit 3; }
   grep '^{"metric"' $OUT/bench_$c.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$c', d['value'], d['ms_per_step'], d['roofline']['bound'], d['roofline']['frac'], d['roofline_step']['bound'], d['roofline_step']['frac'], d['parity'].get('all_frames_match_reference'))"
 done
+# the N > 1 path with the band partition: 2 ranks sharing the GPU over gloo (not a scaling number)
+CERES_BENCH_SHARE_GPU=1 CERES_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --collect bands --steps 5 --warmup 2 --no-orbit \
+    --no-roofline --no-cpu-baseline > $OUT/bench_n2_bands.log 2>&1 || { tail -20 $OUT/bench_n2_bands.log; exit 3; }
+grep '^{"metric"' $OUT/bench_n2_bands.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('n2 bands', d['value'], d['config']['collect'], d['parity']['all_frames_match_reference'], d.get('partition_alt',{}).get('collect'))"
 exit 0
