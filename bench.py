@@ -538,7 +538,7 @@ def choose_collect(requested, cfg, world, frames):
     frames are cut into contiguous bands -- rank r renders band (r + f) mod N of frame f -- and each
     band is sent point to point into its owner rank's frame ("bands", the north star's framebuffer
     partition; round 6: no un-interleave, one-GPU rehearsal at N = 8 with the exchange's traffic
-    emulated C3 0.810 / C4 0.746 / C5 0.933 against 0.749 / 0.734 / 0.882 for "exchange", the round-5 row-interleaved
+    emulated C3 0.822 / C4 0.797 / C5 0.933 against 0.754 / 0.737 / 0.882 for "exchange", the round-5 row-interleaved
     blocks + all-to-all + assembly, which stays selectable).  At N = 2 those take "frames" too: the
     single xGMI link would carry 16 split frames' rows per step and outlast the render (C4 1.23x).
     The other partition is timed in the same run and reported beside it (alt_collect).  Partitions

@@ -154,6 +154,7 @@ struct KParams {
     uint32_t W, H;
     uint32_t row_block, rank, world, local_rows; // this rank's rows of every frame (ceres_tiling)
     uint32_t bands;                              // ceres_tiling.bands: frame f renders band (rank + f) % world
+    uint32_t band_magic;                         // ... ceil(2^32 / world): (rank + f) / world = umulhi(rank + f, magic)
     uint32_t row_blocks_per_frame;               // 16-row blocks of local rows per frame (primary grid.y)
     uint32_t stack_entries;
     uint32_t root_leaf_count, root_leaf_first;   // root is a leaf (single_ray_traverser.hpp:72-73)

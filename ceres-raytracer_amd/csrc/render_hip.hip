@@ -924,7 +924,13 @@ __device__ __forceinline__ void store_pixel(const KParams& P, uint32_t f, uint32
 template <bool kBands = false>
 __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t f, uint32_t lr) {
     if (P.world == 1) return lr;                                      // one rank: local rows are the frame's rows
-    if constexpr (kBands) return ((P.rank + f) % P.world) * P.row_block + lr;   // the frame's band
+    if constexpr (kBands) {                                           // the frame's band: (rank + f) mod world
+        // f is wave-uniform: a scalar multiply-high by the host's magic number instead of an
+        // integer division per call (the division cost C4's band launches ~12 % at N = 8, where
+        // most tiles are culled and cheap)
+        const uint32_t x = P.rank + f, q = __umulhi(x, P.band_magic);
+        return (x - q * P.world) * P.row_block + lr;
+    }
     return ((lr / P.row_block) * P.world + P.rank) * P.row_block + lr % P.row_block;
 }
 
@@ -2065,7 +2071,7 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
     if (tiling) t = *tiling;
     if (t.world == 0 || t.rank >= t.world || t.row_block == 0) return set_error(CERES_EINVAL, "render: bad tiling");
     if (t.world == 1) t.bands = 0;
-    if (t.bands && (t.bands != 1 || size_t(t.row_block) * t.world < H))
+    if (t.bands && (t.bands != 1 || t.world > 65535u || size_t(t.row_block) * t.world < H))
         return set_error(CERES_EINVAL, "render: bands of %u rows x %u ranks do not cover %zu rows", t.row_block, t.world, H);
     const size_t rows = local_rows_of(H, t);
     if (size_t(frames) * W * rows > 0xffffffffull) return set_error(CERES_EINVAL, "render: more than 2^32 pixels per batch");
@@ -2093,6 +2099,7 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
     P.W = uint32_t(W); P.H = uint32_t(H);
     P.row_block = t.row_block; P.rank = t.rank; P.world = t.world; P.local_rows = uint32_t(rows);
     P.bands = t.bands;
+    P.band_magic = t.bands ? uint32_t(((uint64_t(1) << 32) + t.world - 1) / t.world) : 0u;   // exact for rank + f < 2^16
     P.row_blocks_per_frame = by;
     P.stack_entries = s->stack_entries;
     P.shadow_stack_entries = s->shadow_stack_entries;
