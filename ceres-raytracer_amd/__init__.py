@@ -57,7 +57,8 @@ EXPORTED_SYMBOLS = (
     "ceres_free", "ceres_scene_create", "ceres_scene_create_device", "ceres_scene_destroy", "ceres_scene_info", "ceres_scene_shadow_stacks", "ceres_render_f32",
     "ceres_render_device", "ceres_render_batch_device", "ceres_render_multi_f32", "ceres_device_count", "ceres_assemble_rgb8_packed", "ceres_render_records", "ceres_tiling_local_rows",
     "ceres_scene_set_timing", "ceres_scene_read_timing", "ceres_scene_wave_log", "ceres_fetch_counters",
-    "ceres_cpu_scene_create", "ceres_cpu_scene_destroy", "ceres_render_cpu_f32",
+    "ceres_cpu_scene_create", "ceres_cpu_scene_destroy", "ceres_render_cpu_f32", "ceres_cpu_scene_create_f64",
+    "ceres_render_cpu_f64",
     "ceres_orbit_cameras", "ceres_assemble_rgb8",
     "ceres_kernel_names", "ceres_last_error", "ceres_version",
     "ceres_obj_load_arith", "ceres_proc_mesh_arith", "ceres_rotate_triangles_arith", "ceres_bvh_build_arith",
@@ -192,6 +193,10 @@ def lib():
     L.ceres_cpu_scene_destroy.argtypes = [_vp]
     L.ceres_cpu_scene_destroy.restype = None
     L.ceres_render_cpu_f32.argtypes = [_vp, _fp, _fp, ctypes.c_int, _fp, ctypes.POINTER(ctypes.c_uint8), _sz, _sz,
+                                       ctypes.POINTER(_Stats), ctypes.c_int]
+    L.ceres_cpu_scene_create_f64.argtypes = [_dp, _sz, _dp, _vp, _sz, _u64p]
+    L.ceres_cpu_scene_create_f64.restype = _vp
+    L.ceres_render_cpu_f64.argtypes = [_vp, _dp, _dp, ctypes.c_int, _dp, ctypes.POINTER(ctypes.c_uint8), _sz, _sz,
                                        ctypes.POINTER(_Stats), ctypes.c_int]
     L.ceres_content_hash.argtypes = [_vp, _sz]
     L.ceres_content_hash.restype = ctypes.c_uint64
@@ -383,11 +388,16 @@ class CpuScene:
     explicitly (./render --cpu); the GPU classes never fall back to it."""
 
     def __init__(self, mesh, bvh):
-        if mesh.f64:
-            raise CeresError("CpuScene: single-precision scenes only")
         L = lib()
-        self._h = L.ceres_cpu_scene_create(_p(mesh.tri, ctypes.c_float), len(mesh), _p(mesh.norm, ctypes.c_float),
-                                           bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0], _p(bvh.prim, ctypes.c_uint64))
+        self.f64 = mesh.f64
+        if self.f64:
+            self._h = L.ceres_cpu_scene_create_f64(_p(mesh.tri, ctypes.c_double), len(mesh), _p(mesh.norm, ctypes.c_double),
+                                                   bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0],
+                                                   _p(bvh.prim, ctypes.c_uint64))
+        else:
+            self._h = L.ceres_cpu_scene_create(_p(mesh.tri, ctypes.c_float), len(mesh), _p(mesh.norm, ctypes.c_float),
+                                               bvh.nodes.ctypes.data_as(_vp), bvh.nodes.shape[0],
+                                               _p(bvh.prim, ctypes.c_uint64))
         if not self._h:
             raise CeresError("ceres_cpu_scene_create: " + L.ceres_last_error().decode())
 
@@ -403,15 +413,16 @@ class CpuScene:
             pass
 
     def render(self, basis12, sun, W, H, mode=MODE_FULL, threads=0, want_pixels=True, want_rgb8=True):
-        """ceres_render_cpu_f32: (pixels [H*W*3] f32 | None, rgb8 | None, stats dict)."""
-        b = np.ascontiguousarray(basis12, np.float32)
-        s = np.ascontiguousarray(sun, np.float32)
-        px = np.empty(3 * W * H, np.float32) if want_pixels else None
+        """ceres_render_cpu_f32 / _f64: (pixels [H*W*3] f32|f64 | None, rgb8 | None, stats dict)."""
+        dt, ct = (np.float64, ctypes.c_double) if self.f64 else (np.float32, ctypes.c_float)
+        b = np.ascontiguousarray(basis12, dt)
+        s = np.ascontiguousarray(sun, dt)
+        px = np.empty(3 * W * H, dt) if want_pixels else None
         rgb = np.empty(3 * W * H, np.uint8) if want_rgb8 else None
         st = _Stats()
-        _check(lib().ceres_render_cpu_f32(self._h, _p(b, ctypes.c_float), _p(s, ctypes.c_float), int(mode),
-                                          _p(px, ctypes.c_float), _p(rgb, ctypes.c_uint8), W, H, ctypes.byref(st),
-                                          int(threads)))
+        fn = lib().ceres_render_cpu_f64 if self.f64 else lib().ceres_render_cpu_f32
+        _check(fn(self._h, _p(b, ct), _p(s, ct), int(mode), _p(px, ct), _p(rgb, ctypes.c_uint8), W, H, ctypes.byref(st),
+                  int(threads)))
         return px, rgb, dict(rays=st.rays, hits=st.hits, primary_rays=st.primary_rays, shadow_rays=st.shadow_rays,
                              node_pairs=st.node_pairs, tri_tests=st.tri_tests, ms=st.ms)
 

@@ -35,8 +35,8 @@
 // the first frame, and once more per further frame; N frames are written as
 // <out-stem>_000.ppm ... (one file when N = 1), "Total Rays" summed like anim.cpp:127.
 //
-// --cpu renders on the host cores instead (ceres_render_cpu_f32: the product's CPU path, the same
-// images, rays and hits; float pipeline, one process; --threads T, default the OpenMP default) --
+// --cpu renders on the host cores instead (ceres_render_cpu_f32 / _f64: the product's CPU path, the
+// same images, rays and hits, float or --double; one process; --threads T, default the OpenMP default) --
 // SURVEY.md §7 step 3's "config 1 works with no GPU".  It is only ever chosen by the flag:
 //
 // Exit status: 0 on success, 1 on a load/render error (message on stderr), 2 on bad usage.
@@ -171,6 +171,13 @@ template <> struct Api<float> {
                             uint8_t* rgb, size_t W, size_t H, ceres_stats* st) {
         return ceres_render_multi_f32(sc, n, rb, b, s, mode, nullptr, rgb, W, H, st);
     }
+    static ceres_cpu_scene* cpu_scene(const float* t, size_t c, const float* n, const Node* nodes, size_t m, const uint64_t* prim) {
+        return ceres_cpu_scene_create(t, c, n, nodes, m, prim);
+    }
+    static int render_cpu(const ceres_cpu_scene* cs, const float* b, const float* s, int mode, uint8_t* rgb, size_t W, size_t H,
+                          ceres_stats* st, int threads) {
+        return ceres_render_cpu_f32(cs, b, s, mode, nullptr, rgb, W, H, st, threads);
+    }
 };
 template <> struct Api<double> {
     using Node = uint64_t;
@@ -197,6 +204,14 @@ template <> struct Api<double> {
         std::fprintf(stderr, "error: --gpus > 1 renders single precision only\n");
         return CERES_EUNSUPPORTED;
     }
+    static ceres_cpu_scene* cpu_scene(const double* t, size_t c, const double* n, const Node* nodes, size_t m,
+                                      const uint64_t* prim) {
+        return ceres_cpu_scene_create_f64(t, c, n, nodes, m, prim);
+    }
+    static int render_cpu(const ceres_cpu_scene* cs, const double* b, const double* s, int mode, uint8_t* rgb, size_t W,
+                          size_t H, ceres_stats* st, int threads) {
+        return ceres_render_cpu_f64(cs, b, s, mode, nullptr, rgb, W, H, st, threads);
+    }
 };
 
 double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
@@ -221,17 +236,15 @@ int run(const Opts& o, const Num<S>& v) {
     std::printf("%g\n", now_s() - t0);
     std::printf("BVH of %zu node(s) and %zu reference(s)\n", n_nodes, n_tri);
 
-    if constexpr (std::is_same<S, float>::value) {
-        if (o.cpu) {
-            ceres_cpu_scene* cs = ceres_cpu_scene_create(tri, n_tri, norm, nodes, n_nodes, prim);
-            ceres_free(nodes); ceres_free(prim); ceres_free(tri); ceres_free(norm);
-            if (!cs) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
-            const int rc = frames_loop(o, v, [&](const S* basis, const S* sun, uint8_t* rgb, ceres_stats* st) {
-                return ceres_render_cpu_f32(cs, basis, sun, o.mode, nullptr, rgb, o.W, o.H, st, o.threads);
-            }, "CPU");
-            ceres_cpu_scene_destroy(cs);
-            return rc;
-        }
+    if (o.cpu) {
+        ceres_cpu_scene* cs = A::cpu_scene(tri, n_tri, norm, nodes, n_nodes, prim);
+        ceres_free(nodes); ceres_free(prim); ceres_free(tri); ceres_free(norm);
+        if (!cs) { std::fprintf(stderr, "error: %s\n", ceres_last_error()); return 1; }
+        const int rc = frames_loop(o, v, [&](const S* basis, const S* sun, uint8_t* rgb, ceres_stats* st) {
+            return A::render_cpu(cs, basis, sun, o.mode, rgb, o.W, o.H, st, o.threads);
+        }, "CPU");
+        ceres_cpu_scene_destroy(cs);
+        return rc;
     }
     ceres_scene* scene = A::scene(tri, n_tri, norm, nodes, n_nodes, prim, o.device);
     // --gpus N: one scene copy per further rank, on the next devices (mod the device count)
@@ -340,8 +353,8 @@ int main(int argc, char** argv) {
     Opts o;
     if (!parse(argc, argv, o)) return usage();
     if (o.arith == CERES_ARITH_FMA) o.mode |= CERES_MODE_FMA;
-    if (o.cpu && (o.f64 || o.gpus > 1 || o.gpu_bvh || (o.mode & CERES_MODE_QBVH4))) {
-        std::fprintf(stderr, "error: --cpu renders the float pipeline in one process (not with --double, --gpus, --gpu-bvh, --qbvh)\n");
+    if (o.cpu && (o.gpus > 1 || o.gpu_bvh || (o.mode & CERES_MODE_QBVH4))) {
+        std::fprintf(stderr, "error: --cpu renders in one process on the host (not with --gpus, --gpu-bvh, --qbvh)\n");
         return 2;
     }
     return o.f64 ? run<double>(o, o.d) : run<float>(o, o.f);

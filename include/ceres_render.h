@@ -357,6 +357,13 @@ ceres_cpu_scene* ceres_cpu_scene_create(const float* tri48, size_t n_tri, const 
 void ceres_cpu_scene_destroy(ceres_cpu_scene* scene);
 int ceres_render_cpu_f32(const ceres_cpu_scene* scene, const float basis12[12], const float sun[3], int mode,
                          float* pixels, uint8_t* rgb8, size_t width, size_t height, ceres_stats* stats, int threads);
+/* render<double> (anim.cpp -d) on host cores: the double arrays of ceres_scene_create_f64, the
+ * reference's mixed precision (double rays and traversal, float shading helpers; render64.hip);
+ * CERES_MODE_ROBUST is float-only (CERES_EUNSUPPORTED). */
+ceres_cpu_scene* ceres_cpu_scene_create_f64(const double* tri96, size_t n_tri, const double* norm72, const void* nodes64,
+                                            size_t n_nodes, const uint64_t* prim64);
+int ceres_render_cpu_f64(const ceres_cpu_scene* scene, const double basis12[12], const double sun[3], int mode,
+                         double* pixels, uint8_t* rgb8, size_t width, size_t height, ceres_stats* stats, int threads);
 
 /* 64-bit content hash of a byte range (multithreaded; deterministic for a given byte string) --
  * what the drop-in include/ceres/render.hpp uses to honour render.hpp:86-156's per-call reading

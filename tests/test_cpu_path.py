@@ -1,10 +1,12 @@
-"""The product's CPU path (ceres_render_cpu_f32, `./render --cpu`; SURVEY.md §7 step 3: "config 1
-works with no GPU") against the reference's own outputs.  No GPU needed: these run in the CPU suite.
+"""The product's CPU path (ceres_render_cpu_f32 / _f64, `./render --cpu [--double]`; SURVEY.md §7
+step 3: "config 1 works with no GPU") against the reference's own outputs.  No GPU needed: these
+run in the CPU suite.
 
-Every golden config (C1-C5 and the edge cases), both arithmetics: the PPM bytes equal the reference
-build's, rays / hits equal render()'s return pair, and the traversal counters equal the reference's
-Statistics (single_ray_traverser.hpp:132-135, primary + shadow) that make_golden.py recorded.  The
-float framebuffer equals the oracle's bit for bit.  The path is chosen only explicitly: the GPU
+Every golden config (C1-C5 and the edge cases; render<double>: every f64 fixture), both
+arithmetics: the PPM bytes equal the reference build's, rays / hits equal render()'s return pair,
+and the traversal counters equal the reference's Statistics (single_ray_traverser.hpp:132-135,
+primary + shadow) that make_golden.py recorded.  The float framebuffer equals the oracle's bit for
+bit.  The path is chosen only explicitly: the GPU
 entry points still fail without a device (test_abi.py)."""
 import hashlib
 import json
@@ -107,7 +109,49 @@ def test_cpu_path_errors(pkg, tmp_path):
     finally:
         sc.close()
     obj = os.path.join(os.path.dirname(__file__), "golden", "tri1.obj")
-    for flags in (["--double"], ["--gpus", "2"], ["--qbvh"], ["--gpu-bvh"]):
+    for flags in (["--gpus", "2"], ["--qbvh"], ["--gpu-bvh"]):
         r = subprocess.run([pkg.CLI_PATH, obj, "--size", "8", "8", "--cpu", "-o", os.devnull] + flags,
                            capture_output=True, text=True)
         assert r.returncode == 2 and "--cpu" in r.stderr, flags
+
+
+F64 = os.path.join(os.path.dirname(__file__), "golden", "f64")
+F64_NAMES = sorted(n[:-5] for n in os.listdir(F64) if n.endswith(".json"))
+
+
+@pytest.mark.parametrize("build", ["ref", "exact"])
+@pytest.mark.parametrize("name", F64_NAMES)
+def test_cli_cpu_double_writes_reference_ppm(pkg, tmp_path, name, build):
+    """./render --cpu --double (anim.cpp -d on the host): every render<double> fixture of the
+    reference (tests/golden/f64, made by oracle/_ref/ref_render_f64{,_exact}) -- PPM bytes, rays,
+    hits and the reference's traversal statistics, both arithmetics."""
+    meta = json.load(open(os.path.join(F64, name + ".json")))
+    data, st, stdout = run_cli(pkg, name, build, tmp_path, ["--double"])
+    check(meta, build, data, st)
+    assert "on the CPU" in stdout
+
+
+def test_cpu_double_scene_api(pkg):
+    """CpuScene over a double mesh: ceres_render_cpu_f64's double framebuffer quantises to the
+    fixture's PPM; a float render call on it (and ROBUST) is refused."""
+    import ctypes
+    name = "bunny_640"
+    meta = json.load(open(os.path.join(F64, name + ".json")))
+    cfg = pkg.configs.CONFIGS[name]
+    mesh, bvh, cam = pkg.prepare(cfg, f64=True, arith=pkg.ARITH_FMA)
+    W, H = cfg["W"], cfg["H"]
+    sc = pkg.CpuScene(mesh, bvh)
+    try:
+        px, rgb, st = sc.render(cam.basis(W, H), np.asarray(cfg["sun"], np.float64), W, H, mode=pkg.cfg_mode(cfg, pkg.ARITH_FMA))
+        assert px.dtype == np.float64
+        assert hashlib.sha256(pkg.ppm(W, H, rgb)).hexdigest() == meta["ppm_sha256"]["ref"]
+        assert (st["rays"], st["hits"]) == (meta["ref"]["rays"], meta["ref"]["hits"])
+        with pytest.raises(pkg.CeresError):
+            sc.render(cam.basis(W, H), np.asarray(cfg["sun"], np.float64), W, H, mode=pkg.MODE_FULL | pkg.MODE_ROBUST)
+        b = np.zeros(12, np.float32)
+        s = np.zeros(3, np.float32)
+        rc = pkg.lib().ceres_render_cpu_f32(sc._h, pkg._p(b, ctypes.c_float), pkg._p(s, ctypes.c_float), 0, None, None, 4, 4,
+                                            None, 0)
+        assert rc != 0
+    finally:
+        sc.close()
