@@ -1069,6 +1069,11 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
 #ifndef CERES_FUSED_MINW16
 #define CERES_FUSED_MINW16 7     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes, batch kernel (with shadow packets, A/A/B/B: 7 waves / 72 VGPRs beat 6 / 80 by 2.6 % on C3, bunny -0.5 %, dragon 4096^2 +-0)
 #endif
+#ifndef CERES_FUSED_MINW16_TPW4
+#define CERES_FUSED_MINW16_TPW4 6   // ... and the 4-tiles-per-wave batch kernel (frames outside 1-4 Mpixel: C1, C4): 6 waves /
+                                    // 80 VGPRs, no spills (round 6 A/B, 16-frame batches x 8 streams: dragon 4096^2 -3.1 %,
+                                    // bunny 640 +-0; profiles/r06/minw_tpw4)
+#endif
 #ifndef CERES_FUSED_MINW16_SOLO
 #define CERES_FUSED_MINW16_SOLO 7  // ... and the work-stealing single-frame kernel (72 VGPRs, no VGPR spill: dragon 4096^2 -4 %, bunny -1.5 %, C3 +-1 %)
 #endif
@@ -2216,7 +2221,8 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
                     if constexpr (!T) {                              // batches: tiles per wave by frame size
                         if (tpw == 2) { hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, R, T, false, G, 2>), fgrid, fblock, flds, stream, P); return; }
                     }
-                    hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16, R, T, false, G>), fgrid, fblock, flds, stream, P);
+                    constexpr int w16b = T ? CERES_FUSED_MINW16_SOLO : CERES_FUSED_MINW16_TPW4;
+                    hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, w16b, R, T, false, G>), fgrid, fblock, flds, stream, P);
                 }
                 else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
                 else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, R, T, false, G>), fgrid, fblock, flds, stream, P);
@@ -2234,7 +2240,7 @@ int launch_chunk(ceres_scene* s, uint32_t frames, const float* basis12, const fl
                 constexpr bool G = decltype(gt)::value;
                 if (st16) {
                     if (tpw == 2) hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, CERES_FUSED_MINW16, false, false, false, G, 2, true>), fgrid, fblock, flds, stream, P);
-                    else hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, CERES_FUSED_MINW16, false, false, false, G, 0, true>), fgrid, fblock, flds, stream, P);
+                    else hipLaunchKernelGGL((dev::ceres_fused<false, uint16_t*, CERES_FUSED_MINW16_TPW4, false, false, false, G, 0, true>), fgrid, fblock, flds, stream, P);
                 } else if (stw == 3) hipLaunchKernelGGL((dev::ceres_fused<false, dev::Stk24, w32, false, false, false, G, 0, true>), fgrid, fblock, flds, stream, P);
                 else hipLaunchKernelGGL((dev::ceres_fused<false, uint32_t*, w32, false, false, false, G, 0, true>), fgrid, fblock, flds, stream, P);
             };
