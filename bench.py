@@ -425,7 +425,7 @@ def step_trace_entry(cfg_name, arith):
         return json.load(f)
 
 
-def roofline_step_block(nbytes, ms_step, world, pmc=None, launches_per_step=None, trace=None):
+def roofline_step_block(nbytes, ms_step, world, pmc=None, launches_per_step=None, trace=None, scene_bytes=None):
     """The timed regime (K steps over --streams streams) priced at its ceilings, per GPU.
 
     Round 6: with the counters of the step's launch (`pmc`, per dispatch)
@@ -448,7 +448,7 @@ def roofline_step_block(nbytes, ms_step, world, pmc=None, launches_per_step=None
         bname, b = max(ceil.items(), key=lambda kv: kv[1]["frac"] or 0.0)
         out.update({"bound": bname, "achieved": b["achieved"], "peak": b["peak"], "unit": b["unit"],
                     "frac": b["frac"], "launches_per_step": launches_per_step, "ceilings": ceil,
-                    "limiter": limiter_text(ceil, pmc, None)})
+                    "limiter": limiter_text(ceil, pmc, scene_bytes)})
     else:
         out.update({"bound": "unmeasured", "frac": None})
     if trace:
@@ -1078,7 +1078,8 @@ def main():
                            rays_step=rays_step, hits_step=hits_step, full_mode=full_mode, row_block=args.row_block,
                            streams=S, float_fb=not args.no_float, arith=args.arith, roofline=roofline,
                            roofline_step=roofline_step_block(bytes_step, T / args.steps * 1e3, world, step_pmc,
-                                                             launches_step, step_trace_entry(args.config, args.arith)),
+                                                             launches_step, step_trace_entry(args.config, args.arith),
+                                                             scene_bytes=scene.info()["device_bytes"]),
                            roofline_solo=roofline_solo, cpu=cpu, parity=parity, alt=alt, orbit=orbit)
         line["native"] = pkg.native_provenance()
         print(json.dumps(line), flush=True)
