@@ -89,7 +89,9 @@
 #define CERES_LOCAL_ORDER 1                    // XCD-local Morton tile order (ensure_tile_order); 0: never
 #endif
 #ifndef CERES_LOCAL_CHUNK_BATCH
-#define CERES_LOCAL_CHUNK_BATCH 64             // tiles per XCD block: frame-major batches ...
+#define CERES_LOCAL_CHUNK_BATCH 128            // tiles per XCD block: frame-major batches (round 6 A/B, 16-frame
+                                               // batches x 8 streams: 64 -> 128 C3 +1.4..1.8 %, dragon 4096^2
+                                               // +1.0..1.6 %, bunny 1080p +0.7 %, C5 +-0; profiles/r06/chunk) ...
 #endif
 #ifndef CERES_XCD_GROUP_TILES
 #define CERES_XCD_GROUP_TILES 16               // centre-first batch orders: runs of this many adjacent tiles of a row on
