@@ -1068,6 +1068,13 @@ __global__ __launch_bounds__(kBlock) void ceres_primary(const KParams P) {
     if (overflow) atomicOr(&P.shards[shard].error, 1u);
 }
 
+#ifndef CERES_LEAN_WRITES
+// 1: the 7-wave batch kernel keeps no per-wavefront scratch spill (a lane's pixel decoded again after
+// the traversals, the culled tiles' zeros made at the store).  Its spill, written once per wavefront
+// and evicted to DRAM, is the C3 launch's write excess over the framebuffers: WRITE_SIZE 619 -> 524 MB
+// per 16-frame launch, but C3 -1.9 %, bunny 1080p -1.9 % (profiles/r06/spill), so off by default
+#define CERES_LEAN_WRITES 0
+#endif
 #ifndef CERES_FUSED_MINW16
 #define CERES_FUSED_MINW16 7     // waves per SIMD the compiler budgets VGPRs for, 16-bit-stack scenes, batch kernel (with shadow packets, A/A/B/B: 7 waves / 72 VGPRs beat 6 / 80 by 2.6 % on C3, bunny -0.5 %, dragon 4096^2 +-0)
 #endif
@@ -1349,6 +1356,14 @@ __device__ __forceinline__ void shade_pixel(const KParams& P, uint32_t f, uint32
 // launch: the shadow work of early tiles overlaps the primary work of later ones.
 constexpr int kFusedB = 64;      // single-wavefront workgroups (LDS is released per workgroup)
 constexpr size_t kLdsPerCu = 160 * 1024;   // LDS per CU (MI355X_MICROARCH.md)
+// 0.f materialised at its use: the compiler otherwise keeps one zero register triple live from the
+// prologue across every loop and, short of VGPRs, spills it to scratch once per wavefront
+__device__ __forceinline__ float fresh_zero() {
+    float z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+
 template <bool kStats, typename StkT, int kMinW, bool kRobust, bool kSteal, bool kQ, bool kG, int kTPWo = 0, bool kBands = false>
 __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))) void ceres_fused(const KParams P) {
     constexpr int kB = kFusedB;
@@ -1448,8 +1463,19 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     const uint4 tp = q - 1 < 4 ? tiles4 : tiles4b;
     const uint32_t t_prev = qp == 0 ? tp.x : qp == 1 ? tp.y : qp == 2 ? tp.z : tp.w;
     uint32_t f, lr, i;
-    const bool active = tile_pixel(t, f, lr, i);
-    const uint32_t px = (f * P.local_rows + lr) * P.W + i;
+    bool active = tile_pixel(t, f, lr, i);
+    uint32_t px = (f * P.local_rows + lr) * P.W + i;
+    // the lane's pixel decoded again from the wave-uniform entry, for uses after a traversal: kept
+    // live across the traversals, lr / i / px were spilled to scratch by the 7-wave batch kernel
+    // (CERES_LEAN_WRITES; the empty asm keeps the compiler from reusing the first decode)
+    auto redecode = [&]() {
+        if constexpr (CERES_LEAN_WRITES) {
+            uint32_t tr = t;
+            asm volatile("" : "+s"(tr));
+            active = tile_pixel(tr, f, lr, i);
+            px = (f * P.local_rows + lr) * P.W + i;
+        }
+    };
     bool hit = false;
     Hit h{0, 0.f, 0.f, 0.f};
     RayWork w{};
@@ -1458,7 +1484,10 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     // the last tile of this wavefront (a stashed even tile with no odd partner is stored at once)
     const bool last_q = q + 1 == kTPW || (kTPW > 1 && slot_q + 1 >= n_tiles);
     if (!kStats && P.cull && tile_misses_root(P, f, active, i, global_row<kBands>(P, f, lr))) {
-        emit(q, last_q, t_prev, active, f, lr, i, 0.f, 0.f, 0.f);       // render.hpp:116-117, every pixel a miss
+        // render.hpp:116-117, every pixel a miss (zeros made here: a zero triple kept from the
+        // prologue was the 7-wave batch kernel's scratch spill)
+        const float z = CERES_LEAN_WRITES ? fresh_zero() : 0.f;
+        emit(q, last_q, t_prev, active, f, lr, i, z, z, z);
         continue;
     }
     if (active) {
@@ -1468,6 +1497,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
         hit = guarded_trace<kStats, kB, StkT, kRobust, kOctMode, kG>(P, f3(P.cam[f].eye), view, stk, h, n_pairs,
                                                                    n_tests, overflow);
         if (P.rec_prim) {
+            redecode();
             P.rec_prim[px] = hit ? int32_t(P.orig[h.slot]) : -1;
             P.rec_tuv[3 * size_t(px)] = hit ? h.t : 0.f;
             P.rec_tuv[3 * size_t(px) + 1] = hit ? h.u : 0.f;
@@ -1504,6 +1534,7 @@ __global__ __launch_bounds__(kFusedB) __attribute__((amdgpu_waves_per_eu(kMinW))
     else
         L.blocked[tid] = hit && trace_any4<kStats, kB, StkT, kRobust, kQ, kPacketsCompiled ? -2 : -1, kG>(
                                     P, w.o, w.d, stk, n_pairs, n_tests, overflow) ? 1u : 0u;
+    redecode();
     float col[3] = {0.f, 0.f, 0.f};                                    // a miss: render.hpp:116-117
     if (hit) shade_pixel<kG, kBands>(P, f, lr, i, px, L.blocked[tid] != 0, w.d, h.slot, h.u, h.v, occluded, col);
     emit(q, last_q, t_prev, active, f, lr, i, col[0], col[1], col[2]);
